@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark of the decoding hot path (contract: see README / DESIGN.md "Measurement").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload minsum-z32|...]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+One step = one decode pass over this rank's batch of synthetic frames that are already resident
+in HBM (all-zero codeword through the on-device QPSK/AWGN channel at a fixed SNR).  Frames shard
+across ranks (weak scaling, no collective on the data path); the BER/FER counters and the timing
+are reduced over ranks once at the end.  Rank 0 prints ONE JSON line.
+
+Workloads (BASELINE.json configs):
+  minsum-z32  cfg3 (default): BG2 Z=32, scaled min-sum alpha 0.75, 10 iterations, B=65536/GPU
+  bp-z4       cfg1 sizes on the GPU: BG2 Z=4, BP, 5 iterations, B=64 (x --batch)
+  gnn-z4      cfg2: BG2 Z=4, MessageGNN 5 layers, H=64, T=4, B=4096, fp32
+  gnn-z32     cfg4 per GPU: BG2 Z=32, MessageGNN 10 layers, H=64, T=32, B=32768/GPU, fp32
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ldpc-neuralnetwork-decoder_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X fp32 matrix (spec), same guide
+
+WORKLOADS = {
+    # name: (decoder, Z, iterations, default batch per GPU, SNR dB)
+    "minsum-z32": ("minsum", 32, 10, 65536, 2.0),
+    "bp-z4": ("bp", 4, 5, 64, 2.0),
+    "gnn-z4": ("gnn", 4, 5, 4096, 2.0),
+    "gnn-z32": ("gnn", 32, 10, 32768, 2.0),
+}
+
+
+def flood_bytes_per_cw(E, N, iters):
+    """every edge message read + written once per iteration (fp32), every APP read
+    + written once per iteration, the LLR read once (4N) and the decision written once (N)."""
+    return iters * 8 * (E + N) + 5 * N
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="minsum-z32", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="frames per GPU (0 = workload default)")
+    ap.add_argument("--snr", type=float, default=None)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
+                    help="target CPU work for the oracle baseline sample (0 disables)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary (profiles/*_pmc.json) to report as roofline.traffic")
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.device("cuda", torch.cuda.current_device())
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def cpu_baseline(workload, z, iters, target_s):
+    """The oracle (oracle/ldpc_oracle.c, single thread, the reference's literal loop order) on a
+    bounded sample of the same workload, timed on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    kind, _, _, _, snr = WORKLOADS[workload]
+    H = oracle.expand(oracle.load_base(os.path.join(ROOT, "codes", f"NR_2_0_{z}.txt")), z)
+    g = oracle.Graph(H)
+    rng = np.random.default_rng(0)
+    s = 10 ** (snr / 10)
+
+    def sample(b):
+        noise = rng.normal(0.0, np.sqrt(1 / (2 * s)), size=(b, g.N))
+        return (2 * s * (1 / np.sqrt(2) + noise)).astype(np.float32)
+
+    if kind == "gnn":
+        return None
+    algo = "minsum" if kind == "minsum" else "bp"
+    b = 4
+    t0 = time.perf_counter()
+    oracle.flood_decode(g, sample(b), algo, iters, 0.75, 0)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    b = int(min(4096, max(8, b * target_s / dt)))
+    x = sample(b)
+    t0 = time.perf_counter()
+    oracle.flood_decode(g, x, algo, iters, 0.75, 0)
+    dt = time.perf_counter() - t0
+    return {"value": b / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
+            "sample": f"{b} frames, BG2 Z={z}, {algo} {iters} it, {snr} dB, oracle/ldpc_oracle.c "
+                      f"single-threaded on {platform.processor() or platform.machine()} "
+                      f"(os.cpu_count()={os.cpu_count()}), {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world, rank, dev = setup_dist()
+    kind, z, iters, bdef, snr = WORKLOADS[a.workload]
+    snr = a.snr if a.snr is not None else snr
+    B = a.batch or bdef
+
+    from ldpc_neural_decoder import _native as N
+    from ldpc_neural_decoder.utils import awgn_llr, expand_base_matrix, load_base_matrix
+
+    base = load_base_matrix(os.path.join(ROOT, "codes", f"NR_2_0_{z}.txt"))
+    H = expand_base_matrix(base, z)
+    n = H.shape[1]
+    llr = awgn_llr(B, n, snr, seed=20251015, frame_offset=rank * B, device=dev)
+    counters = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    if kind in ("minsum", "bp"):
+        from ldpc_neural_decoder.models import BeliefPropagationDecoder, MinSumScaledDecoder
+        dec = (MinSumScaledDecoder(H, iters, 0.75, early_stopping=False) if kind == "minsum"
+               else BeliefPropagationDecoder(H, iters, early_stopping=False))
+        g = dec.graph(dev)
+        bits = torch.empty((B, n), dtype=torch.uint8, device=dev)
+        algo = N.LDPC_ALGO_MINSUM if kind == "minsum" else N.LDPC_ALGO_BP
+        stream = N.stream_ptr(dev)
+
+        def step(count):
+            N.check(N.lib().ldpc_flood_decode(
+                g.handle, algo, N.ptr(llr), B, iters, 0.75, N.LDPC_ES_OFF, N.LDPC_OUT_U8,
+                N.ptr(bits), None, None, N.ptr(counters) if count else None, None, 0, stream))
+
+        dtype = "f32"
+        per_launch_alg = flood_bytes_per_cw(g.E, g.N, iters) * B
+        bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+        dominant = "flood_kernel<minsum>" if kind == "minsum" else "flood_kernel<bp>"
+    else:
+        from ldpc_neural_decoder.models import create_message_gnn_decoder
+        torch.manual_seed(7)
+        gdec, conv = create_message_gnn_decoder(H, num_iterations=iters, hidden_dim=64,
+                                                base_graph=base, Z=z)
+        gdec = gdec.to(dev)
+        types = conv.get_message_types(base, z).to(dev).to(torch.int32)
+        io = conv.message_to_var_index().to(dev).to(torch.int32)
+        probs = torch.empty((B, n), dtype=torch.float32, device=dev)
+        vg, cg = conv.var_groups, conv.check_groups
+
+        def step(count):
+            p = gdec.native_forward(llr, io, types, vg, cg)
+            if count:
+                from ldpc_neural_decoder.utils import count_errors
+                count_errors((p > 0.5).to(torch.uint8), counters=counters)
+
+        dtype = "f32"
+        E = len(conv.messages)
+        per_launch_alg = 12 * 64 * 64 * E * B * iters  # useful MLP FLOPs per forward
+        bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
+        dominant = "gnn forward (all layers)"
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    barrier(world)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record()
+        step(i == a.steps - 1)
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    tot = counters.clone()
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed, kern_ms = t.tolist()
+    be, fe, fr, _ = tot.tolist()
+
+    if rank == 0:
+        total_frames = B * world * a.steps
+        value = total_frames / elapsed
+        achieved = per_launch_alg / (kern_ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
+        traffic = None
+        tj = a.traffic_json
+        if tj and os.path.exists(tj):
+            traffic = json.load(open(tj)).get("bytes_per_launch")
+        cpu = None
+        if world == 1 and a.cpu_baseline_seconds > 0:
+            cpu = cpu_baseline(a.workload, z, iters, a.cpu_baseline_seconds)
+        out = {
+            "metric": "codewords/s at fixed SNR (BG2, %d iters)" % iters,
+            "value": value,
+            "unit": "codewords/s",
+            "coded_bits_per_s": value * n,
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": dtype,
+            "data": f"synthetic: all-zero codeword through the on-device QPSK/AWGN channel at {snr} dB "
+                    f"(Philox seed 20251015, frame offset rank*B), resident in HBM",
+            "config": {"workload": a.workload, "code": f"5G NR BG2 Z={z} (N={n})",
+                       "decoder": kind, "iterations": iters, "batch_per_gpu": B,
+                       "global_batch": B * world, "snr_db": snr, "parallelism": f"dp{world}"},
+            "ber": be / max(fr * n, 1),
+            "fer": fe / max(fr, 1),
+            "roofline": {"bound": bound, "kernel": dominant, "achieved": achieved, "peak": peak,
+                         "unit": unit, "frac": achieved / peak, "traffic": traffic,
+                         "kernel_ms": kern_ms,
+                         "algorithmic_per_launch": per_launch_alg},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

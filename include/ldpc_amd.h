@@ -1,0 +1,149 @@
+/*
+ * ldpc_amd.h -- C ABI of the MI355X-native LDPC decoding library (libldpc_amd.so).
+ *
+ * The reference (BananaFalls/LDPC-NeuralNetwork-Decoder) is pure Python/PyTorch and has no
+ * FFI of its own; its hot-path interface is the set of Python calls listed next to each entry
+ * point below.  The Python package ldpc_neural_decoder (this repo) keeps those Python
+ * signatures and binds these symbols with ctypes.
+ *
+ * Conventions
+ *   - Every pointer named d_* is DEVICE memory owned by the caller (e.g. torch tensors on a HIP
+ *     device, passed as data_ptr()).  Host pointers are named h_*.
+ *   - Work is enqueued on `stream` (a hipStream_t, passed as void*; NULL = the legacy default
+ *     stream) and is asynchronous unless stated otherwise.  No entry point allocates device
+ *     memory on the decode path: scratch is caller-provided (query its size first).
+ *   - Return value: 0 on success, a negative LDPC_E* code on error; the message of the last
+ *     error on the calling thread is available from ldpc_last_error().
+ *   - Layouts follow the reference: LLRs are float32 (B, N) row-major (utils/channel.py:90-154),
+ *     hard decisions are (B, N) row-major, 0/1, either uint8 or float32
+ *     (traditional_decoders.py:101,252 returns float32).
+ */
+#ifndef LDPC_AMD_H
+#define LDPC_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    LDPC_OK = 0,
+    LDPC_EINVAL = -1,       /* bad argument */
+    LDPC_EHIP = -2,         /* HIP runtime error */
+    LDPC_EUNSUPPORTED = -3, /* shape/degree outside what the kernels support */
+    LDPC_ENOMEM = -4
+};
+
+enum { LDPC_ALGO_MINSUM = 0, LDPC_ALGO_BP = 1 };
+enum { LDPC_ES_OFF = 0, LDPC_ES_BATCH = 1, LDPC_ES_FRAME = 2 };
+enum { LDPC_OUT_U8 = 0, LDPC_OUT_F32 = 1 };
+
+typedef struct ldpc_graph ldpc_graph; /* opaque: a Tanner graph resident on one device */
+
+/* Last error message of the calling thread ("" if none). */
+const char *ldpc_last_error(void);
+/* Library version string. */
+const char *ldpc_version(void);
+
+/* ------------------------------------------------------------------ graph (setup, host-sync)
+ * Replaces: the per-decoder Python setup loops
+ *   traditional_decoders.py:26-40 / 161-175  (_precompute_indices over a dense H)
+ *   message_gnn_decoder.py:382-488           (TannerToMessageGraph edge list + groups)
+ * The edge list is check-major (checks ascending, vars ascending inside a check), i.e. the
+ * order of TannerToMessageGraph.messages (message_gnn_decoder.py:397-406).  The library
+ * detects quasi-cyclic structure (largest lifting Z <= 64 that H is block-circulant for) and
+ * builds the per-wave schedules; a non-QC H is handled as Z = 1.
+ * Tables are uploaded to the current HIP device; the call synchronizes. */
+int ldpc_graph_create(int M, int N, int64_t E, const int32_t *h_edge_chk,
+                      const int32_t *h_edge_var, ldpc_graph **out);
+/* Base-graph form: replaces load_base_matrix + expand_base_matrix (ldpc_utils.py:97-147),
+ * h_base is (mb, nb) int32 with -1 for a zero block; shifts are taken modulo z. */
+int ldpc_graph_create_qc(const int32_t *h_base, int mb, int nb, int z, ldpc_graph **out);
+int ldpc_graph_destroy(ldpc_graph *g);
+/* M, N, E, detected lifting Z, max check degree, max variable degree. */
+int ldpc_graph_info(const ldpc_graph *g, int *M, int *N, int64_t *E, int *Z, int *max_dc,
+                    int *max_dv);
+/* Check-major edge list of the graph (E entries each) -- the reference's message order. */
+int ldpc_graph_edges(const ldpc_graph *g, int32_t *h_edge_chk, int32_t *h_edge_var);
+
+/* ------------------------------------------------------------------ flooding BP / min-sum
+ * Replaces: MinSumScaledDecoder.decode  (traditional_decoders.py:177-260, alpha = scaling_factor)
+ *           BeliefPropagationDecoder.decode (traditional_decoders.py:42-109, alpha ignored)
+ * early_stop: LDPC_ES_OFF, LDPC_ES_BATCH (the reference's rule: stop at the first iteration at
+ *   which ALL B frames satisfy H x = 0, traditional_decoders.py:104-107), LDPC_ES_FRAME
+ *   (per-frame freeze at the first valid iteration; no reference counterpart).
+ * d_llr     (B, N) float32
+ * d_bits    (B, N) uint8 or float32 (out_dtype), 0/1, bit = (APP < 0)
+ * d_iters   optional (B,) int32: iterations each frame ran (all equal unless LDPC_ES_FRAME)
+ * d_batch_iters optional int32 scalar: the reference's returned `iterations`
+ * d_counters optional uint64[4] += {bit errors vs the all-zero codeword, frame errors,
+ *   frames, sum of per-frame iterations} -- the all-zero transmit of every reference harness
+ *   (comparative_evaluation.py:133); counting is fused into the decoder's epilogue.
+ * d_work / work_bytes: scratch, at least ldpc_flood_workspace_size(...) bytes. */
+int64_t ldpc_flood_workspace_size(const ldpc_graph *g, int64_t B, int max_iter, int early_stop);
+int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_llr, int64_t B, int max_iter,
+                      float alpha, int early_stop, int out_dtype, void *d_bits, int32_t *d_iters,
+                      int32_t *d_batch_iters, uint64_t *d_counters, void *d_work,
+                      int64_t work_bytes, void *stream);
+
+/* ------------------------------------------------------------------ channel
+ * Replaces: qpsk_modulate -> awgn_channel -> qpsk_demodulate (utils/channel.py:4-154) fused:
+ *   s = 1/sqrt2 - b*sqrt2 (I = even bits, Q = odd bits), n ~ N(0, (1/snr)/2) per component,
+ *   llr = 2*(s+n) / (1/snr), all in float32 as the reference rounds them.
+ * Noise comes from Philox-4x32-10 keyed by `seed`, counter = (frame_offset + b, symbol), so a
+ * frame's LLRs depend only on (seed, its global frame index, snr): ranks of a sharded sweep
+ * draw disjoint streams by passing disjoint frame_offset.
+ * d_bits optional (B, N) uint8 transmitted bits (NULL = the all-zero codeword).
+ * bpsk != 0 selects AWGNChannel.transmit instead (utils/channel.py:193-232). */
+int ldpc_awgn_llr(uint64_t seed, uint64_t frame_offset, float snr_db, const uint8_t *d_bits,
+                  int64_t B, int N, int bpsk, float *d_llr, void *stream);
+/* Raw Philox-4x32-10 stream (for known-answer tests): out[4*i + j] = word j of block
+ * (counter = {i lo, i hi, ctr2, ctr3}, key = seed). */
+int ldpc_philox_raw(uint64_t seed, uint32_t ctr2, uint32_t ctr3, int64_t n_blocks,
+                    uint32_t *d_out, void *stream);
+
+/* ------------------------------------------------------------------ BER / FER
+ * Replaces: compute_ber_fer (utils/channel.py:156-190) as integer counts:
+ * d_counters uint64[3] += {bit errors, frame errors, frames}.  d_ref NULL = all-zero codeword.
+ * bits_dtype: LDPC_OUT_U8 / LDPC_OUT_F32 (a decision is "1" iff the value != 0). */
+int ldpc_count_errors(const void *d_bits, int bits_dtype, const uint8_t *d_ref, int64_t B, int N,
+                      uint64_t *d_counters, void *stream);
+
+/* ------------------------------------------------------------------ message-centred GNN
+ * Replaces: MessageGNNDecoder.forward (message_gnn_decoder.py:190-317) with its
+ *           MessageGNNLayer.forward (:51-129) and decode_messages (:131-152).
+ * The reference aggregates with dense normalized adjacencies D^-1/2 (A+I) D^-1/2 over the
+ * messages that share a variable / a check (:410-469); those are group means.  A plan holds
+ * the two groupings (message -> variable group, message -> check group) and the kernels
+ * compute segment means, O(E*H) instead of the reference's O(E^2*H) bmm.
+ *
+ * Weights: one contiguous float32 blob (H = hidden, T = message types, L = layers):
+ *   w_in[H], b_in[H]                                  input_embedding (Linear(1,H))
+ *   per layer l: emb[T*H]                             message_type_embeddings
+ *                w1v[H*2H] b1v[H] w2v[H*H] b2v[H]     var_to_check_update.{0,2}
+ *                w1c[H*2H] b1c[H] w2c[H*H] b2c[H]     check_to_var_update.{0,2}
+ *                wo[H] bo[1]                          output_projection
+ * (nn.Linear weights as stored: (out, in) row-major; ldpc_gnn_weights_size gives the count.)
+ * d_msg_type (E,) int32 already padded/truncated/clamped to [0,T) (the Python layer does
+ *   :68-81).  d_msg_var (E,) int32 message -> variable for the LLR gather and the output sum
+ *   (the reference's message_to_var_mapping, or its column-0 quirk: :218-229 / :285-295).
+ * precision: 0 = float32 features, fp32 MFMA; 1 = bf16 MLP operands, fp32 accumulate.
+ * d_probs (B, N) float32 = sigmoid(llr + sum of each variable's projected messages).
+ * d_work: at least ldpc_gnn_workspace_size(plan, H, N, B, precision) bytes. */
+typedef struct ldpc_gnn_plan ldpc_gnn_plan;
+int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_vgroup, int n_cgroups,
+                         const int32_t *h_cgroup, ldpc_gnn_plan **out);
+int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p);
+int64_t ldpc_gnn_weights_size(int hidden, int types, int layers);
+int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers,
+                                int precision);
+int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                     const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                     const float *d_llr, int N, int64_t B, int precision, float *d_probs,
+                     void *d_work, int64_t work_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_AMD_H */

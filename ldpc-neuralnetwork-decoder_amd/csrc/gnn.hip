@@ -1,0 +1,508 @@
+// gnn.hip -- message-centred GNN decoder forward for gfx950.
+//
+// Replaces MessageGNNDecoder.forward (message_gnn_decoder.py:190-317):
+//   x0 = Linear(1,H)(llr[msg_var])                                      (:215-235)
+//   per layer i:  c = x + emb_i[type]                                   (:81-90)
+//                 a = A_v c,  b = A_c c   -- group means (the normalized clique adjacencies
+//                                            of :410-469 are exactly segment means)
+//                 y = MLP_v([c;a]) + MLP_c([c;b]),  x <- y (+ x if i > 0)  (:106-127, :261-262)
+//   out_m = output_projection_{L-1}(x_m)                                (:270, :142)
+//   probs = sigmoid(llr + sum_{m -> v} out_m)                           (:273-307)
+//
+// Kernels per layer (no E x E matrix anywhere):
+//   gnn_group_mean_kernel   one wave per (frame, group): mean of c over the group's messages,
+//                           H lanes, 256-B coalesced rows.  Layer 0 builds c from the LLRs.
+//   gnn_mlp_mfma_kernel     H = 64.  Persistent, one 256-thread workgroup per CU holding the
+//                           layer's four weight matrices (96 KB fp32) in LDS; every wave owns a
+//                           32-message tile and runs the four GEMMs on v_mfma_f32_32x32x2_f32 in
+//                           the transposed orientation (hidden units on the MFMA rows, messages
+//                           on the lanes), so GEMM1's accumulator IS GEMM2's B operand with no
+//                           data movement; bias, ReLU, the v+c sum, the residual and (last
+//                           layer) the output projection + per-variable scatter are fused.
+//   gnn_mlp_generic_kernel  any H (VALU); used for H != 64 (e.g. the small-H test fixtures).
+//   gnn_output_kernel       probs = sigmoid(var_sum + llr).
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "common.hpp"
+
+struct ldpc_gnn_plan {
+    int device = 0;
+    int64_t E = 0;
+    int Gv = 0, Gc = 0;
+    int32_t *d_tab = nullptr;  // vgroup[E] cgroup[E] vg_ptr[Gv+1] vg_mem[E] cg_ptr[Gc+1] cg_mem[E]
+    float *d_inv = nullptr;    // 1/|group|: inv_v[Gv] inv_c[Gc]
+    const int32_t *vgroup, *cgroup, *vg_ptr, *vg_mem, *cg_ptr, *cg_mem;
+    const float *inv_v, *inv_c;
+};
+
+namespace ldpc {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMfmaH = 64;
+constexpr int kMlpThreads = 256;
+
+struct GnnLayer {
+    // input features: x_in (B, E, H) or, for layer 0, the embedding of the LLRs
+    const float *x_in;
+    const float *llr;      // (B, N)
+    const int32_t *msg_var;
+    const float *w_in, *b_in;
+    int N;
+    // layer weights (blob section, see ldpc_amd.h)
+    const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
+    int T;
+    const int32_t *msg_type;
+    // plan
+    const int32_t *vgroup, *cgroup, *vg_ptr, *vg_mem, *cg_ptr, *cg_mem;
+    const float *inv_v, *inv_c;
+    int Gv, Gc;
+    int64_t E, B;
+    // group means
+    float *Mv, *Mc;  // (B, Gv, H), (B, Gc, H)
+    // outputs
+    float *x_out;    // (B, E, H), unused on the last layer
+    float *var_sum;  // (B, N), last layer only
+    int residual, last;
+};
+
+// feature u of message m of frame b *before* the type embedding
+__device__ __forceinline__ float x_feat(const GnnLayer &P, int64_t b, int64_t m, int u, int H) {
+    if (P.x_in) return P.x_in[(b * P.E + m) * H + u];
+    const float l = P.llr[b * P.N + P.msg_var[m]];
+    return l * P.w_in[u] + P.b_in[u];  // Linear(1, H)
+}
+
+// ------------------------------------------------------------------------ group means
+__global__ __launch_bounds__(256) void gnn_group_mean_kernel(GnnLayer P, int H) {
+    const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t G = P.Gv + P.Gc;
+    if (wid >= P.B * G) return;
+    const int64_t b = wid / G;
+    const int g = (int)(wid - b * G);
+    const bool isv = g < P.Gv;
+    const int gg = isv ? g : g - P.Gv;
+    const int32_t *ptr = isv ? P.vg_ptr : P.cg_ptr;
+    const int32_t *mem = isv ? P.vg_mem : P.cg_mem;
+    const float inv = isv ? P.inv_v[gg] : P.inv_c[gg];
+    float *dst = (isv ? P.Mv + (b * P.Gv + gg) * H : P.Mc + (b * P.Gc + gg) * H);
+    const int p0 = ptr[gg], p1 = ptr[gg + 1];
+    for (int u = lane; u < H; u += 64) {
+        float s = 0.0f;
+        for (int p = p0; p < p1; ++p) {
+            const int m = mem[p];
+            s += x_feat(P, b, m, u, H) + P.emb[P.msg_type[m] * H + u];
+        }
+        dst[u] = s * inv;
+    }
+}
+
+// ------------------------------------------------------------------------ fused MLP, H = 64
+// LDS image (floats): W1vT[128][64] W2vT[64][64] W1cT[128][64] W2cT[64][64]
+//                     b1v b2v b1c b2c wo [64 each]  emb[T][64]
+constexpr int kW1 = 128 * 64, kW2 = 64 * 64;
+constexpr int kOffW1v = 0, kOffW2v = kW1, kOffW1c = kW1 + kW2, kOffW2c = 2 * kW1 + kW2;
+constexpr int kOffBias = 2 * kW1 + 2 * kW2;  // b1v, b2v, b1c, b2c, wo
+constexpr int kOffEmb = kOffBias + 5 * 64;
+
+__device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+__global__ __launch_bounds__(kMlpThreads, 1) void gnn_mlp_mfma_kernel(GnnLayer P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int H = kMfmaH;
+    const int tid = threadIdx.x;
+    // stage the layer's weights, transposed so lanes read consecutive output units
+    for (int i = tid; i < kW1; i += kMlpThreads) {
+        const int o = i / 128, k = i - o * 128;
+        lds[kOffW1v + k * 64 + o] = P.w1v[i];
+        lds[kOffW1c + k * 64 + o] = P.w1c[i];
+    }
+    for (int i = tid; i < kW2; i += kMlpThreads) {
+        const int o = i / 64, k = i - o * 64;
+        lds[kOffW2v + k * 64 + o] = P.w2v[i];
+        lds[kOffW2c + k * 64 + o] = P.w2c[i];
+    }
+    if (tid < 64) {
+        lds[kOffBias + tid] = P.b1v[tid];
+        lds[kOffBias + 64 + tid] = P.b2v[tid];
+        lds[kOffBias + 128 + tid] = P.b1c[tid];
+        lds[kOffBias + 192 + tid] = P.b2c[tid];
+        lds[kOffBias + 256 + tid] = P.last ? P.wo[tid] : 0.0f;
+    }
+    for (int i = tid; i < P.T * 64; i += kMlpThreads) lds[kOffEmb + i] = P.emb[i];
+    __syncthreads();
+
+    const int lane = tid & 63, j = lane & 31, half = lane >> 5;
+    const int wave = tid >> 6;
+    const int64_t R = P.B * P.E;
+    const int64_t ntiles = (R + 31) / 32;
+    const float bo = P.last ? P.bo[0] : 0.0f;
+    for (int64_t t = (int64_t)blockIdx.x * (kMlpThreads / 64) + wave; t < ntiles;
+         t += (int64_t)gridDim.x * (kMlpThreads / 64)) {
+        const int64_t row = t * 32 + j;
+        const bool ok = row < R;
+        const int64_t rr = ok ? row : R - 1;
+        const int64_t b = rr / P.E, m = rr - b * P.E;
+        // B operands: half 0 lanes carry c (k = 0..63), half 1 lanes carry a, then b (k = 64..127)
+        float in[H];
+        const float4 *grp = nullptr;  // half 1: the group-mean row of the current side
+        if (half == 0) {
+            const int ty = P.msg_type[m];
+            const float *e = lds + kOffEmb + ty * 64;
+            if (P.x_in) {
+                const float4 *xr = reinterpret_cast<const float4 *>(P.x_in + rr * H);
+#pragma unroll
+                for (int q = 0; q < H / 4; ++q) {
+                    const float4 v = xr[q];
+                    in[4 * q + 0] = v.x + e[4 * q + 0];
+                    in[4 * q + 1] = v.y + e[4 * q + 1];
+                    in[4 * q + 2] = v.z + e[4 * q + 2];
+                    in[4 * q + 3] = v.w + e[4 * q + 3];
+                }
+            } else {
+                const float l = P.llr[b * P.N + P.msg_var[m]];
+#pragma unroll
+                for (int u = 0; u < H; ++u) in[u] = (l * P.w_in[u] + P.b_in[u]) + e[u];
+            }
+        } else {
+            grp = reinterpret_cast<const float4 *>(P.Mv + (b * P.Gv + P.vgroup[m]) * H);
+#pragma unroll
+            for (int q = 0; q < H / 4; ++q) {
+                const float4 v = grp[q];
+                in[4 * q + 0] = v.x; in[4 * q + 1] = v.y; in[4 * q + 2] = v.z; in[4 * q + 3] = v.w;
+            }
+            grp = reinterpret_cast<const float4 *>(P.Mc + (b * P.Gc + P.cgroup[m]) * H);
+        }
+        f32x16 y0 = {}, y1 = {};
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            if (side == 1 && half == 1) {
+#pragma unroll
+                for (int q = 0; q < H / 4; ++q) {
+                    const float4 v = grp[q];
+                    in[4 * q + 0] = v.x; in[4 * q + 1] = v.y; in[4 * q + 2] = v.z; in[4 * q + 3] = v.w;
+                }
+            }
+            const float *W1 = lds + (side == 0 ? kOffW1v : kOffW1c);
+            const float *W2 = lds + (side == 0 ? kOffW2v : kOffW2c);
+            const float *b1 = lds + kOffBias + (side == 0 ? 0 : 128);
+            // GEMM1^T: h[u][msg] = sum_k W1[u][k] * in[k][msg], k = half*64 + kk
+            f32x16 h0 = {}, h1 = {};
+#pragma unroll
+            for (int kk = 0; kk < 64; ++kk) {
+                const float *wr = W1 + (half * 64 + kk) * 64;
+                h0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[j], in[kk], h0, 0, 0, 0);
+                h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32 + j], in[kk], h1, 0, 0, 0);
+            }
+            // bias + ReLU; register r of row tile rt holds unit 32*rt + crow(r, half)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                h0[r] = fmaxf(h0[r] + b1[crow(r, half)], 0.0f);
+                h1[r] = fmaxf(h1[r] + b1[32 + crow(r, half)], 0.0f);
+            }
+            // GEMM2^T: y[o][msg] += sum_u W2[o][u] * h[u][msg]; step (rt, r) pairs unit
+            // crow(r,0) (half 0) with crow(r,1) (half 1) -- exactly the registers each lane holds
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float *wa = W2 + (crow(r, half)) * 64;
+                const float *wb = W2 + (32 + crow(r, half)) * 64;
+                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[j], h0[r], y0, 0, 0, 0);
+                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[32 + j], h0[r], y1, 0, 0, 0);
+                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[j], h1[r], y0, 0, 0, 0);
+                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[32 + j], h1[r], y1, 0, 0, 0);
+            }
+        }
+        // epilogue: + b2v + b2c (+ residual); lane holds units 32*ot + crow(r, half) of message j
+        const float *b2v = lds + kOffBias + 64, *b2c = lds + kOffBias + 192, *wo = lds + kOffBias + 256;
+        float part = 0.0f;
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int o0 = 32 * ot + 8 * q + 4 * half;
+                float4 v;
+                float *vv = reinterpret_cast<float *>(&v);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float acc = ot == 0 ? y0[4 * q + i] : y1[4 * q + i];
+                    vv[i] = (acc + b2v[o0 + i]) + b2c[o0 + i];
+                }
+                if (P.residual) {
+                    const float4 xr = *reinterpret_cast<const float4 *>(P.x_in + rr * H + o0);
+                    v.x += xr.x; v.y += xr.y; v.z += xr.z; v.w += xr.w;
+                }
+                if (P.last) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) part += vv[i] * wo[o0 + i];
+                } else if (ok) {
+                    *reinterpret_cast<float4 *>(P.x_out + row * H + o0) = v;
+                }
+            }
+        }
+        if (P.last) {
+            part += __shfl_xor(part, 32, 64);
+            if (ok && half == 0) atomicAdd(&P.var_sum[b * P.N + P.msg_var[m]], part + bo);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------ fused MLP, any H
+// one wave per message, lanes = output units (H <= 64 per pass); VALU fp32.
+__global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H) {
+    extern __shared__ __attribute__((aligned(16))) float sh[];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *in = sh + w * (4 * H);  // [c (H) | a or b (H) | h (H) | spare]
+    const int64_t R = P.B * P.E;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
+        const int64_t b = row / P.E, m = row - b * P.E;
+        const int ty = P.msg_type[m];
+        float y[2] = {0.0f, 0.0f};  // units lane and lane + 64
+        for (int side = 0; side < 2; ++side) {
+            const float *W1 = side ? P.w1c : P.w1v, *b1 = side ? P.b1c : P.b1v;
+            const float *W2 = side ? P.w2c : P.w2v, *b2 = side ? P.b2c : P.b2v;
+            const float *M = side ? P.Mc + (b * P.Gc + P.cgroup[m]) * H : P.Mv + (b * P.Gv + P.vgroup[m]) * H;
+            for (int u = lane; u < H; u += 64) {
+                in[u] = x_feat(P, b, m, u, H) + P.emb[ty * H + u];
+                in[H + u] = M[u];
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int o = lane; o < H; o += 64) {
+                float s = b1[o];
+                for (int k = 0; k < 2 * H; ++k) s += W1[o * 2 * H + k] * in[k];
+                in[2 * H + o] = fmaxf(s, 0.0f);
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int o = lane, i = 0; o < H; o += 64, ++i) {
+                float s = b2[o];
+                for (int u = 0; u < H; ++u) s += W2[o * H + u] * in[2 * H + u];
+                y[i] += s;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        float part = 0.0f;
+        for (int o = lane, i = 0; o < H; o += 64, ++i) {
+            float v = y[i];
+            if (P.residual) v += P.x_in[row * H + o];
+            if (P.last) part += v * P.wo[o];
+            else P.x_out[row * H + o] = v;
+        }
+        if (P.last) {
+            for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+            if (lane == 0) atomicAdd(&P.var_sum[b * P.N + P.msg_var[m]], part + P.bo[0]);
+        }
+    }
+}
+
+__global__ void gnn_output_kernel(const float *__restrict__ var_sum, const float *__restrict__ llr,
+                                  int64_t n, float *__restrict__ probs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const float z = var_sum[i] + llr[i];  // (sum of messages) + input_llr (:298)
+        probs[i] = 1.0f / (1.0f + expf(-z));  // torch.sigmoid (:307)
+    }
+}
+
+int64_t layer_floats(int H, int T) { return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1; }
+
+struct Ws {
+    float *xa, *xb, *Mv, *Mc, *var_sum;
+    int64_t bytes;
+};
+
+Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, void *base) {
+    Ws w{};
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    const int64_t xb = layers > 1 ? al(B * p->E * H * 4) : 0;
+    const int64_t xb2 = layers > 2 ? xb : 0;
+    const int64_t mv = al(B * (int64_t)p->Gv * H * 4), mc = al(B * (int64_t)p->Gc * H * 4);
+    const int64_t vs = al(B * (int64_t)N * 4);
+    char *c = static_cast<char *>(base);
+    w.xa = reinterpret_cast<float *>(c);
+    w.xb = reinterpret_cast<float *>(c + xb);
+    w.Mv = reinterpret_cast<float *>(c + xb + xb2);
+    w.Mc = reinterpret_cast<float *>(c + xb + xb2 + mv);
+    w.var_sum = reinterpret_cast<float *>(c + xb + xb2 + mv + mc);
+    w.bytes = xb + xb2 + mv + mc + vs;
+    return w;
+}
+
+int g_num_cus = 0;
+
+}  // namespace
+}  // namespace ldpc
+
+using namespace ldpc;
+
+extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_vgroup, int n_cgroups,
+                                    const int32_t *h_cgroup, ldpc_gnn_plan **out) {
+    if (!out) return fail(LDPC_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (E <= 0 || n_vgroups <= 0 || n_cgroups <= 0 || !h_vgroup || !h_cgroup)
+        return fail(LDPC_EINVAL, "bad GNN plan arguments");
+    std::vector<int32_t> vptr(n_vgroups + 1, 0), cptr(n_cgroups + 1, 0), vmem(E), cmem(E);
+    for (int64_t m = 0; m < E; ++m) {
+        if (h_vgroup[m] < 0 || h_vgroup[m] >= n_vgroups || h_cgroup[m] < 0 || h_cgroup[m] >= n_cgroups)
+            return fail(LDPC_EINVAL, "group label out of range");
+        vptr[h_vgroup[m] + 1]++;
+        cptr[h_cgroup[m] + 1]++;
+    }
+    for (int g = 0; g < n_vgroups; ++g) vptr[g + 1] += vptr[g];
+    for (int g = 0; g < n_cgroups; ++g) cptr[g + 1] += cptr[g];
+    {
+        std::vector<int32_t> fv(vptr.begin(), vptr.end() - 1), fc(cptr.begin(), cptr.end() - 1);
+        for (int64_t m = 0; m < E; ++m) {  // members in ascending message order
+            vmem[fv[h_vgroup[m]]++] = (int32_t)m;
+            cmem[fc[h_cgroup[m]]++] = (int32_t)m;
+        }
+    }
+    std::vector<float> inv(n_vgroups + n_cgroups);
+    for (int g = 0; g < n_vgroups; ++g) {
+        const int d = vptr[g + 1] - vptr[g];
+        inv[g] = d ? 1.0f / (float)d : 0.0f;
+    }
+    for (int g = 0; g < n_cgroups; ++g) {
+        const int d = cptr[g + 1] - cptr[g];
+        inv[n_vgroups + g] = d ? 1.0f / (float)d : 0.0f;
+    }
+    std::vector<int32_t> blob;
+    blob.insert(blob.end(), h_vgroup, h_vgroup + E);
+    blob.insert(blob.end(), h_cgroup, h_cgroup + E);
+    blob.insert(blob.end(), vptr.begin(), vptr.end());
+    blob.insert(blob.end(), vmem.begin(), vmem.end());
+    blob.insert(blob.end(), cptr.begin(), cptr.end());
+    blob.insert(blob.end(), cmem.begin(), cmem.end());
+    auto *p = new ldpc_gnn_plan();
+    p->E = E;
+    p->Gv = n_vgroups;
+    p->Gc = n_cgroups;
+    hipError_t e1 = hipGetDevice(&p->device);
+    hipError_t e2 = hipMalloc(&p->d_tab, blob.size() * 4);
+    hipError_t e3 = hipMalloc(&p->d_inv, inv.size() * 4);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+        ldpc_gnn_plan_destroy(p);
+        return fail(LDPC_EHIP, "GNN plan allocation failed");
+    }
+    if (hipMemcpy(p->d_tab, blob.data(), blob.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_inv, inv.data(), inv.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        ldpc_gnn_plan_destroy(p);
+        return fail(LDPC_EHIP, "GNN plan upload failed");
+    }
+    p->vgroup = p->d_tab;
+    p->cgroup = p->vgroup + E;
+    p->vg_ptr = p->cgroup + E;
+    p->vg_mem = p->vg_ptr + n_vgroups + 1;
+    p->cg_ptr = p->vg_mem + E;
+    p->cg_mem = p->cg_ptr + n_cgroups + 1;
+    p->inv_v = p->d_inv;
+    p->inv_c = p->d_inv + n_vgroups;
+    *out = p;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p) {
+    if (!p) return LDPC_OK;
+    if (p->d_tab) (void)hipFree(p->d_tab);
+    if (p->d_inv) (void)hipFree(p->d_inv);
+    delete p;
+    return LDPC_OK;
+}
+
+extern "C" int64_t ldpc_gnn_weights_size(int hidden, int types, int layers) {
+    if (hidden <= 0 || types <= 0 || layers <= 0) return fail(LDPC_EINVAL, "bad GNN dimensions");
+    return 2LL * hidden + (int64_t)layers * layer_floats(hidden, types);
+}
+
+extern "C" int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers,
+                                           int precision) {
+    if (!p || hidden <= 0 || N <= 0 || B < 0 || layers <= 0) return fail(LDPC_EINVAL, "bad arguments");
+    (void)precision;
+    return carve(p, hidden, N, B, layers, nullptr).bytes;
+}
+
+extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                                const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                                int64_t B, int precision, float *d_probs, void *d_work, int64_t work_bytes,
+                                void *stream) {
+    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    if (hidden <= 0 || types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
+    if (precision != 0) return fail(LDPC_EUNSUPPORTED, "precision 1 (bf16) not built yet");
+    if (B == 0) return LDPC_OK;
+    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
+    const int H = hidden;
+    Ws w = carve(p, H, N, B, layers, d_work);
+    if (!d_work || work_bytes < w.bytes)
+        return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!g_num_cus) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    LDPC_HIP(hipMemsetAsync(w.var_sum, 0, (size_t)B * N * 4, s));
+    GnnLayer L{};
+    L.llr = d_llr;
+    L.msg_var = d_msg_var;
+    L.w_in = d_weights;
+    L.b_in = d_weights + H;
+    L.N = N;
+    L.T = types;
+    L.msg_type = d_msg_type;
+    L.vgroup = p->vgroup; L.cgroup = p->cgroup;
+    L.vg_ptr = p->vg_ptr; L.vg_mem = p->vg_mem; L.cg_ptr = p->cg_ptr; L.cg_mem = p->cg_mem;
+    L.inv_v = p->inv_v; L.inv_c = p->inv_c;
+    L.Gv = p->Gv; L.Gc = p->Gc;
+    L.E = p->E; L.B = B;
+    L.Mv = w.Mv; L.Mc = w.Mc;
+    const bool mfma = H == kMfmaH;
+    if (!mfma && H > 128) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be 64 (MFMA path) or <= 128");
+    const size_t mfma_lds = (size_t)(kOffEmb + types * 64) * 4;
+    if (mfma && mfma_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
+    if (mfma)
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp_mfma_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mfma_lds));
+    const float *x_in = nullptr;
+    for (int l = 0; l < layers; ++l) {
+        const float *lw = d_weights + 2 * H + (int64_t)l * layer_floats(H, types);
+        L.emb = lw;
+        L.w1v = L.emb + (int64_t)types * H;
+        L.b1v = L.w1v + 2LL * H * H;
+        L.w2v = L.b1v + H;
+        L.b2v = L.w2v + (int64_t)H * H;
+        L.w1c = L.b2v + H;
+        L.b1c = L.w1c + 2LL * H * H;
+        L.w2c = L.b1c + H;
+        L.b2c = L.w2c + (int64_t)H * H;
+        L.wo = L.b2c + H;
+        L.bo = L.wo + H;
+        L.x_in = x_in;
+        L.residual = l > 0;
+        L.last = l == layers - 1;
+        L.x_out = (l % 2 == 0) ? w.xa : w.xb;
+        L.var_sum = w.var_sum;
+        const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
+        hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);
+        LDPC_CHECK_LAUNCH("gnn_group_mean_kernel");
+        if (mfma) {
+            const int64_t tiles = (B * p->E + 31) / 32;
+            const int64_t want = (tiles + kMlpThreads / 64 - 1) / (kMlpThreads / 64);
+            const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus);
+            hipLaunchKernelGGL(gnn_mlp_mfma_kernel, dim3(grid), dim3(kMlpThreads), mfma_lds, s, L);
+            LDPC_CHECK_LAUNCH("gnn_mlp_mfma_kernel");
+        } else {
+            const int64_t want = (B * p->E + 3) / 4;
+            const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus * 8);
+            hipLaunchKernelGGL(gnn_mlp_generic_kernel, dim3(grid), dim3(256), (size_t)16 * H * 4, s, L, H);
+            LDPC_CHECK_LAUNCH("gnn_mlp_generic_kernel");
+        }
+        x_in = L.x_out;
+    }
+    const int64_t n = B * N;
+    hipLaunchKernelGGL(gnn_output_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.var_sum, d_llr, n,
+                       d_probs);
+    LDPC_CHECK_LAUNCH("gnn_output_kernel");
+    return LDPC_OK;
+}

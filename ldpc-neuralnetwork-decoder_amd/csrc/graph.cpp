@@ -1,0 +1,273 @@
+// graph.cpp -- host-side graph construction: QC detection, slot assignment, wave schedules.
+//
+// Replaces: traditional_decoders.py:26-40 / 161-175 and message_gnn_decoder.py:382-488 (the
+// Python M x N loops that build index lists; 18.7 s at Z = 32 in the reference).  Here: O(E)
+// per candidate lifting size, once per code, then one upload.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <thread>
+
+#include "common.hpp"
+#include "graph.hpp"
+
+namespace ldpc {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+const char *last_error() { return g_last_error.c_str(); }
+
+namespace {
+
+// Is H (edge list) block-circulant at lifting z?  Fills blocks (row-major) on success.
+bool try_lift(int M, int N, const std::vector<int32_t> &ec, const std::vector<int32_t> &ev, int z,
+              std::vector<Block> &blocks) {
+    if (M % z || N % z) return false;
+    const int mb = M / z, nb = N / z;
+    std::map<int64_t, std::pair<int, int>> shift_count;  // block -> (shift, count)
+    for (size_t e = 0; e < ec.size(); ++e) {
+        const int r = ec[e] / z, c = ev[e] / z;
+        const int k = ec[e] % z, t = ev[e] % z;
+        const int s = ((t - k) % z + z) % z;
+        const int64_t key = (int64_t)r * nb + c;
+        auto it = shift_count.find(key);
+        if (it == shift_count.end()) {
+            shift_count.emplace(key, std::make_pair(s, 1));
+        } else {
+            if (it->second.first != s) return false;
+            ++it->second.second;
+        }
+    }
+    blocks.clear();
+    for (auto &kv : shift_count) {
+        if (kv.second.second != z) return false;
+        blocks.push_back({(int)(kv.first / nb), (int)(kv.first % nb), kv.second.first});
+    }
+    (void)mb;
+    return true;  // std::map iterates keys ascending = row-major, c ascending
+}
+
+// Longest-processing-time-first assignment of tasks to kWaves waves.
+void schedule(const std::vector<int> &tasks, const std::vector<double> &cost,
+              std::vector<int32_t> &ptr, std::vector<int32_t> &list) {
+    std::vector<int> order(tasks.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return cost[a] > cost[b]; });
+    std::vector<std::vector<int>> per(kWaves);
+    std::vector<double> load(kWaves, 0.0);
+    for (int i : order) {
+        int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        per[w].push_back(tasks[i]);
+        load[w] += cost[i];
+    }
+    ptr.assign(kWaves + 1, 0);
+    list.clear();
+    for (int w = 0; w < kWaves; ++w) {
+        std::sort(per[w].begin(), per[w].end());
+        list.insert(list.end(), per[w].begin(), per[w].end());
+        ptr[w + 1] = (int32_t)list.size();
+    }
+}
+
+int build(ldpc_graph *g) {
+    const int M = g->M, N = g->N;
+    // choose the lifting: every z <= 64 that H is block-circulant for; prefer full lane use
+    // (FG * Z == 64), then the larger z (fewer, longer slots).
+    int best = 1;
+    double best_util = 1.0;  // z = 1 always valid, 64 frames x 1 lane = 100 %
+    std::vector<Block> blocks, cand;
+    try_lift(M, N, g->edge_chk, g->edge_var, 1, blocks);
+    for (int z = 2; z <= 64; ++z) {
+        if (M % z || N % z) continue;
+        if (!try_lift(M, N, g->edge_chk, g->edge_var, z, cand)) continue;
+        const double util = (double)((64 / z) * z) / 64.0;
+        if (util > best_util + 1e-9 || (util > best_util - 1e-9 && z > best)) {
+            best = z;
+            best_util = util;
+            blocks = cand;
+        }
+    }
+    g->Z = best;
+    g->FG = 64 / best;
+    g->Mb = M / best;
+    g->Nb = N / best;
+    g->blocks = blocks;
+    const int Mb = g->Mb, Nb = g->Nb;
+
+    std::vector<int> dv(Nb, 0), dc(Mb, 0);
+    for (auto &b : blocks) { ++dv[b.c]; ++dc[b.r]; }
+    g->max_dc = Mb ? *std::max_element(dc.begin(), dc.end()) : 0;
+    g->max_dv = Nb ? *std::max_element(dv.begin(), dv.end()) : 0;
+
+    // slots: blocks of columns with degree >= 2
+    std::vector<int32_t> slot_of(blocks.size(), -1);
+    int nslots = 0;
+    for (size_t i = 0; i < blocks.size(); ++i)
+        if (dv[blocks[i].c] >= 2) slot_of[i] = nslots++;
+    g->nslots = nslots;
+
+    // row tables
+    std::vector<int32_t> row_ptr(Mb + 1, 0), row_col, row_shift, row_slot;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+        row_col.push_back(blocks[i].c);
+        row_shift.push_back(blocks[i].s);
+        row_slot.push_back(slot_of[i]);
+        row_ptr[blocks[i].r + 1]++;
+    }
+    for (int r = 0; r < Mb; ++r) row_ptr[r + 1] += row_ptr[r];
+
+    // var tasks: columns with degree != 1, blocks in ascending row order
+    std::vector<std::vector<int>> col_blocks(Nb);
+    for (size_t i = 0; i < blocks.size(); ++i) col_blocks[blocks[i].c].push_back((int)i);
+    std::vector<int32_t> vc_ptr(1, 0), vc_col, vc_slot, vc_shift;
+    for (int c = 0; c < Nb; ++c) {
+        if (dv[c] == 1) continue;
+        vc_col.push_back(c);
+        for (int i : col_blocks[c]) {  // blocks were pushed row-major: rows ascending
+            vc_slot.push_back(slot_of[i]);
+            vc_shift.push_back(blocks[i].s);
+        }
+        vc_ptr.push_back((int32_t)vc_slot.size());
+    }
+
+    // schedules (cost in VALU-ish units per lane vector)
+    std::vector<int> rtasks(Mb), vtasks(vc_col.size()), btasks(Nb);
+    std::vector<double> rcost(Mb), vcost(vc_col.size()), bcost(Nb, 1.0);
+    for (int r = 0; r < Mb; ++r) { rtasks[r] = r; rcost[r] = 6.0 * dc[r] + 0.5 * dc[r] * dc[r] + 8; }
+    for (size_t i = 0; i < vc_col.size(); ++i) {
+        const double d = dv[vc_col[i]];
+        vtasks[i] = (int)i;
+        vcost[i] = 0.5 * d * (d + 1) + 4.0 * d + 6;
+    }
+    for (int c = 0; c < Nb; ++c) btasks[c] = c;
+    std::vector<int32_t> cw_ptr, cw_task, vw_ptr, vw_task, bw_ptr, bw_task;
+    schedule(rtasks, rcost, cw_ptr, cw_task);
+    schedule(vtasks, vcost, vw_ptr, vw_task);
+    schedule(btasks, bcost, bw_ptr, bw_task);
+
+    // one int32 blob on the device
+    std::vector<int32_t> blob;
+    auto put = [&](const std::vector<int32_t> &v) {
+        size_t off = blob.size();
+        blob.insert(blob.end(), v.begin(), v.end());
+        blob.push_back(0);  // keep every table non-empty
+        return off;
+    };
+    const size_t o_rp = put(row_ptr), o_rc = put(row_col), o_rs = put(row_shift),
+                 o_rsl = put(row_slot), o_vp = put(vc_ptr), o_vc = put(vc_col),
+                 o_vsl = put(vc_slot), o_vs = put(vc_shift), o_cwp = put(cw_ptr),
+                 o_cwt = put(cw_task), o_vwp = put(vw_ptr), o_vwt = put(vw_task),
+                 o_bwp = put(bw_ptr), o_bwt = put(bw_task);
+    LDPC_HIP(hipGetDevice(&g->device));
+    LDPC_HIP(hipMalloc(&g->d_tab, blob.size() * sizeof(int32_t)));
+    LDPC_HIP(hipMemcpy(g->d_tab, blob.data(), blob.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    FloodTables &t = g->ft;
+    t.row_ptr = g->d_tab + o_rp;
+    t.row_col = g->d_tab + o_rc;
+    t.row_shift = g->d_tab + o_rs;
+    t.row_slot = g->d_tab + o_rsl;
+    t.vc_ptr = g->d_tab + o_vp;
+    t.vc_col = g->d_tab + o_vc;
+    t.vc_slot = g->d_tab + o_vsl;
+    t.vc_shift = g->d_tab + o_vs;
+    t.cw_ptr = g->d_tab + o_cwp;
+    t.cw_task = g->d_tab + o_cwt;
+    t.vw_ptr = g->d_tab + o_vwp;
+    t.vw_task = g->d_tab + o_vwt;
+    t.bw_ptr = g->d_tab + o_bwp;
+    t.bw_task = g->d_tab + o_bwt;
+    t.Z = g->Z;
+    t.FG = g->FG;
+    t.Mb = Mb;
+    t.Nb = Nb;
+    t.N = N;
+    t.nslots = nslots;
+
+    LDPC_HIP(hipDeviceSynchronize());
+    return LDPC_OK;
+}
+
+}  // namespace
+}  // namespace ldpc
+
+using namespace ldpc;
+
+extern "C" const char *ldpc_last_error(void) { return ldpc::last_error(); }
+extern "C" const char *ldpc_version(void) { return "ldpc_amd 0.1.0 (gfx950)"; }
+
+extern "C" int ldpc_graph_create(int M, int N, int64_t E, const int32_t *h_edge_chk,
+                                 const int32_t *h_edge_var, ldpc_graph **out) {
+    if (!out) return fail(LDPC_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (M < 0 || N <= 0 || E < 0 || (E > 0 && (!h_edge_chk || !h_edge_var)))
+        return fail(LDPC_EINVAL, "bad graph dimensions");
+    auto *g = new ldpc_graph();
+    g->M = M;
+    g->N = N;
+    g->E = E;
+    g->edge_chk.assign(h_edge_chk, h_edge_chk + E);
+    g->edge_var.assign(h_edge_var, h_edge_var + E);
+    for (int64_t e = 0; e < E; ++e) {
+        if (g->edge_chk[e] < 0 || g->edge_chk[e] >= M || g->edge_var[e] < 0 || g->edge_var[e] >= N) {
+            delete g;
+            return fail(LDPC_EINVAL, "edge index out of range");
+        }
+        if (e && (g->edge_chk[e] < g->edge_chk[e - 1] ||
+                  (g->edge_chk[e] == g->edge_chk[e - 1] && g->edge_var[e] <= g->edge_var[e - 1]))) {
+            delete g;
+            return fail(LDPC_EINVAL, "edge list must be check-major, strictly ascending, no duplicates");
+        }
+    }
+    int rc = build(g);
+    if (rc != LDPC_OK) {
+        ldpc_graph_destroy(g);
+        return rc;
+    }
+    *out = g;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_graph_create_qc(const int32_t *h_base, int mb, int nb, int z, ldpc_graph **out) {
+    if (!h_base || mb <= 0 || nb <= 0 || z <= 0) return fail(LDPC_EINVAL, "bad base graph");
+    std::vector<int32_t> ec, ev;
+    for (int r = 0; r < mb; ++r)
+        for (int k = 0; k < z; ++k)
+            for (int c = 0; c < nb; ++c) {
+                const int s = h_base[r * nb + c];
+                if (s < 0) continue;
+                ec.push_back(r * z + k);
+                ev.push_back(c * z + (k + s % z) % z);
+            }
+    // inside a check row the vars must ascend: blocks are visited c ascending, and each block
+    // contributes one var in [c*z, (c+1)*z), so the order is already ascending.
+    return ldpc_graph_create(mb * z, nb * z, (int64_t)ec.size(), ec.data(), ev.data(), out);
+}
+
+extern "C" int ldpc_graph_destroy(ldpc_graph *g) {
+    if (!g) return LDPC_OK;
+    if (g->d_tab) (void)hipFree(g->d_tab);
+    delete g;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_graph_info(const ldpc_graph *g, int *M, int *N, int64_t *E, int *Z, int *max_dc,
+                               int *max_dv) {
+    if (!g) return fail(LDPC_EINVAL, "graph is NULL");
+    if (M) *M = g->M;
+    if (N) *N = g->N;
+    if (E) *E = g->E;
+    if (Z) *Z = g->Z;
+    if (max_dc) *max_dc = g->max_dc;
+    if (max_dv) *max_dv = g->max_dv;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_graph_edges(const ldpc_graph *g, int32_t *h_edge_chk, int32_t *h_edge_var) {
+    if (!g) return fail(LDPC_EINVAL, "graph is NULL");
+    if (h_edge_chk) std::memcpy(h_edge_chk, g->edge_chk.data(), g->E * sizeof(int32_t));
+    if (h_edge_var) std::memcpy(h_edge_var, g->edge_var.data(), g->E * sizeof(int32_t));
+    return LDPC_OK;
+}

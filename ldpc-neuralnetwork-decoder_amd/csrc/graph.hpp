@@ -1,0 +1,59 @@
+// graph.hpp -- device-resident Tanner graph, quasi-cyclic layout and per-wave schedules.
+//
+// Replaces the reference's per-call Python index building:
+//   traditional_decoders.py:26-40 / 161-175 (_precompute_indices: check_to_var / var_to_check)
+//   message_gnn_decoder.py:382-488 (TannerToMessageGraph: check-major edge list, groups)
+//
+// Layout (see DESIGN.md "Data layout"):
+//   The graph is lifted: H = [block (r, c) = cyclic shift s of I_Z, or 0].  A non-QC H is the
+//   Z = 1 case.  One wave-wide "lane vector" is FG = 64 / Z frames x Z rows: lane l = f * Z + k.
+//   Every block of a column with degree >= 2 owns one LDS "slot" of 64 floats holding, for each
+//   lane, the message on the edge (check r*Z + k, var c*Z + (k + s) % Z) of frame f.  Slots are
+//   indexed by the CHECK row k, so the check update reads slot[lane] unrotated and the variable
+//   update reads slot[f*Z + (t - s) mod Z] (a permutation inside a Z-lane group: no bank
+//   conflicts).  Degree-1 columns own no slot: their v2c is the channel LLR forever.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <vector>
+
+namespace ldpc {
+
+constexpr int kWaves = 4;        // waves per flood workgroup
+constexpr int kMaxUnroll = 24;   // check/var degrees handled by unrolled register code
+
+// Device view of the flooding tables (all int32, one allocation).  Passed by value.
+struct FloodTables {
+    const int32_t *row_ptr;    // [Mb+1]
+    const int32_t *row_col;    // [nnz] column of each block of the row (ascending)
+    const int32_t *row_shift;  // [nnz]
+    const int32_t *row_slot;   // [nnz] LDS slot, or -1 for a degree-1 column
+    const int32_t *vc_ptr;     // [nvc+1] var tasks: columns with degree != 1
+    const int32_t *vc_col;     // [nvc]
+    const int32_t *vc_slot;    // [nnz_vc] slots of the column's blocks (ascending row)
+    const int32_t *vc_shift;   // [nnz_vc]
+    const int32_t *cw_ptr;     // [kWaves+1] check-phase task list per wave
+    const int32_t *cw_task;    // [Mb]
+    const int32_t *vw_ptr;     // [kWaves+1] var-phase task list per wave
+    const int32_t *vw_task;    // [nvc]
+    const int32_t *bw_ptr;     // [kWaves+1] column list per wave for bit emission
+    const int32_t *bw_task;    // [Nb]
+    int Z, FG, Mb, Nb, N, nslots;
+};
+
+struct Block { int r, c, s; };
+
+}  // namespace ldpc
+
+struct ldpc_graph {
+    int device = 0;
+    int M = 0, N = 0;
+    int64_t E = 0;
+    int Z = 1, Mb = 0, Nb = 0, FG = 64;
+    int max_dc = 0, max_dv = 0;
+    int nslots = 0;
+    std::vector<int32_t> edge_chk, edge_var;   // check-major
+    std::vector<ldpc::Block> blocks;            // row-major (r asc, c asc)
+    int32_t *d_tab = nullptr;
+    ldpc::FloodTables ft{};
+};

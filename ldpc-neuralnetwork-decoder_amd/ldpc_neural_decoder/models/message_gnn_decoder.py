@@ -1,0 +1,338 @@
+"""Message-centred GNN decoder (drop-in for models/message_gnn_decoder.py:15-582 of the reference).
+
+Same classes, constructor arguments, parameter names (so the same state_dict keys and
+saved_models checkpoints) and forward/decode signatures as the reference; the forward pass
+runs in libldpc_amd (csrc/gnn.hip): segment-mean aggregation instead of the dense E x E
+normalized-adjacency bmm, the four message MLPs on fp32 MFMA (bf16 optional), and the
+input embedding, residuals, output projection, per-variable sum and sigmoid fused around them.
+
+Compatibility notes (each mirrors the reference line cited):
+  * a 2-D ``message_to_var_mapping`` uses its column 0 as the variable index (:220-226, :287-292),
+    so the one-hot ``.long()`` mapping of the examples reproduces the reference's output exactly
+    as the reference computes it; a float mapping raises IndexError as torch indexing does.
+  * ``message_types`` None -> all zeros (:240-241); shorter/longer -> zero-pad/truncate (:68-78);
+    values clamped to [0, T-1] (:81).
+  * ``var_to_check_adjacency`` / ``check_to_var_adjacency`` are required (None fails like the
+    reference, :93).  They must be message adjacencies of the kind TannerToMessageGraph builds
+    (normalized cliques of messages sharing a variable / a check, :410-469); the groups are read
+    off the matrix once and verified by probing (A @ r == group-mean(r)).
+  * the unused ``output_layer`` (:188) is kept so state_dicts round-trip.
+  * the forward is inference-only (no autograd through the HIP kernels yet; training backward is
+    SURVEY §8(f) rank 1).  ``ground_truth`` still returns (probs, BCE loss) as in :313-315.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ldpc_neural_decoder import _native as N
+from ldpc_neural_decoder.utils.ldpc_utils import edge_list
+
+
+class MessageGNNLayer(nn.Module):
+    """message_gnn_decoder.py:15-152 (parameters only; the math runs in the HIP kernels)."""
+
+    def __init__(self, num_message_types=1, hidden_dim=64):
+        super().__init__()
+        self.message_type_embeddings = nn.Parameter(torch.randn(num_message_types, hidden_dim))
+        self.var_to_check_update = nn.Sequential(
+            nn.Linear(hidden_dim * 2, hidden_dim), nn.ReLU(), nn.Linear(hidden_dim, hidden_dim))
+        self.check_to_var_update = nn.Sequential(
+            nn.Linear(hidden_dim * 2, hidden_dim), nn.ReLU(), nn.Linear(hidden_dim, hidden_dim))
+        self.output_projection = nn.Linear(hidden_dim, 1)
+
+    def decode_messages(self, message_features):
+        """message_gnn_decoder.py:131-152: project features to one LLR per message."""
+        llr_values = self.output_projection(message_features).squeeze(-1)
+        if llr_values.dim() == 1:
+            llr_values = llr_values.unsqueeze(0)
+        elif llr_values.shape[0] != message_features.shape[0]:
+            llr_values = llr_values.transpose(0, 1)
+        return llr_values
+
+    def flat_weights(self):
+        """This layer's section of the C-ABI weight blob (include/ldpc_amd.h)."""
+        v, c = self.var_to_check_update, self.check_to_var_update
+        parts = [self.message_type_embeddings, v[0].weight, v[0].bias, v[2].weight, v[2].bias,
+                 c[0].weight, c[0].bias, c[2].weight, c[2].bias, self.output_projection.weight,
+                 self.output_projection.bias]
+        return [p.detach().reshape(-1) for p in parts]
+
+
+def _types_for(message_types, E, T, device):
+    """message_gnn_decoder.py:68-81 and :240-241."""
+    if message_types is None:
+        t = torch.zeros(E, dtype=torch.long, device=device)
+    else:
+        t = torch.as_tensor(message_types, device=device).long().reshape(-1)
+        if t.numel() < E:
+            t = torch.cat([t, torch.zeros(E - t.numel(), dtype=torch.long, device=device)])
+        elif t.numel() > E:
+            t = t[:E]
+    return torch.clamp(t, 0, T - 1).to(torch.int32).contiguous()
+
+
+def _io_mapping(mapping, E, N_vars, device):
+    """message_gnn_decoder.py:218-229 / 285-295: the message -> variable index actually used."""
+    m = torch.as_tensor(mapping)
+    if m.dim() > 1:
+        m = m[:, 0]  # the reference's column-0 rule
+    if m.dtype.is_floating_point or m.dtype == torch.bool or m.dtype == torch.uint8:
+        raise IndexError("tensors used as indices must be long, int, byte or bool tensors")
+    m = m.to(device).long()
+    if m.numel() != E:
+        raise RuntimeError(f"message_to_var_mapping selects {m.numel()} values for {E} messages")
+    if m.numel() and (int(m.max()) >= N_vars or int(m.min()) < -N_vars):
+        raise IndexError(f"index out of range for {N_vars} variables")
+    m = torch.where(m < 0, m + N_vars, m)
+    return m.to(torch.int32).contiguous()
+
+
+def _groups_from_adjacency(A, E):
+    """Read the message groups off a normalized clique adjacency (message_gnn_decoder.py:410-469).
+
+    Returns (labels (E,) int64 numpy, number of groups).  The labels are the first nonzero column
+    of every row, renumbered densely; the matrix is then probed with random vectors to check that
+    A @ r equals the group mean of r (the only property the decoder relies on)."""
+    tagged = getattr(A, "_ldpc_groups", None)
+    if tagged is not None:
+        return tagged
+    if A is None:
+        raise AttributeError("'NoneType' object has no attribute 'size'")
+    if A.dim() != 2 or A.shape[0] != E or A.shape[1] != E:
+        raise NotImplementedError(
+            f"adjacency of shape {tuple(A.shape)} for {E} messages: the reference's pad/crop "
+            "resize (message_gnn_decoder.py:93-104) is not supported")
+    dev = A.device  # setup-time structure probe, on whichever device holds the matrix
+    Ad = A.to(torch.float32)
+    nz = Ad != 0
+    first = torch.argmax(nz.to(torch.int8), dim=1)
+    uniq, labels = torch.unique(first, return_inverse=True)
+    n = int(uniq.numel())
+    gen = torch.Generator(device="cpu").manual_seed(1234)
+    for _ in range(2):
+        r = torch.rand(E, generator=gen).to(dev)
+        sums = torch.zeros(n, device=dev).index_add_(0, labels, r)
+        cnt = torch.zeros(n, device=dev).index_add_(0, labels, torch.ones(E, device=dev))
+        want = (sums / cnt)[labels]
+        got = Ad @ r
+        if not torch.allclose(got, want, rtol=1e-4, atol=1e-5):
+            raise NotImplementedError(
+                "adjacency is not a normalized clique adjacency of message groups; only the "
+                "TannerToMessageGraph construction (message_gnn_decoder.py:410-469) is supported")
+    out = (labels.cpu().numpy().astype(np.int64), n)
+    try:
+        A._ldpc_groups = out
+    except Exception:
+        pass
+    return out
+
+
+class MessageGNNDecoder(nn.Module):
+    """message_gnn_decoder.py:155-353."""
+
+    def __init__(self, num_messages, num_iterations=5, hidden_dim=64, num_message_types=1):
+        super().__init__()
+        self.num_messages = num_messages
+        self.num_iterations = num_iterations
+        self.hidden_dim = hidden_dim
+        self.input_embedding = nn.Linear(1, hidden_dim)
+        self.gnn_layers = nn.ModuleList([MessageGNNLayer(num_message_types, hidden_dim)
+                                         for _ in range(num_iterations)])
+        self.output_layer = nn.Linear(hidden_dim, 1)  # unused by forward (:188), kept for state_dicts
+        self.precision = "fp32"  # or "bf16": bf16 MLP operands, fp32 accumulate
+        self._plans = {}
+        self._blob_key = None
+        self._blob = None
+
+    # -------------------------------------------------------------- native plumbing
+    def _weights_blob(self, device):
+        params = [self.input_embedding.weight, self.input_embedding.bias]
+        params += [p for layer in self.gnn_layers for p in layer.parameters()]
+        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+        if key != self._blob_key:
+            parts = [self.input_embedding.weight.detach().reshape(-1),
+                     self.input_embedding.bias.detach().reshape(-1)]
+            for layer in self.gnn_layers:
+                parts += layer.flat_weights()
+            blob = torch.cat([p.to(device, torch.float32) for p in parts]).contiguous()
+            T = self.gnn_layers[0].message_type_embeddings.shape[0]
+            want = N.check(N.lib().ldpc_gnn_weights_size(self.hidden_dim, T, len(self.gnn_layers)))
+            assert blob.numel() == want, (blob.numel(), want)
+            self._blob, self._blob_key = blob, key
+        return self._blob
+
+    def _plan(self, vlab, n_v, clab, n_c, device):
+        key = (str(device), vlab.tobytes(), clab.tobytes())
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = N.NativeGnnPlan(vlab, n_v, clab, n_c, device)
+            self._plans = {key: plan}  # keep one plan; graphs rarely change
+        return plan
+
+    def native_forward(self, llr, io_map, types, vgroups, cgroups, chunk=None):
+        """llr (B, N) on a HIP device; io_map/types (E,) int32; groups = (labels, count)."""
+        dev = llr.device
+        B, Nv = llr.shape
+        T = self.gnn_layers[0].message_type_embeddings.shape[0]
+        L = len(self.gnn_layers)
+        plan = self._plan(vgroups[0], vgroups[1], cgroups[0], cgroups[1], dev)
+        blob = self._weights_blob(dev)
+        prec = 1 if self.precision == "bf16" else 0
+        probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
+        if B == 0:
+            return probs
+        per_frame = N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, self.hidden_dim, Nv, 1, L, prec))
+        budget = int(os.environ.get("LDPC_GNN_WORKSPACE_BYTES", 48 << 30))
+        chunk = chunk or max(1, min(B, budget // max(per_frame, 1)))
+        wsb = N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, self.hidden_dim, Nv, chunk, L, prec))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        for s in range(0, B, chunk):
+            n = min(chunk, B - s)
+            N.check(N.lib().ldpc_gnn_forward(
+                plan.handle, self.hidden_dim, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map),
+                N.ptr(llr[s:s + n]), Nv, n, prec, N.ptr(probs[s:s + n]), N.ptr(ws), wsb,
+                N.stream_ptr(dev)))
+        return probs
+
+    # -------------------------------------------------------------- reference API
+    def forward(self, input_llr, message_to_var_mapping, message_types=None,
+                var_to_check_adjacency=None, check_to_var_adjacency=None, ground_truth=None):
+        """message_gnn_decoder.py:190-317 -> probs (B, N) [, BCE loss]."""
+        home = input_llr.device
+        dev = N.device_of(input_llr)
+        E = self.num_messages
+        vg = _groups_from_adjacency(var_to_check_adjacency, E)
+        cg = _groups_from_adjacency(check_to_var_adjacency, E)
+        llr = input_llr.to(dev, torch.float32).contiguous()
+        io_map = _io_mapping(message_to_var_mapping, E, llr.shape[1], dev)
+        T = self.gnn_layers[0].message_type_embeddings.shape[0]
+        types = _types_for(message_types, E, T, dev)
+        with torch.no_grad():
+            probs = self.native_forward(llr, io_map, types, vg, cg)
+        if home != dev:
+            probs = probs.to(home)
+        if ground_truth is not None:
+            loss = F.binary_cross_entropy(probs, ground_truth.to(probs.device).float())
+            return probs, loss
+        return probs
+
+    def decode(self, input_llr, message_to_var_mapping, message_types=None,
+               var_to_check_adjacency=None, check_to_var_adjacency=None):
+        """message_gnn_decoder.py:319-353: hard decision (probs > 0.5) as float32."""
+        soft_bits = self.forward(input_llr, message_to_var_mapping, message_types,
+                                 var_to_check_adjacency, check_to_var_adjacency)
+        return (soft_bits > 0.5).float()
+
+
+class TannerToMessageGraph:
+    """message_gnn_decoder.py:356-536.  Same attributes; the two dense (E, E) adjacencies and the
+    (E, N) one-hot mapping are built on first access (vectorised) and carry their message groups
+    so the decoder never has to re-derive them."""
+
+    def __init__(self, H):
+        self.H = H
+        self.num_checks, self.num_variables = H.shape
+        self.edge_chk, self.edge_var = edge_list(H)  # check-major (:397-406)
+        self.messages = list(zip(self.edge_var.tolist(), self.edge_chk.tolist()))
+        self.var_to_messages = {i: [] for i in range(self.num_variables)}
+        self.check_to_messages = {i: [] for i in range(self.num_checks)}
+        for idx, (v, c) in enumerate(self.messages):
+            self.var_to_messages[v].append(idx)
+            self.check_to_messages[c].append(idx)
+        self._adj = None
+        self._map = None
+
+    @property
+    def var_groups(self):
+        return self.edge_var.astype(np.int64), self.num_variables
+
+    @property
+    def check_groups(self):
+        return self.edge_chk.astype(np.int64), self.num_checks
+
+    def _build_adjacency(self):
+        E = len(self.messages)
+        dev = self.H.device if torch.is_tensor(self.H) else torch.device("cpu")
+        out = []
+        for lab, groups in ((self.edge_var, self.var_groups), (self.edge_chk, self.check_groups)):
+            lab_t = torch.as_tensor(lab.astype(np.int64))
+            deg = torch.bincount(lab_t).float()
+            A = (lab_t.view(-1, 1) == lab_t.view(1, -1)).float()  # clique incl. self (:426-441 + eye)
+            dis = deg[lab_t].pow(-0.5)
+            A = (dis.view(-1, 1) * A) * dis.view(1, -1)            # D^-1/2 (A+I) D^-1/2 (:449-469)
+            A = A.to(dev)
+            A._ldpc_groups = groups
+            out.append(A)
+        self._adj = tuple(out)
+        assert out[0].shape == (E, E)
+
+    @property
+    def var_to_check_adjacency(self):
+        if self._adj is None:
+            self._build_adjacency()
+        return self._adj[0]
+
+    @property
+    def check_to_var_adjacency(self):
+        if self._adj is None:
+            self._build_adjacency()
+        return self._adj[1]
+
+    @property
+    def message_to_var_mapping(self):
+        """(E, N) float one-hot (:471-488)."""
+        if self._map is None:
+            E = len(self.messages)
+            m = torch.zeros((E, self.num_variables))
+            m[torch.arange(E), torch.as_tensor(self.edge_var.astype(np.int64))] = 1.0
+            self._map = m
+        return self._map
+
+    def message_to_var_index(self):
+        """The 1-D message -> variable index (the mapping form the decoder wants)."""
+        return torch.as_tensor(self.edge_var.astype(np.int64))
+
+    def get_message_types(self, base_graph=None, Z=None):
+        """:490-536: index of the block's shift among the sorted distinct shifts (0 without args)."""
+        E = len(self.messages)
+        if base_graph is None or Z is None:
+            return torch.zeros(E, dtype=torch.long)
+        base = np.asarray(torch.as_tensor(base_graph).cpu(), dtype=np.float64)
+        shifts = sorted({int(s) for s in base.ravel() if s >= 0})
+        idx = {s: i for i, s in enumerate(shifts)}
+        sh = base[self.edge_chk // Z, self.edge_var // Z]
+        return torch.tensor([idx[int(s)] if s >= 0 else 0 for s in sh], dtype=torch.long)
+
+
+def create_message_gnn_decoder(H, num_iterations=5, hidden_dim=64, base_graph=None, Z=None):
+    """message_gnn_decoder.py:539-582 -> (decoder, converter)."""
+    converter = TannerToMessageGraph(H)
+    num_messages = len(converter.messages)
+    if base_graph is not None and Z is not None:
+        base = np.asarray(torch.as_tensor(base_graph).cpu())
+        shifts = {int(s) for s in base.ravel() if s >= 0}
+        num_message_types = len(shifts) if shifts else 1
+    else:
+        num_message_types = 1
+    decoder = MessageGNNDecoder(num_messages=num_messages, num_iterations=num_iterations,
+                                hidden_dim=hidden_dim, num_message_types=num_message_types)
+    return decoder, converter
+
+
+def load_message_gnn_model(model_path, H, device):
+    """run_comparison_all.py:124-143: rebuild a decoder from a saved_models checkpoint
+    ({'model_state_dict', ['num_iterations'], ['hidden_dim']}); loaded with weights_only=True."""
+    checkpoint = torch.load(model_path, map_location="cpu", weights_only=True)
+    num_iterations = checkpoint.get("num_iterations", 5)
+    hidden_dim = checkpoint.get("hidden_dim", 64)
+    sd = checkpoint["model_state_dict"]
+    T = sd["gnn_layers.0.message_type_embeddings"].shape[0]
+    decoder, converter = create_message_gnn_decoder(H, num_iterations=num_iterations,
+                                                    hidden_dim=hidden_dim)
+    if T != 1:
+        decoder = MessageGNNDecoder(len(converter.messages), num_iterations, hidden_dim, T)
+    decoder.load_state_dict(sd)
+    return decoder.to(device), converter

@@ -1,0 +1,189 @@
+"""Python side of the CPU oracle.  TEST INFRASTRUCTURE ONLY — never imported by the product.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+It is pinned against the golden fixtures in tests/golden/ (made by importing the reference
+itself, tests/golden/make_golden.py); see tests/test_oracle_golden.py.
+
+Contents
+  load_base / expand / edge_lists   restate utils/ldpc_utils.py:97-147 and the check-major edge
+                                    order of message_gnn_decoder.py:397-406
+  flood_decode                      ctypes front-end of oracle/ldpc_oracle.c (min-sum / BP,
+                                    traditional_decoders.py:42-134, 177-285)
+  gnn_forward                       torch-fp32 restatement of MessageGNNDecoder.forward
+                                    (message_gnn_decoder.py:51-129, 190-317) with the normalized
+                                    clique adjacency written as a segment mean (the identity
+                                    D^-1/2 (A+I) D^-1/2 = group mean, message_gnn_decoder.py:423-469)
+  message_types                     restates TannerToMessageGraph.get_message_types (MGD:490-536)
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(HERE, "_build", "libldpc_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        _lib.ldpc_oracle_flood_decode.restype = ctypes.c_int
+        _lib.ldpc_oracle_flood_decode.argtypes = [
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P,
+            ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_int, P, P, P]
+        _lib.ldpc_oracle_expand.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+        _lib.ldpc_oracle_syndrome.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P,
+                                              ctypes.c_int64, P]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# --------------------------------------------------------------------------- codes
+def load_base(path):
+    """utils/ldpc_utils.py:127-147: whitespace floats, one row per line."""
+    with open(path) as f:
+        rows = [[float(x) for x in line.split()] for line in f if line.strip()]
+    return np.array(rows, dtype=np.float64)
+
+
+def expand(base, z):
+    """utils/ldpc_utils.py:97-125 via the C restatement -> dense uint8 H (M, N)."""
+    b = np.ascontiguousarray(base, dtype=np.int32)
+    H = np.zeros((b.shape[0] * z, b.shape[1] * z), dtype=np.uint8)
+    lib().ldpc_oracle_expand(_p(b), b.shape[0], b.shape[1], z, _p(H))
+    return H
+
+
+class Graph:
+    """Check-major edge list of a dense H (message_gnn_decoder.py:397-406)."""
+
+    def __init__(self, H):
+        H = np.asarray(H)
+        self.M, self.N = H.shape
+        chk, var = np.nonzero(H == 1)  # row-major nonzero = checks ascending, vars ascending
+        self.edge_chk = chk.astype(np.int32)
+        self.edge_var = var.astype(np.int32)
+        self.E = len(chk)
+        self.chk_ptr = np.zeros(self.M + 1, dtype=np.int32)
+        np.cumsum(np.bincount(chk, minlength=self.M), out=self.chk_ptr[1:])
+        order = np.lexsort((chk, var))  # by var, then ascending check
+        self.var_edge = order.astype(np.int32)
+        self.var_ptr = np.zeros(self.N + 1, dtype=np.int32)
+        np.cumsum(np.bincount(var, minlength=self.N), out=self.var_ptr[1:])
+
+
+def flood_decode(graph, llr, algo, max_iter, alpha=0.75, early_stop=0):
+    """algo 'minsum' | 'bp'.  Returns (bits uint8 (B,N), app f32 (B,N), iterations, iters[B])."""
+    llr = np.ascontiguousarray(llr, dtype=np.float32)
+    B = llr.shape[0]
+    bits = np.zeros((B, graph.N), dtype=np.uint8)
+    app = np.zeros((B, graph.N), dtype=np.float32)
+    iters = np.zeros(B, dtype=np.int32)
+    r = lib().ldpc_oracle_flood_decode(
+        0 if algo == "minsum" else 1, graph.M, graph.N, graph.E, _p(graph.chk_ptr),
+        _p(graph.edge_var), _p(graph.var_ptr), _p(graph.var_edge), _p(llr), B, max_iter,
+        float(alpha), int(early_stop), _p(bits), _p(app), _p(iters))
+    if r < 0:
+        raise MemoryError("oracle allocation failed")
+    return bits, app, r, iters
+
+
+def syndrome_valid(graph, bits):
+    bits = np.ascontiguousarray(bits, dtype=np.uint8)
+    valid = np.zeros(bits.shape[0], dtype=np.uint8)
+    lib().ldpc_oracle_syndrome(graph.M, _p(graph.chk_ptr), _p(graph.edge_var), graph.N,
+                               _p(bits), bits.shape[0], _p(valid))
+    return valid.astype(bool)
+
+
+def message_types(graph, base, z):
+    """TannerToMessageGraph.get_message_types (message_gnn_decoder.py:490-536)."""
+    base = np.asarray(base)
+    shifts = sorted({int(s) for s in base.ravel() if s >= 0})
+    idx = {s: i for i, s in enumerate(shifts)}
+    sh = base[graph.edge_chk // z, graph.edge_var // z]
+    return np.array([idx[int(s)] if s >= 0 else 0 for s in sh], dtype=np.int64)
+
+
+# --------------------------------------------------------------------------- GNN (torch fp32)
+def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, types=None,
+                ground_truth=None):
+    """MessageGNNDecoder.forward restated (message_gnn_decoder.py:190-317).
+
+    sd          state_dict (tensors) in the reference's key schema
+    msg_var_io  (E,) int64 message->variable index used for the LLR gather and the output sum
+                (the reference's `message_to_var_mapping`, 1-D form; MGD:218-229, 285-295)
+    edge_var/edge_chk  the Tanner-graph groups that the normalized adjacencies encode
+    """
+    import torch
+    import torch.nn.functional as F
+
+    llr = torch.as_tensor(llr, dtype=torch.float32)
+    B, E = llr.shape[0], len(edge_var)
+    mv = torch.as_tensor(msg_var_io, dtype=torch.long)
+    ev = torch.as_tensor(edge_var, dtype=torch.long)
+    ec = torch.as_tensor(edge_chk, dtype=torch.long)
+    n_layers = len({k.split(".")[1] for k in sd if k.startswith("gnn_layers.")})
+    x = llr[:, mv].unsqueeze(-1) * sd["input_embedding.weight"][:, 0] + sd["input_embedding.bias"]
+    t = torch.zeros(E, dtype=torch.long) if types is None else torch.as_tensor(types).long()
+    deg_v = torch.bincount(ev, minlength=num_vars).float()
+    deg_c = torch.bincount(ec, minlength=num_checks).float()
+
+    def seg_mean(c, idx, deg, n):
+        s = torch.zeros(B, n, c.shape[-1]).index_add_(1, idx, c)
+        return (s / deg.clamp(min=1).view(1, -1, 1))[:, idx]
+
+    def mlp(p, z):
+        h = torch.relu(z @ sd[p + ".0.weight"].T + sd[p + ".0.bias"])
+        return h @ sd[p + ".2.weight"].T + sd[p + ".2.bias"]
+
+    for i in range(n_layers):
+        p = f"gnn_layers.{i}."
+        emb = sd[p + "message_type_embeddings"]
+        c = x + emb[t.clamp(0, emb.shape[0] - 1)]
+        a = seg_mean(c, ev, deg_v, num_vars)
+        b = seg_mean(c, ec, deg_c, num_checks)
+        y = mlp(p + "var_to_check_update", torch.cat([c, a], 2)) + \
+            mlp(p + "check_to_var_update", torch.cat([c, b], 2))
+        x = y + x if i > 0 else y
+    last = f"gnn_layers.{n_layers - 1}.output_projection."
+    out = (x @ sd[last + "weight"][0]) + sd[last + "bias"][0]
+    var_llrs = torch.zeros(B, num_vars).index_add_(1, mv, out)
+    probs = torch.sigmoid(var_llrs + llr)
+    if ground_truth is not None:
+        return probs, F.binary_cross_entropy(probs, torch.as_tensor(ground_truth).float())
+    return probs
+
+
+# --------------------------------------------------------------------------- Philox-4x32-10
+def philox4x32_10(ctr, key):
+    """Random123 Philox-4x32-10 (Salmon et al., SC'11) on uint32 arrays.
+    ctr: (n, 4) uint32, key: (2,) uint32 -> (n, 4) uint32.  Used to pin the HIP channel RNG."""
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    W0, W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+    c = np.array(ctr, dtype=np.uint32).reshape(-1, 4).copy()
+    k0 = np.full(c.shape[0], key[0], dtype=np.uint32)
+    k1 = np.full(c.shape[0], key[1], dtype=np.uint32)
+    mask = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = M0 * c[:, 0].astype(np.uint64)
+        p1 = M1 * c[:, 2].astype(np.uint64)
+        hi0, lo0 = (p0 >> np.uint64(32)).astype(np.uint32), (p0 & mask).astype(np.uint32)
+        hi1, lo1 = (p1 >> np.uint64(32)).astype(np.uint32), (p1 & mask).astype(np.uint32)
+        c = np.stack([hi1 ^ c[:, 1] ^ k0, lo1, hi0 ^ c[:, 3] ^ k1, lo0], axis=1)
+        k0 = k0 + W0
+        k1 = k1 + W1
+    return c

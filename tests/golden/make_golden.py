@@ -1,0 +1,186 @@
+"""Generate the golden fixtures that pin the oracle (and through it the HIP path).
+
+Run ONCE in the build container, where the reference is importable:
+
+    PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports the reference package (`ldpc_neural_decoder` under /root/reference) and records
+inputs and outputs of the hot-path functions as plain arrays in `tests/golden/*.npz`
+(no pickles, no reference source).  Nothing here runs on the GPU box: the .npz files travel,
+this script does not need to.
+
+What is recorded (SURVEY.md §8c list):
+  codes_z{4,32}.npz      base graph, check-major edge list (TannerToMessageGraph.messages,
+                         MGD:397-406), message types (MGD:490-536), dense-H checksum (LU:97-125)
+  channel_z{Z}.npz       seeded LLRs from qpsk_modulate -> awgn_channel -> qpsk_demodulate
+                         (CH:4-154) for several SNRs
+  minsum_z{Z}.npz        MinSumScaledDecoder.decode bits/iters (TD:177-260), ES off/on, alpha 0.75/0.8
+  bp_z4.npz              BeliefPropagationDecoder.decode bits/iters (TD:42-109), ES off/on
+  gnn_z{Z}.npz           seeded MessageGNNDecoder state_dict + forward probs / loss / decode bits
+                         (MGD:190-353) for the 1-D mapping and the 2-D one-hot `.long()` quirk
+  gnn_z4_ckpt.pt         the same Z=4 model saved in the trainer's checkpoint dict format (TR:344-350)
+"""
+import contextlib
+import io
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("LDPC_REFERENCE", "/root/reference")
+sys.path.insert(0, REF)
+
+from ldpc_neural_decoder.utils.ldpc_utils import load_base_matrix, expand_base_matrix  # noqa: E402
+from ldpc_neural_decoder.utils.channel import (  # noqa: E402
+    qpsk_modulate, awgn_channel, qpsk_demodulate, compute_ber_fer)
+from ldpc_neural_decoder.models.traditional_decoders import (  # noqa: E402
+    BeliefPropagationDecoder, MinSumScaledDecoder)
+from ldpc_neural_decoder.models.message_gnn_decoder import (  # noqa: E402
+    TannerToMessageGraph, create_message_gnn_decoder)
+
+SNRS = [-1.0, 0.0, 2.0, 4.0, 6.0]
+
+
+def code(z):
+    base = load_base_matrix(os.path.join(REF, "5G LDPC CODES", f"NR_2_0_{z}.txt"))
+    H = expand_base_matrix(base, z)
+    return base, H
+
+
+def channel_llrs(batch, n, snr_db, seed):
+    torch.manual_seed(seed)
+    bits = torch.zeros((batch, n))
+    sym = qpsk_modulate(bits)
+    rx = awgn_channel(sym, snr_db)
+    return qpsk_demodulate(rx, snr_db).view(batch, -1)
+
+
+def quiet(fn, *a, **k):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a, **k)
+
+
+def gen_codes_and_channel(z, batch):
+    t0 = time.time()
+    base, H = code(z)
+    conv = TannerToMessageGraph(H)
+    msgs = np.array(conv.messages, dtype=np.int32)  # (E, 2) = (var, check), check-major
+    types = conv.get_message_types(base, z).numpy().astype(np.int32)
+    Hn = H.numpy()
+    np.savez_compressed(
+        os.path.join(HERE, f"codes_z{z}.npz"),
+        base=base.numpy().astype(np.int32), Z=np.int32(z), messages=msgs, message_types=types,
+        H_rows=np.nonzero(Hn)[0].astype(np.int32), H_cols=np.nonzero(Hn)[1].astype(np.int32),
+        H_sum=np.float64(Hn.sum()), H_shape=np.array(Hn.shape, dtype=np.int32),
+        Av_diag=np.diag(conv.var_to_check_adjacency.numpy()).astype(np.float32),
+        Ac_diag=np.diag(conv.check_to_var_adjacency.numpy()).astype(np.float32),
+        Av_rowsum=conv.var_to_check_adjacency.numpy().sum(1).astype(np.float32),
+        Ac_rowsum=conv.check_to_var_adjacency.numpy().sum(1).astype(np.float32),
+    )
+    llrs = np.stack([channel_llrs(batch, H.shape[1], s, 1000 + i).numpy()
+                     for i, s in enumerate(SNRS)])
+    np.savez_compressed(os.path.join(HERE, f"channel_z{z}.npz"), snrs=np.array(SNRS),
+                        seeds=np.arange(1000, 1000 + len(SNRS)), llrs=llrs.astype(np.float32))
+    print(f"codes/channel z={z}: E={len(msgs)} {time.time()-t0:.1f}s", flush=True)
+    return base, H, conv, llrs
+
+
+def gen_traditional(z, H, llrs, iters, algos):
+    out = {}
+    for name, alpha in algos:
+        for es in (False, True):
+            bits_all, it_all = [], []
+            t0 = time.time()
+            for k in range(llrs.shape[0]):
+                x = torch.from_numpy(llrs[k])
+                if name == "bp":
+                    dec = BeliefPropagationDecoder(H, max_iterations=iters, early_stopping=es)
+                else:
+                    dec = MinSumScaledDecoder(H, max_iterations=iters, scaling_factor=alpha,
+                                              early_stopping=es)
+                bits, it = dec.decode(x)
+                bits_all.append(bits.numpy().astype(np.uint8))
+                it_all.append(it)
+            key = f"{name}_a{alpha}_es{int(es)}" if name == "ms" else f"{name}_es{int(es)}"
+            out[key + "_bits"] = np.stack(bits_all)
+            out[key + "_iters"] = np.array(it_all, dtype=np.int32)
+            ber = [compute_ber_fer(torch.zeros_like(torch.from_numpy(b).float()),
+                                   torch.from_numpy(b).float()) for b in bits_all]
+            out[key + "_ber_fer"] = np.array(ber, dtype=np.float64)
+            print(f"  {key} z={z}: iters={it_all} {time.time()-t0:.1f}s", flush=True)
+    return out
+
+
+def gen_gnn(z, base, H, conv, llrs, iters, hidden, seed, batch):
+    torch.manual_seed(seed)
+    dec, conv2 = create_message_gnn_decoder(H, num_iterations=iters, hidden_dim=hidden,
+                                            base_graph=base, Z=z)
+    dec.eval()
+    types = conv.get_message_types(base, z)
+    msg_var = torch.tensor([v for v, _ in conv.messages], dtype=torch.long)
+    x = torch.from_numpy(llrs[2][:batch])  # 2 dB
+    gt = torch.zeros_like(x)
+    gt[:, ::3] = 1.0  # an arbitrary target so the loss is not trivial
+    with torch.no_grad():
+        probs = quiet(dec, x, msg_var, types, conv.var_to_check_adjacency,
+                      conv.check_to_var_adjacency)
+        probs_nt = quiet(dec, x, msg_var, None, conv.var_to_check_adjacency,
+                         conv.check_to_var_adjacency)
+        probs2d = quiet(dec, x, conv.message_to_var_mapping.long(), types,
+                        conv.var_to_check_adjacency, conv.check_to_var_adjacency)
+        probs_l, loss = quiet(dec, x, msg_var, types, conv.var_to_check_adjacency,
+                              conv.check_to_var_adjacency, ground_truth=gt)
+        bits = quiet(dec.decode, x, msg_var, types, conv.var_to_check_adjacency,
+                     conv.check_to_var_adjacency)
+    sd = {("w__" + k): v.detach().numpy().astype(np.float32) for k, v in dec.state_dict().items()}
+    np.savez_compressed(
+        os.path.join(HERE, f"gnn_z{z}.npz"), llr=x.numpy(), ground_truth=gt.numpy(),
+        num_iterations=np.int32(iters), hidden_dim=np.int32(hidden),
+        num_message_types=np.int32(dec.gnn_layers[0].message_type_embeddings.shape[0]),
+        probs=probs.numpy(), probs_no_types=probs_nt.numpy(), probs_2d_quirk=probs2d.numpy(),
+        loss=np.float32(loss.item()), decode_bits=bits.numpy().astype(np.uint8),
+        state_keys=np.array(list(dec.state_dict().keys())), **sd)
+    if z == 4:
+        torch.save({"model_state_dict": dec.state_dict(), "num_iterations": iters,
+                    "hidden_dim": hidden, "train_losses": [1.0], "val_losses": [1.0],
+                    "ber_history": [0.5], "fer_history": [1.0]},
+                   os.path.join(HERE, "gnn_z4_ckpt.pt"))
+    print(f"  gnn z={z}: loss={loss.item():.6f}", flush=True)
+
+
+LOW_SNRS = [-6.0, -5.0, -4.0]
+
+
+def gen_low_snr_z32():
+    """Z=32 decodes cleanly at -1 dB (rate ~1/5); add low-SNR frames with decoding errors so
+    that bit-equality of min-sum decisions is a strong test."""
+    base, H = code(32)
+    llrs = np.stack([channel_llrs(8, H.shape[1], s, 2000 + i).numpy()
+                     for i, s in enumerate(LOW_SNRS)])
+    out = {"snrs": np.array(LOW_SNRS), "llrs": llrs.astype(np.float32)}
+    out.update(gen_traditional(32, H, llrs, 10, [("ms", 0.75)]))
+    np.savez_compressed(os.path.join(HERE, "trad_z32_low.npz"), **out)
+
+
+def main():
+    torch.set_num_threads(8)
+    base4, H4, conv4, llr4 = gen_codes_and_channel(4, 64)
+    np.savez_compressed(os.path.join(HERE, "trad_z4.npz"), **gen_traditional(
+        4, H4, llr4, 5, [("bp", None), ("ms", 0.75), ("ms", 0.8)]))
+    gen_gnn(4, base4, H4, conv4, llr4, iters=5, hidden=64, seed=7, batch=8)
+
+    base32, H32, conv32, llr32 = gen_codes_and_channel(32, 8)
+    np.savez_compressed(os.path.join(HERE, "trad_z32.npz"), **gen_traditional(
+        32, H32, llr32, 10, [("ms", 0.75)]))
+    gen_gnn(32, base32, H32, conv32, llr32, iters=3, hidden=16, seed=11, batch=4)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "low":
+        gen_low_snr_z32()
+    else:
+        main()
+        gen_low_snr_z32()

@@ -1,0 +1,187 @@
+"""HIP min-sum / BP decoder vs the oracle and the reference's golden fixtures (GPU).
+
+Bar: min-sum decisions bit-exact (integer-like work: the reference's float32 operation sequence
+is reproduced); BP decisions within a stated tolerance (the reference's torch-CPU tanh/atanh are
+SLEEF approximations, not correctly rounded -- see DESIGN.md "Parity")."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import code_path, golden
+
+from ldpc_neural_decoder import _native as N
+from ldpc_neural_decoder.models import BeliefPropagationDecoder, MinSumScaledDecoder
+from ldpc_neural_decoder.utils import expand_base_matrix, load_base_matrix
+
+pytestmark = pytest.mark.gpu
+SNRS = [-1.0, 0.0, 2.0, 4.0, 6.0]
+
+
+def H_of(z):
+    return expand_base_matrix(load_base_matrix(code_path(z)), z)
+
+
+@pytest.fixture(scope="module")
+def H4():
+    return H_of(4)
+
+
+@pytest.fixture(scope="module")
+def H32():
+    return H_of(32)
+
+
+def test_lifting_detected(cuda, H4, H32):
+    for H, z in ((H4, 4), (H32, 32)):
+        dec = MinSumScaledDecoder(H, max_iterations=5)
+        g = dec.graph(cuda)
+        assert g.Z == z and g.E == 788 * z // 4 and g.max_dc == 10 and g.max_dv == 23
+
+
+@pytest.mark.parametrize("alpha,key", [(0.75, "ms_a0.75"), (0.8, "ms_a0.8")])
+@pytest.mark.parametrize("es", [False, True])
+def test_minsum_z4_golden_bitexact(cuda, H4, alpha, key, es):
+    t, ch = golden("trad_z4.npz"), golden("channel_z4.npz")
+    dec = MinSumScaledDecoder(H4, max_iterations=5, scaling_factor=alpha, early_stopping=es)
+    for k in range(len(SNRS)):
+        bits, it = dec.decode(torch.from_numpy(ch["llrs"][k]).to(cuda))
+        assert bits.dtype == torch.float32 and bits.shape == (64, 208)
+        assert np.array_equal(bits.cpu().numpy().astype(np.uint8), t[f"{key}_es{int(es)}_bits"][k])
+        assert it == t[f"{key}_es{int(es)}_iters"][k]
+
+
+@pytest.mark.parametrize("es", [False, True])
+def test_minsum_z32_golden_bitexact(cuda, H32, es):
+    dec = MinSumScaledDecoder(H32, max_iterations=10, scaling_factor=0.75, early_stopping=es)
+    for name in ("trad_z32.npz", "trad_z32_low.npz"):
+        t = golden(name)
+        llrs = golden("channel_z32.npz")["llrs"] if name == "trad_z32.npz" else t["llrs"]
+        for k in range(llrs.shape[0]):
+            bits, it = dec.decode(torch.from_numpy(llrs[k]).to(cuda))
+            assert np.array_equal(bits.cpu().numpy().astype(np.uint8),
+                                  t[f"ms_a0.75_es{int(es)}_bits"][k]), (name, k)
+            assert it == t[f"ms_a0.75_es{int(es)}_iters"][k]
+
+
+@pytest.mark.parametrize("es", [False, True])
+def test_bp_z4_golden(cuda, H4, es):
+    """Decisions within tolerance: at most 0.1 % of bits may differ from the reference
+    (tanh/atanh rounding); iteration counts must agree."""
+    t, ch = golden("trad_z4.npz"), golden("channel_z4.npz")
+    dec = BeliefPropagationDecoder(H4, max_iterations=5, early_stopping=es)
+    total = diff = 0
+    for k in range(len(SNRS)):
+        bits, it = dec.decode(torch.from_numpy(ch["llrs"][k]).to(cuda))
+        ref = t[f"bp_es{int(es)}_bits"][k]
+        diff += int((bits.cpu().numpy().astype(np.uint8) != ref).sum())
+        total += ref.size
+        assert it == t[f"bp_es{int(es)}_iters"][k]
+    assert diff <= 1e-3 * total, diff
+
+
+@pytest.mark.parametrize("z,iters", [(4, 5), (32, 10)])
+@pytest.mark.parametrize("algo", ["minsum", "bp"])
+def test_vs_oracle_random_batches(cuda, oracle_mod, z, iters, algo):
+    """Odd batch sizes (tail workgroups), low and high SNR; min-sum exact, BP exact vs the
+    oracle (both evaluate tanh/atanh in double and round)."""
+    H = H_of(z)
+    g = oracle_mod.Graph(H.numpy())
+    rng = np.random.default_rng(z * 7 + iters)
+    for B, snr in ((1, -3.0), (37, 0.0), (129 if z == 4 else 19, 2.0)):
+        llr = (rng.normal(1.0, 1.0, size=(B, H.shape[1])) * (2 * 10 ** (snr / 10))).astype(np.float32)
+        if algo == "minsum":
+            dec = MinSumScaledDecoder(H, max_iterations=iters, early_stopping=False)
+        else:
+            dec = BeliefPropagationDecoder(H, max_iterations=iters, early_stopping=False)
+        bits, _ = dec.decode(torch.from_numpy(llr).to(cuda))
+        ref, _, _, _ = oracle_mod.flood_decode(g, llr, algo, iters, 0.75, 0)
+        got = bits.cpu().numpy().astype(np.uint8)
+        if algo == "minsum":
+            assert np.array_equal(got, ref), (B, snr)
+        else:
+            assert (got != ref).mean() <= 1e-4, (B, snr)
+
+
+def test_per_frame_early_stop(cuda, oracle_mod, H4):
+    llr = golden("channel_z4.npz")["llrs"][3]
+    g = oracle_mod.Graph(H4.numpy())
+    dec = MinSumScaledDecoder(H4, max_iterations=8, early_stopping="frame")
+    bits, it, fi = dec.decode(torch.from_numpy(llr).to(cuda), return_frame_iters=True)
+    rb, _, _, ri = oracle_mod.flood_decode(g, llr, "minsum", 8, 0.75, 2)
+    assert np.array_equal(bits.cpu().numpy().astype(np.uint8), rb)
+    assert np.array_equal(fi.cpu().numpy(), ri)
+    assert it == ri.max()
+
+
+def test_counters_and_u8_output(cuda, H32):
+    llr = torch.from_numpy(golden("trad_z32_low.npz")["llrs"][0]).to(cuda)
+    dec = MinSumScaledDecoder(H32, max_iterations=10, early_stopping=False)
+    cnt = torch.zeros(4, dtype=torch.int64, device=cuda)
+    b8, _ = dec.decode(llr, out_dtype=torch.uint8, counters=cnt)
+    bf, _ = dec.decode(llr)
+    assert b8.dtype == torch.uint8 and torch.equal(b8.float(), bf)
+    be = int(bf.sum().item())
+    fe = int((bf.sum(1) > 0).sum().item())
+    assert cnt.tolist() == [be, fe, llr.shape[0], 10 * llr.shape[0]]
+
+
+def test_generic_code_z1(cuda, oracle_mod):
+    """A non-QC parity-check matrix (lifting Z = 1): Hamming(7,4) and a random sparse code."""
+    Hh = torch.tensor([[1, 1, 0, 1, 1, 0, 0], [1, 0, 1, 1, 0, 1, 0], [0, 1, 1, 1, 0, 0, 1]],
+                      dtype=torch.float32)
+    rng = np.random.default_rng(5)
+    Hr = np.zeros((30, 60), dtype=np.float32)
+    for j in range(60):
+        Hr[rng.choice(30, size=3, replace=False), j] = 1
+    for H in (Hh, torch.from_numpy(Hr)):
+        dec = MinSumScaledDecoder(H, max_iterations=6, early_stopping=False)
+        assert dec.graph(cuda).Z == 1
+        llr = rng.normal(1.5, 2.0, size=(70, H.shape[1])).astype(np.float32)
+        bits, _ = dec.decode(torch.from_numpy(llr).to(cuda))
+        ref, _, _, _ = oracle_mod.flood_decode(oracle_mod.Graph(H.numpy()), llr, "minsum", 6, 0.75, 0)
+        assert np.array_equal(bits.cpu().numpy().astype(np.uint8), ref)
+
+
+def test_special_values(cuda, oracle_mod, H4):
+    """Zeros (torch.sign(0) = 0), infinities and NaN follow the reference's float semantics."""
+    rng = np.random.default_rng(3)
+    llr = rng.normal(0.5, 1.0, size=(16, 208)).astype(np.float32)
+    llr[0, :40] = 0.0
+    llr[1, 5] = np.inf
+    llr[2, 9] = -np.inf
+    llr[3, 11] = np.nan
+    g = oracle_mod.Graph(H4.numpy())
+    dec = MinSumScaledDecoder(H4, max_iterations=4, early_stopping=False)
+    bits, _ = dec.decode(torch.from_numpy(llr).to(cuda))
+    ref, _, _, _ = oracle_mod.flood_decode(g, llr, "minsum", 4, 0.75, 0)
+    assert np.array_equal(bits.cpu().numpy().astype(np.uint8), ref)
+
+
+def test_cpu_input_roundtrip_and_errors(cuda, H4):
+    dec = MinSumScaledDecoder(H4, max_iterations=3, early_stopping=False)
+    llr = torch.randn(5, 208) + 2
+    bits, it = dec.decode(llr)
+    assert bits.device.type == "cpu" and it == 3
+    with pytest.raises(ValueError):
+        dec.decode(torch.randn(5, 207))
+    with pytest.raises(UnboundLocalError):
+        MinSumScaledDecoder(H4, max_iterations=0).decode(llr)
+    empty, _ = dec.decode(torch.zeros(0, 208))
+    assert empty.shape == (0, 208)
+
+
+def test_large_batch_properties(cuda, H32):
+    """Full-size batch (B = 65536, cfg3): at 6 dB every frame decodes to the all-zero codeword
+    (and the counters say so); the decision is independent of the batch it rides in."""
+    from ldpc_neural_decoder.utils import awgn_llr
+    B = 65536
+    llr = awgn_llr(B, 1664, 6.0, seed=11, device=cuda)
+    dec = MinSumScaledDecoder(H32, max_iterations=10, early_stopping=False)
+    cnt = torch.zeros(4, dtype=torch.int64, device=cuda)
+    bits, _ = dec.decode(llr, out_dtype=torch.uint8, counters=cnt)
+    assert cnt.tolist()[:3] == [0, 0, B]
+    low = awgn_llr(B, 1664, -4.0, seed=12, device=cuda)
+    full, _ = dec.decode(low, out_dtype=torch.uint8)
+    part, _ = dec.decode(low[1000:1037].contiguous(), out_dtype=torch.uint8)
+    assert torch.equal(full[1000:1037], part)
+    assert full.sum() > 0

@@ -1,0 +1,100 @@
+"""HIP message-GNN forward vs the reference's golden outputs and the torch-fp32 oracle (GPU).
+
+Tolerance (floating point, stated): |probs - ref| <= 2e-5 absolute for the fp32 path.  The
+reference aggregates with a dense normalized-adjacency bmm and MKL GEMMs, this build with
+segment means and fp32 MFMA (exact fp32 products, different summation order), so results agree
+to float32 rounding, not bitwise."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import code_path, golden
+
+from ldpc_neural_decoder.models import MessageGNNDecoder, create_message_gnn_decoder
+from ldpc_neural_decoder.utils import expand_base_matrix, load_base_matrix
+
+pytestmark = pytest.mark.gpu
+TOL = 2e-5
+
+
+def load_model(z):
+    f = golden(f"gnn_z{z}.npz")
+    base = load_base_matrix(code_path(z))
+    H = expand_base_matrix(base, z)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=int(f["num_iterations"]),
+                                           hidden_dim=int(f["hidden_dim"]), base_graph=base, Z=z)
+    sd = {k[3:]: torch.from_numpy(f[k]) for k in f.files if k.startswith("w__")}
+    dec.load_state_dict(sd)
+    return f, base, dec, conv, sd
+
+
+@pytest.mark.parametrize("z", [4, 32])
+def test_forward_matches_reference(cuda, z):
+    f, base, dec, conv, _ = load_model(z)
+    dec = dec.to(cuda)
+    llr = torch.from_numpy(f["llr"]).to(cuda)
+    types = conv.get_message_types(base, z)
+    mv = conv.message_to_var_index()
+    Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
+    p = dec(llr, mv, types, Av, Ac)
+    np.testing.assert_allclose(p.cpu().numpy(), f["probs"], atol=TOL)
+    p = dec(llr, mv, None, Av, Ac)
+    np.testing.assert_allclose(p.cpu().numpy(), f["probs_no_types"], atol=TOL)
+    p, loss = dec(llr, mv, types, Av, Ac, ground_truth=torch.from_numpy(f["ground_truth"]).to(cuda))
+    assert abs(loss.item() - float(f["loss"])) < 1e-4
+    bits = dec.decode(llr, mv, types, Av, Ac)
+    ref_p = f["probs"]
+    sure = np.abs(ref_p - 0.5) > 1e-4  # decisions away from the threshold must agree
+    assert np.array_equal(bits.cpu().numpy()[sure].astype(np.uint8), f["decode_bits"][sure])
+
+
+def test_2d_mapping_quirk(cuda):
+    """The examples pass converter.message_to_var_mapping.long() (run_message_gnn.py:304-310):
+    column 0 of the one-hot is used as the variable index (message_gnn_decoder.py:220-226)."""
+    f, base, dec, conv, _ = load_model(4)
+    dec = dec.to(cuda)
+    llr = torch.from_numpy(f["llr"]).to(cuda)
+    p = dec(llr, conv.message_to_var_mapping.long(), conv.get_message_types(base, 4),
+            conv.var_to_check_adjacency, conv.check_to_var_adjacency)
+    np.testing.assert_allclose(p.cpu().numpy(), f["probs_2d_quirk"], atol=TOL)
+    with pytest.raises(IndexError):  # the float one-hot fails in the reference too
+        dec(llr, conv.message_to_var_mapping, None, conv.var_to_check_adjacency,
+            conv.check_to_var_adjacency)
+
+
+def test_untagged_adjacency_on_device(cuda):
+    """Adjacencies that went through .to(device) lose the tag: groups are derived by probing."""
+    f, base, dec, conv, _ = load_model(4)
+    dec = dec.to(cuda)
+    llr = torch.from_numpy(f["llr"]).to(cuda)
+    p = dec(llr, conv.message_to_var_index(), conv.get_message_types(base, 4),
+            conv.var_to_check_adjacency.to(cuda), conv.check_to_var_adjacency.to(cuda))
+    np.testing.assert_allclose(p.cpu().numpy(), f["probs"], atol=TOL)
+
+
+@pytest.mark.parametrize("B,chunk", [(3, None), (70, 16)])
+def test_z32_h64_vs_oracle(cuda, oracle_mod, B, chunk):
+    """The MFMA path at the headline code (Z = 32, H = 64, 3 layers, random weights)."""
+    torch.manual_seed(0)
+    base = load_base_matrix(code_path(32))
+    H = expand_base_matrix(base, 32)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=3, hidden_dim=64, base_graph=base, Z=32)
+    with torch.no_grad():
+        for p in dec.parameters():
+            p.mul_(0.5)
+    dec = dec.to(cuda)
+    types = conv.get_message_types(base, 32)
+    llr = (torch.randn(B, H.shape[1]) * 2 + 1.5).to(cuda)
+    ev, ec = conv.edge_var, conv.edge_chk
+    io = conv.message_to_var_index().to(cuda).to(torch.int32)
+    vg, cg = conv.var_groups, conv.check_groups
+    p = dec.native_forward(llr, io, types.to(cuda).to(torch.int32), vg, cg, chunk=chunk)
+    sd = {k: v.cpu() for k, v in dec.state_dict().items()}
+    ref = oracle_mod.gnn_forward(sd, llr.cpu(), ev, ev, ec, H.shape[1], H.shape[0], types)
+    np.testing.assert_allclose(p.cpu().numpy(), ref.numpy(), atol=TOL)
+
+
+def test_state_dict_keys_match_reference():
+    f = golden("gnn_z4.npz")
+    dec = MessageGNNDecoder(788, 5, 64, 4)
+    assert list(dec.state_dict().keys()) == list(f["state_keys"])
