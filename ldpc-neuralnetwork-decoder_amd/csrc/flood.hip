@@ -31,6 +31,14 @@ namespace ldpc {
 
 namespace {
 
+// Graph tables are read-only for the kernel's lifetime and indexed by wave-uniform values:
+// reading them through the constant address space lets the compiler use scalar (SMEM) loads
+// instead of per-lane vector loads.
+typedef const __attribute__((address_space(4))) int32_t const_i32;
+__device__ __forceinline__ int32_t tab(const int32_t *p, int i) {
+    return ((const_i32 *)p)[i];
+}
+
 __device__ __forceinline__ int rot_add(int k, int s, int Z) {
     const int t = k + s;
     return t >= Z ? t - Z : t;
@@ -42,15 +50,14 @@ __device__ __forceinline__ int rot_sub(int k, int s, int Z) {
 
 struct Lane {
     int lane, f, k, fz, Z;
-    bool pos_ok;   // lane maps to a (frame, row) position of the lane vector
-    bool valid;    // ... and that frame exists
+    bool valid;    // the lane's frame exists (Z divides 64: every lane has a position)
     int64_t frame;
     const float *llr_row;
     // index of the message on a block with shift s, seen from variable t = k of frame f
-    __device__ __forceinline__ int vidx(int s) const { return pos_ok ? fz + rot_sub(k, s, Z) : lane; }
-    __device__ __forceinline__ float llr(int col, int t) const {
-        return valid ? llr_row[col * Z + t] : 0.0f;
-    }
+    __device__ __forceinline__ int vidx(int s) const { return fz + rot_sub(k, s, Z); }
+    // llr_row points at a real row for every lane (frame 0 for lanes without a frame), so the
+    // load needs no branch; results of such lanes are never stored.
+    __device__ __forceinline__ float llr(int col, int t) const { return llr_row[col * Z + t]; }
 };
 
 __device__ __forceinline__ void put_bit(void *bits, int out_dtype, int64_t idx, int bit) {
@@ -75,13 +82,10 @@ struct MinSumStats {
         const float a = fabsf(x);
         nz += is_zero_sign(x);
         neg ^= (x < 0.0f);
-        if (a < m1) {
-            m2 = m1;
-            m1 = a;
-            i1 = e;
-        } else if (a < m2) {
-            m2 = a;
-        }
+        const bool lt1 = a < m1, lt2 = a < m2;  // NaN: both false
+        m2 = lt1 ? m1 : (lt2 ? a : m2);
+        i1 = lt1 ? e : i1;
+        m1 = lt1 ? a : m1;
     }
     __device__ __forceinline__ float c2v(int e, float x, float alpha) const {
         const float m = (e == i1) ? m2 : m1;
@@ -117,7 +121,7 @@ __device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int co
     }
     if (C.ballots) {
         // move the bit of variable t to lane f*Z + t before the ballot
-        const int src = L.pos_ok ? L.fz + rot_sub(L.k, s, L.Z) : L.lane;
+        const int src = L.fz + rot_sub(L.k, s, L.Z);
         const int bt = __shfl(bit, src, 64);
         const uint64_t w = __ballot(bt);
         if (L.lane == 0) C.words[col] = w;
@@ -140,22 +144,22 @@ __device__ __forceinline__ void var_decision(const Ctx &C, const Lane &L, int co
 
 template <int ALGO, int DC>
 __device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, int r, int &errs) {
-    const int p0 = C.T.row_ptr[r];
+    const int p0 = tab(C.T.row_ptr, r);
     float v[DC];
 #pragma unroll
     for (int e = 0; e < DC; ++e) {
-        const int sl = C.T.row_slot[p0 + e];
+        const int sl = tab(C.T.row_slot, p0 + e);
         if (sl >= 0)
             v[e] = C.lds[sl * 64 + L.lane];
         else
-            v[e] = L.llr(C.T.row_col[p0 + e], rot_add(L.k, C.T.row_shift[p0 + e], L.Z));
+            v[e] = L.llr(tab(C.T.row_col, p0 + e), rot_add(L.k, tab(C.T.row_shift, p0 + e), L.Z));
     }
     auto emit = [&](int e, float o) {
-        const int sl = C.T.row_slot[p0 + e];
+        const int sl = tab(C.T.row_slot, p0 + e);
         if (sl >= 0)
             C.lds[sl * 64 + L.lane] = o;
         else if (C.direct_bits || C.ballots)  // degree-1 variable: APP = llr.clone() + c2v
-            ext_decision(C, L, C.T.row_col[p0 + e], C.T.row_shift[p0 + e], v[e] + o, errs);
+            ext_decision(C, L, tab(C.T.row_col, p0 + e), tab(C.T.row_shift, p0 + e), v[e] + o, errs);
     };
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
         MinSumStats st;
@@ -185,17 +189,17 @@ __device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, int r, i
 // kMaxUnroll).  In-place is safe in ascending e: slot e is overwritten after P_{e+1} used it.
 template <int ALGO>
 __device__ __forceinline__ void check_task_dyn(const Ctx &C, const Lane &L, int r, int &errs) {
-    const int p0 = C.T.row_ptr[r], p1 = C.T.row_ptr[r + 1];
+    const int p0 = tab(C.T.row_ptr, r), p1 = tab(C.T.row_ptr, r + 1);
     auto rd = [&](int p) -> float {
-        const int sl = C.T.row_slot[p];
-        return sl >= 0 ? C.lds[sl * 64 + L.lane] : L.llr(C.T.row_col[p], rot_add(L.k, C.T.row_shift[p], L.Z));
+        const int sl = tab(C.T.row_slot, p);
+        return sl >= 0 ? C.lds[sl * 64 + L.lane] : L.llr(tab(C.T.row_col, p), rot_add(L.k, tab(C.T.row_shift, p), L.Z));
     };
     auto wr = [&](int p, float in, float out) {
-        const int sl = C.T.row_slot[p];
+        const int sl = tab(C.T.row_slot, p);
         if (sl >= 0)
             C.lds[sl * 64 + L.lane] = out;
         else if (C.direct_bits || C.ballots)
-            ext_decision(C, L, C.T.row_col[p], C.T.row_shift[p], in + out, errs);
+            ext_decision(C, L, tab(C.T.row_col, p), tab(C.T.row_shift, p), in + out, errs);
     };
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
         MinSumStats st;
@@ -222,14 +226,14 @@ __device__ __forceinline__ void check_task_dyn(const Ctx &C, const Lane &L, int 
 // the APP is P_DV = llr + c_0 + ... + c_{DV-1}.
 template <int DV>
 __device__ __forceinline__ void var_task(const Ctx &C, const Lane &L, int task, bool write, int &errs) {
-    const int col = C.T.vc_col[task];
-    const int p0 = C.T.vc_ptr[task];
+    const int col = tab(C.T.vc_col, task);
+    const int p0 = tab(C.T.vc_ptr, task);
     float P = L.llr(col, L.k);
     if constexpr (DV > 0) {
         float acc[DV];
 #pragma unroll
         for (int j = 0; j < DV; ++j) {
-            const float c = C.lds[C.T.vc_slot[p0 + j] * 64 + L.vidx(C.T.vc_shift[p0 + j])];
+            const float c = C.lds[tab(C.T.vc_slot, p0 + j) * 64 + L.vidx(tab(C.T.vc_shift, p0 + j))];
 #pragma unroll
             for (int e = 0; e < j; ++e) acc[e] = acc[e] + c;
             acc[j] = P;
@@ -237,22 +241,22 @@ __device__ __forceinline__ void var_task(const Ctx &C, const Lane &L, int task, 
         }
         if (write) {
 #pragma unroll
-            for (int e = 0; e < DV; ++e) C.lds[C.T.vc_slot[p0 + e] * 64 + L.vidx(C.T.vc_shift[p0 + e])] = acc[e];
+            for (int e = 0; e < DV; ++e) C.lds[tab(C.T.vc_slot, p0 + e) * 64 + L.vidx(tab(C.T.vc_shift, p0 + e))] = acc[e];
         }
     }
     if (C.direct_bits || C.ballots) var_decision(C, L, col, P, errs);
 }
 
 __device__ __forceinline__ void var_task_dyn(const Ctx &C, const Lane &L, int task, bool write, int &errs) {
-    const int col = C.T.vc_col[task];
-    const int p0 = C.T.vc_ptr[task], p1 = C.T.vc_ptr[task + 1];
+    const int col = tab(C.T.vc_col, task);
+    const int p0 = tab(C.T.vc_ptr, task), p1 = tab(C.T.vc_ptr, task + 1);
     const float x = L.llr(col, L.k);
     float P = x;
     for (int p = p0; p < p1; ++p) {
-        const int id = C.T.vc_slot[p] * 64 + L.vidx(C.T.vc_shift[p]);
+        const int id = tab(C.T.vc_slot, p) * 64 + L.vidx(tab(C.T.vc_shift, p));
         const float cp = C.lds[id];
         float acc = P;
-        for (int q = p + 1; q < p1; ++q) acc = acc + C.lds[C.T.vc_slot[q] * 64 + L.vidx(C.T.vc_shift[q])];
+        for (int q = p + 1; q < p1; ++q) acc = acc + C.lds[tab(C.T.vc_slot, q) * 64 + L.vidx(tab(C.T.vc_shift, q))];
         P = P + cp;
         if (write) C.lds[id] = acc;
     }
@@ -267,7 +271,7 @@ __device__ __forceinline__ void var_task_dyn(const Ctx &C, const Lane &L, int ta
 
 template <int ALGO>
 __device__ __forceinline__ void check_dispatch(const Ctx &C, const Lane &L, int r, int &errs) {
-    const int dc = C.T.row_ptr[r + 1] - C.T.row_ptr[r];
+    const int dc = tab(C.T.row_ptr, r + 1) - tab(C.T.row_ptr, r);
     switch (dc) {
         case 0: break;
 #define X(n) case n: check_task<ALGO, n>(C, L, r, errs); break;
@@ -278,7 +282,7 @@ __device__ __forceinline__ void check_dispatch(const Ctx &C, const Lane &L, int 
 }
 
 __device__ __forceinline__ void var_dispatch(const Ctx &C, const Lane &L, int task, bool write, int &errs) {
-    const int dv = C.T.vc_ptr[task + 1] - C.T.vc_ptr[task];
+    const int dv = tab(C.T.vc_ptr, task + 1) - tab(C.T.vc_ptr, task);
     switch (dv) {
         case 0: var_task<0>(C, L, task, write, errs); break;
 #define X(n) case n: var_task<n>(C, L, task, write, errs); break;
@@ -290,8 +294,8 @@ __device__ __forceinline__ void var_dispatch(const Ctx &C, const Lane &L, int ta
 
 __device__ __forceinline__ int parity_row(const Ctx &C, const Lane &L, int r) {
     int p = 0;
-    for (int q = C.T.row_ptr[r]; q < C.T.row_ptr[r + 1]; ++q)
-        p ^= (int)((C.words[C.T.row_col[q]] >> (L.fz + rot_add(L.k, C.T.row_shift[q], L.Z))) & 1ull);
+    for (int q = tab(C.T.row_ptr, r); q < tab(C.T.row_ptr, r + 1); ++q)
+        p ^= (int)((C.words[tab(C.T.row_col, q)] >> (L.fz + rot_add(L.k, tab(C.T.row_shift, q), L.Z))) & 1ull);
     return p;
 }
 
@@ -307,8 +311,8 @@ __device__ __forceinline__ uint64_t frame_valid_mask(uint64_t invalid_lanes, int
 __device__ __forceinline__ void emit_from_words(const Ctx &C, const Lane &L, const uint64_t *words, uint64_t mask,
                                 int wave, int &errs) {
     if (!(L.valid && ((mask >> L.f) & 1ull))) return;
-    for (int i = C.T.bw_ptr[wave]; i < C.T.bw_ptr[wave + 1]; ++i) {
-        const int col = C.T.bw_task[i];
+    for (int i = tab(C.T.bw_ptr, wave); i < tab(C.T.bw_ptr, wave + 1); ++i) {
+        const int col = tab(C.T.bw_task, i);
         const int bit = (int)((words[col] >> L.lane) & 1ull);
         put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (int64_t)col * L.Z + L.k, bit);
         errs += bit;
@@ -319,20 +323,21 @@ __device__ __forceinline__ void emit_from_words(const Ctx &C, const Lane &L, con
 __device__ __forceinline__ void reduce_counters(float *lds, const Lane &L, int errs, int my_iters, int nf, int FG,
                                 int Z, uint64_t *counters, int32_t *batch_iters) {
     uint32_t *u = reinterpret_cast<uint32_t *>(lds);
+    const int nt = blockDim.x;
     __syncthreads();
     u[threadIdx.x] = (uint32_t)errs;
-    u[256 + threadIdx.x] = (uint32_t)my_iters;
+    u[nt + threadIdx.x] = (uint32_t)my_iters;
     __syncthreads();
     if (threadIdx.x < 64) {
         const int f = threadIdx.x;
         uint64_t be = 0, fe = 0, fr = 0, it = 0;
         int itmax = 0;
         if (f < nf) {
-            for (int w = 0; w < kWaves; ++w)
+            for (int w = 0; w < nt / 64; ++w)
                 for (int k = 0; k < Z; ++k) be += u[w * 64 + f * Z + k];
             fe = be > 0;
             fr = 1;
-            it = u[256 + f * Z];
+            it = u[nt + f * Z];
             itmax = (int)it;
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -358,7 +363,7 @@ __device__ __forceinline__ void reduce_counters(float *lds, const Lane &L, int e
 }  // namespace
 
 template <int ALGO, int ES>
-__global__ __launch_bounds__(256) void flood_kernel(FloodTables T, const float *__restrict__ llr,
+__global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *__restrict__ llr,
                                                     int64_t B, int max_iter, float alpha,
                                                     int out_dtype, void *__restrict__ bits,
                                                     int32_t *__restrict__ iters_out,
@@ -375,9 +380,8 @@ __global__ __launch_bounds__(256) void flood_kernel(FloodTables T, const float *
     L.f = L.lane / T.Z;
     L.k = L.lane - L.f * T.Z;
     L.fz = L.f * T.Z;
-    L.pos_ok = L.f < T.FG;
     L.frame = (int64_t)blockIdx.x * T.FG + L.f;
-    L.valid = L.pos_ok && L.frame < B;
+    L.valid = L.frame < B;
     L.llr_row = llr + (L.valid ? L.frame : 0) * (int64_t)T.N;
     const int nf = (int)min<int64_t>((int64_t)T.FG, B - (int64_t)blockIdx.x * T.FG);
     const uint64_t exist = nf >= 64 ? ~0ull : ((1ull << nf) - 1ull);
@@ -393,12 +397,12 @@ __global__ __launch_bounds__(256) void flood_kernel(FloodTables T, const float *
     C.ballots = ES != LDPC_ES_OFF;
 
     // v2c <- llr on every slot (traditional_decoders.py:199-202)
-    for (int i = T.vw_ptr[wave]; i < T.vw_ptr[wave + 1]; ++i) {
-        const int task = T.vw_task[i];
-        const int col = T.vc_col[task];
+    for (int i = tab(T.vw_ptr, wave); i < tab(T.vw_ptr, wave + 1); ++i) {
+        const int task = tab(T.vw_task, i);
+        const int col = tab(T.vc_col, task);
         const float x = L.llr(col, L.k);
-        for (int p = T.vc_ptr[task]; p < T.vc_ptr[task + 1]; ++p)
-            lds[T.vc_slot[p] * 64 + L.vidx(T.vc_shift[p])] = x;
+        for (int p = tab(T.vc_ptr, task); p < tab(T.vc_ptr, task + 1); ++p)
+            lds[tab(T.vc_slot, p) * 64 + L.vidx(tab(T.vc_shift, p))] = x;
     }
     __syncthreads();
 
@@ -408,16 +412,15 @@ __global__ __launch_bounds__(256) void flood_kernel(FloodTables T, const float *
     for (int it = 0; it < max_iter; ++it) {
         const bool last = it == max_iter - 1;
         C.direct_bits = (ES == LDPC_ES_OFF) && last;
-        for (int i = T.cw_ptr[wave]; i < T.cw_ptr[wave + 1]; ++i) check_dispatch<ALGO>(C, L, T.cw_task[i], errs);
+        for (int i = tab(T.cw_ptr, wave); i < tab(T.cw_ptr, wave + 1); ++i) check_dispatch<ALGO>(C, L, tab(T.cw_task, i), errs);
         __syncthreads();
         if (ES != LDPC_ES_OFF && tid == 0) C.words[T.Nb] = 0;
-        for (int i = T.vw_ptr[wave]; i < T.vw_ptr[wave + 1]; ++i) var_dispatch(C, L, T.vw_task[i], !last, errs);
+        for (int i = tab(T.vw_ptr, wave); i < tab(T.vw_ptr, wave + 1); ++i) var_dispatch(C, L, tab(T.vw_task, i), !last, errs);
         __syncthreads();
         if constexpr (ES != LDPC_ES_OFF) {
             // syndrome H x = 0 per frame (traditional_decoders.py:111-134), from the ballots
             int inv = 0;
-            if (L.pos_ok)
-                for (int i = T.cw_ptr[wave]; i < T.cw_ptr[wave + 1]; ++i) inv |= parity_row(C, L, T.cw_task[i]);
+            for (int i = tab(T.cw_ptr, wave); i < tab(T.cw_ptr, wave + 1); ++i) inv |= parity_row(C, L, tab(T.cw_task, i));
             const uint64_t m = __ballot(inv);
             if (L.lane == 0 && m) atomicOr((unsigned long long *)&C.words[T.Nb], (unsigned long long)m);
             __syncthreads();
@@ -468,12 +471,12 @@ __global__ void batch_and_kernel(const uint32_t *__restrict__ ws_valid, int64_t 
     if (threadIdx.x < nvw) atomicAnd(&all_words[threadIdx.x], sh[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(256) void batch_emit_kernel(FloodTables T, const uint64_t *__restrict__ ws_words,
+__global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const uint64_t *__restrict__ ws_words,
                                                          const uint32_t *__restrict__ all_words, int max_iter,
                                                          int nvw, int64_t B, int out_dtype, void *bits,
                                                          int32_t *iters_out, int32_t *batch_iters,
                                                          uint64_t *counters) {
-    __shared__ float red[512];
+    __shared__ float red[2 * 512];
     int tstar = max_iter - 1;  // first iteration at which every frame was valid
     for (int w = 0; w < nvw; ++w) {
         const uint32_t aw = all_words[w];
@@ -489,9 +492,8 @@ __global__ __launch_bounds__(256) void batch_emit_kernel(FloodTables T, const ui
     L.f = L.lane / T.Z;
     L.k = L.lane - L.f * T.Z;
     L.fz = L.f * T.Z;
-    L.pos_ok = L.f < T.FG;
     L.frame = (int64_t)blockIdx.x * T.FG + L.f;
-    L.valid = L.pos_ok && L.frame < B;
+    L.valid = L.frame < B;
     L.llr_row = nullptr;
     Ctx C;
     C.T = T;
@@ -513,7 +515,7 @@ constexpr size_t kLdsMax = 160 * 1024;
 size_t flood_lds_bytes(const ldpc_graph *g, int es) {
     size_t b = (size_t)g->nslots * 64 * sizeof(float);
     if (es != LDPC_ES_OFF) b += (size_t)(g->Nb + 1) * sizeof(uint64_t);
-    return std::max<size_t>(b, 2 * 256 * sizeof(uint32_t));
+    return std::max<size_t>(b, 2 * 64 * (size_t)g->ft.W * sizeof(uint32_t));
 }
 
 struct BatchWs {
@@ -547,7 +549,7 @@ int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter,
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t nwg = (B + g->FG - 1) / g->FG;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), lds, s, g->ft, llr, B, max_iter, alpha,
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(64 * g->ft.W), lds, s, g->ft, llr, B, max_iter, alpha,
                        out_dtype, bits, iters, counters, batch_iters, ws_words, ws_valid, nvw);
     LDPC_CHECK_LAUNCH("flood_kernel");
     return LDPC_OK;
@@ -618,7 +620,7 @@ extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_l
             LDPC_CHECK_LAUNCH("fill");
         }
         const int64_t nwg = (B + g->FG - 1) / g->FG;
-        hipLaunchKernelGGL(batch_emit_kernel, dim3((unsigned)nwg), dim3(256), 0, s, g->ft, bw.words, bw.all,
+        hipLaunchKernelGGL(batch_emit_kernel, dim3((unsigned)nwg), dim3(64 * g->ft.W), 0, s, g->ft, bw.words, bw.all,
                            max_iter, bw.nvw, B, out_dtype, d_bits, d_iters, d_batch_iters, d_counters);
         LDPC_CHECK_LAUNCH("batch_emit_kernel");
     }

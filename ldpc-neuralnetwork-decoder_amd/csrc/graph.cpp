@@ -4,6 +4,7 @@
 // Python M x N loops that build index lists; 18.7 s at Z = 32 in the reference).  Here: O(E)
 // per candidate lifting size, once per code, then one upload.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -49,23 +50,23 @@ bool try_lift(int M, int N, const std::vector<int32_t> &ec, const std::vector<in
     return true;  // std::map iterates keys ascending = row-major, c ascending
 }
 
-// Longest-processing-time-first assignment of tasks to kWaves waves.
-void schedule(const std::vector<int> &tasks, const std::vector<double> &cost,
+// Longest-processing-time-first assignment of tasks to W waves.
+void schedule(const std::vector<int> &tasks, const std::vector<double> &cost, int W,
               std::vector<int32_t> &ptr, std::vector<int32_t> &list) {
     std::vector<int> order(tasks.size());
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(),
                      [&](int a, int b) { return cost[a] > cost[b]; });
-    std::vector<std::vector<int>> per(kWaves);
-    std::vector<double> load(kWaves, 0.0);
+    std::vector<std::vector<int>> per(W);
+    std::vector<double> load(W, 0.0);
     for (int i : order) {
         int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
         per[w].push_back(tasks[i]);
         load[w] += cost[i];
     }
-    ptr.assign(kWaves + 1, 0);
+    ptr.assign(W + 1, 0);
     list.clear();
-    for (int w = 0; w < kWaves; ++w) {
+    for (int w = 0; w < W; ++w) {
         std::sort(per[w].begin(), per[w].end());
         list.insert(list.end(), per[w].begin(), per[w].end());
         ptr[w + 1] = (int32_t)list.size();
@@ -74,21 +75,17 @@ void schedule(const std::vector<int> &tasks, const std::vector<double> &cost,
 
 int build(ldpc_graph *g) {
     const int M = g->M, N = g->N;
-    // choose the lifting: every z <= 64 that H is block-circulant for; prefer full lane use
-    // (FG * Z == 64), then the larger z (fewer, longer slots).
+    // choose the lifting: the largest z dividing 64 that H is block-circulant for, so that a
+    // wave's 64 lanes are exactly FG = 64/z frames x z rows (every lane owns a position; no
+    // lane predicates on the hot path).  z = 1 (one frame per lane) always works.
     int best = 1;
-    double best_util = 1.0;  // z = 1 always valid, 64 frames x 1 lane = 100 %
     std::vector<Block> blocks, cand;
     try_lift(M, N, g->edge_chk, g->edge_var, 1, blocks);
-    for (int z = 2; z <= 64; ++z) {
+    for (int z = 2; z <= 64; z *= 2) {
         if (M % z || N % z) continue;
         if (!try_lift(M, N, g->edge_chk, g->edge_var, z, cand)) continue;
-        const double util = (double)((64 / z) * z) / 64.0;
-        if (util > best_util + 1e-9 || (util > best_util - 1e-9 && z > best)) {
-            best = z;
-            best_util = util;
-            blocks = cand;
-        }
+        best = z;
+        blocks = cand;
     }
     g->Z = best;
     g->FG = 64 / best;
@@ -144,9 +141,12 @@ int build(ldpc_graph *g) {
     }
     for (int c = 0; c < Nb; ++c) btasks[c] = c;
     std::vector<int32_t> cw_ptr, cw_task, vw_ptr, vw_task, bw_ptr, bw_task;
-    schedule(rtasks, rcost, cw_ptr, cw_task);
-    schedule(vtasks, vcost, vw_ptr, vw_task);
-    schedule(btasks, bcost, bw_ptr, bw_task);
+    int W = 4;
+    if (const char *env = std::getenv("LDPC_FLOOD_WAVES")) W = std::atoi(env);
+    W = std::max(1, std::min(kMaxWaves, W));
+    schedule(rtasks, rcost, W, cw_ptr, cw_task);
+    schedule(vtasks, vcost, W, vw_ptr, vw_task);
+    schedule(btasks, bcost, W, bw_ptr, bw_task);
 
     // one int32 blob on the device
     std::vector<int32_t> blob;
@@ -185,6 +185,7 @@ int build(ldpc_graph *g) {
     t.Nb = Nb;
     t.N = N;
     t.nslots = nslots;
+    t.W = W;
 
     LDPC_HIP(hipDeviceSynchronize());
     return LDPC_OK;

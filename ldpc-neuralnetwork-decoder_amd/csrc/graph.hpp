@@ -19,7 +19,7 @@
 
 namespace ldpc {
 
-constexpr int kWaves = 4;        // waves per flood workgroup
+constexpr int kMaxWaves = 8;     // waves per flood workgroup (runtime W <= this)
 constexpr int kMaxUnroll = 24;   // check/var degrees handled by unrolled register code
 
 // Device view of the flooding tables (all int32, one allocation).  Passed by value.
@@ -32,13 +32,14 @@ struct FloodTables {
     const int32_t *vc_col;     // [nvc]
     const int32_t *vc_slot;    // [nnz_vc] slots of the column's blocks (ascending row)
     const int32_t *vc_shift;   // [nnz_vc]
-    const int32_t *cw_ptr;     // [kWaves+1] check-phase task list per wave
+    const int32_t *cw_ptr;     // [W+1] check-phase task list per wave
     const int32_t *cw_task;    // [Mb]
-    const int32_t *vw_ptr;     // [kWaves+1] var-phase task list per wave
+    const int32_t *vw_ptr;     // [W+1] var-phase task list per wave
     const int32_t *vw_task;    // [nvc]
-    const int32_t *bw_ptr;     // [kWaves+1] column list per wave for bit emission
+    const int32_t *bw_ptr;     // [W+1] column list per wave for bit emission
     const int32_t *bw_task;    // [Nb]
     int Z, FG, Mb, Nb, N, nslots;
+    int W;  // waves per workgroup
 };
 
 struct Block { int r, c, s; };
