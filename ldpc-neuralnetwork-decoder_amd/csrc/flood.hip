@@ -31,34 +31,35 @@ namespace ldpc {
 
 namespace {
 
-// Graph tables are read-only for the kernel's lifetime and indexed by wave-uniform values:
-// reading them through the constant address space lets the compiler use scalar (SMEM) loads
-// instead of per-lane vector loads.
+// Graph programs are read-only for the kernel's lifetime and indexed by wave-uniform values:
+// reading them through the constant address space makes every word a scalar (SMEM) load.
 typedef const __attribute__((address_space(4))) int32_t const_i32;
-__device__ __forceinline__ int32_t tab(const int32_t *p, int i) {
-    return ((const_i32 *)p)[i];
-}
-
-__device__ __forceinline__ int rot_add(int k, int s, int Z) {
-    const int t = k + s;
-    return t >= Z ? t - Z : t;
-}
-__device__ __forceinline__ int rot_sub(int k, int s, int Z) {
-    const int t = k - s;
-    return t < 0 ? t + Z : t;
-}
+__device__ __forceinline__ int32_t tab(const int32_t *p, int i) { return ((const_i32 *)p)[i]; }
 
 struct Lane {
-    int lane, f, k, fz, Z;
-    bool valid;    // the lane's frame exists (Z divides 64: every lane has a position)
+    int lane;      // 0..63 = f * Z + k
+    int f, k;      // frame within the lane vector, row (or column position) within a block
+    int lane4;     // 4 * lane: byte offset of this lane's entry in a slot
+    int fz4;       // 4 * f * Z
+    int k4;        // 4 * k
+    int zmask4;    // 4 * Z - 1 (Z is a power of two)
+    int z4;        // 4 * Z
+    bool valid;    // the lane's frame exists
     int64_t frame;
-    const float *llr_row;
-    // index of the message on a block with shift s, seen from variable t = k of frame f
-    __device__ __forceinline__ int vidx(int s) const { return fz + rot_sub(k, s, Z); }
-    // llr_row points at a real row for every lane (frame 0 for lanes without a frame), so the
-    // load needs no branch; results of such lanes are never stored.
-    __device__ __forceinline__ float llr(int col, int t) const { return llr_row[col * Z + t]; }
+    const char *llr_row;  // this lane's frame row (frame 0 for lanes without a frame)
+    // byte offset inside a slot of the message on a block with byte shift s4, seen from the
+    // variable at position k: row (k - s) mod Z of frame f
+    __device__ __forceinline__ int vrot(int s4) const { return fz4 + ((k4 - s4) & zmask4); }
+    // byte offset of variable (col, (k + s) mod Z) in an LLR row
+    __device__ __forceinline__ int col_off(int col, int s4) const { return col * z4 + ((k4 + s4) & zmask4); }
+    __device__ __forceinline__ int Z() const { return z4 >> 2; }
+    __device__ __forceinline__ float llr_at(int byte_off) const {
+        return *reinterpret_cast<const float *>(llr_row + byte_off);
+    }
 };
+
+__device__ __forceinline__ float lds_rd(const char *lds, int off) { return *reinterpret_cast<const float *>(lds + off); }
+__device__ __forceinline__ void lds_wr(char *lds, int off, float v) { *reinterpret_cast<float *>(lds + off) = v; }
 
 __device__ __forceinline__ void put_bit(void *bits, int out_dtype, int64_t idx, int bit) {
     if (out_dtype == LDPC_OUT_F32)
@@ -69,7 +70,6 @@ __device__ __forceinline__ void put_bit(void *bits, int out_dtype, int64_t idx, 
 
 __device__ __forceinline__ bool is_zero_sign(float x) { return !(x > 0.0f || x < 0.0f); }
 
-// ---------------------------------------------------------------- check updates (registers)
 // Min-sum statistics of one check row (traditional_decoders.py:207-232):
 //   c2v_e = prod_{e'!=e} sign(v) * (alpha * min_{e'!=e} |v|)
 // with torch.sign(0) = torch.sign(NaN) = 0 and NaN never winning the min (mag < min_mag fails).
@@ -100,8 +100,8 @@ __device__ __forceinline__ float two_atanh(float p) { return 2.0f * (float)atanh
 
 struct Ctx {
     FloodTables T;
-    float *lds;
-    uint64_t *words;  // ES: Nb decision ballots + 1 invalid-lane word
+    char *lds;
+    uint64_t *words;  // ES: Nb decision ballots + 1 invalid-lane word (in LDS)
     float alpha;
     int out_dtype;
     void *bits;
@@ -109,20 +109,17 @@ struct Ctx {
     bool ballots;      // ES: record decisions as ballots
 };
 
-// decision of variable (col, t = rot_add(k, s)) computed on the lane of check row k
-__device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int col, int s, float app,
+// decision of variable (col, (k + s) mod Z) computed on the lane of check row k
+__device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int col, int s4, float app,
                                              int &errs) {
     const int bit = app < 0.0f;  // NaN < 0 is false -> 0 (traditional_decoders.py:252)
-    if (C.direct_bits) {
-        if (L.valid) {
-            put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (int64_t)col * L.Z + rot_add(L.k, s, L.Z), bit);
-            errs += bit;
-        }
+    if (C.direct_bits && L.valid) {
+        put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (L.col_off(col, s4) >> 2), bit);
+        errs += bit;
     }
     if (C.ballots) {
         // move the bit of variable t to lane f*Z + t before the ballot
-        const int src = L.fz + rot_sub(L.k, s, L.Z);
-        const int bt = __shfl(bit, src, 64);
+        const int bt = __shfl(bit, L.vrot(s4) >> 2, 64);
         const uint64_t w = __ballot(bt);
         if (L.lane == 0) C.words[col] = w;
     }
@@ -130,11 +127,9 @@ __device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int co
 
 __device__ __forceinline__ void var_decision(const Ctx &C, const Lane &L, int col, float app, int &errs) {
     const int bit = app < 0.0f;
-    if (C.direct_bits) {
-        if (L.valid) {
-            put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (int64_t)col * L.Z + L.k, bit);
-            errs += bit;
-        }
+    if (C.direct_bits && L.valid) {
+        put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (int64_t)col * L.Z() + L.k, bit);
+        errs += bit;
     }
     if (C.ballots) {
         const uint64_t w = __ballot(bit);
@@ -142,24 +137,24 @@ __device__ __forceinline__ void var_decision(const Ctx &C, const Lane &L, int co
     }
 }
 
+// ---------------------------------------------------------------- check node update
+// prog points at the row's first edge word (uniform); DC compile-time.
 template <int ALGO, int DC>
-__device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, int r, int &errs) {
-    const int p0 = tab(C.T.row_ptr, r);
+__device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, const int32_t *prog, int &errs) {
     float v[DC];
+    int32_t w[DC];
 #pragma unroll
     for (int e = 0; e < DC; ++e) {
-        const int sl = tab(C.T.row_slot, p0 + e);
-        if (sl >= 0)
-            v[e] = C.lds[sl * 64 + L.lane];
-        else
-            v[e] = L.llr(tab(C.T.row_col, p0 + e), rot_add(L.k, tab(C.T.row_shift, p0 + e), L.Z));
+        w[e] = tab(prog, e);
+        const int lo = w[e] & kLowMask, s4 = (w[e] >> kShiftBit) & 0xFF;
+        v[e] = w[e] < 0 ? L.llr_at(L.col_off(lo, s4)) : lds_rd(C.lds, lo + L.lane4);
     }
     auto emit = [&](int e, float o) {
-        const int sl = tab(C.T.row_slot, p0 + e);
-        if (sl >= 0)
-            C.lds[sl * 64 + L.lane] = o;
+        const int lo = w[e] & kLowMask;
+        if (w[e] >= 0)
+            lds_wr(C.lds, lo + L.lane4, o);
         else if (C.direct_bits || C.ballots)  // degree-1 variable: APP = llr.clone() + c2v
-            ext_decision(C, L, tab(C.T.row_col, p0 + e), tab(C.T.row_shift, p0 + e), v[e] + o, errs);
+            ext_decision(C, L, lo, (w[e] >> kShiftBit) & 0xFF, v[e] + o, errs);
     };
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
         MinSumStats st;
@@ -185,55 +180,60 @@ __device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, int r, i
     }
 }
 
-// Any degree: messages re-read from LDS instead of registers (O(dc^2) reads; only used past
-// kMaxUnroll).  In-place is safe in ascending e: slot e is overwritten after P_{e+1} used it.
+// Any degree: messages re-read instead of kept in registers (O(dc^2) reads; used past the
+// unrolled range).  In-place is safe in ascending e: slot e is overwritten after P_{e+1} used it.
 template <int ALGO>
-__device__ __forceinline__ void check_task_dyn(const Ctx &C, const Lane &L, int r, int &errs) {
-    const int p0 = tab(C.T.row_ptr, r), p1 = tab(C.T.row_ptr, r + 1);
-    auto rd = [&](int p) -> float {
-        const int sl = tab(C.T.row_slot, p);
-        return sl >= 0 ? C.lds[sl * 64 + L.lane] : L.llr(tab(C.T.row_col, p), rot_add(L.k, tab(C.T.row_shift, p), L.Z));
+__device__ __forceinline__ void check_task_dyn(const Ctx &C, const Lane &L, const int32_t *prog, int dc,
+                                               int &errs) {
+    auto rd = [&](int e) -> float {
+        const int32_t w = tab(prog, e);
+        const int lo = w & kLowMask;
+        return w < 0 ? L.llr_at(L.col_off(lo, (w >> kShiftBit) & 0xFF)) : lds_rd(C.lds, lo + L.lane4);
     };
-    auto wr = [&](int p, float in, float out) {
-        const int sl = tab(C.T.row_slot, p);
-        if (sl >= 0)
-            C.lds[sl * 64 + L.lane] = out;
+    auto wr = [&](int e, float in, float out) {
+        const int32_t w = tab(prog, e);
+        const int lo = w & kLowMask;
+        if (w >= 0)
+            lds_wr(C.lds, lo + L.lane4, out);
         else if (C.direct_bits || C.ballots)
-            ext_decision(C, L, tab(C.T.row_col, p), tab(C.T.row_shift, p), in + out, errs);
+            ext_decision(C, L, lo, (w >> kShiftBit) & 0xFF, in + out, errs);
     };
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
         MinSumStats st;
-        for (int p = p0; p < p1; ++p) st.add(p, rd(p));
-        for (int p = p0; p < p1; ++p) {
-            const float x = rd(p);
-            wr(p, x, st.c2v(p, x, C.alpha));
+        for (int e = 0; e < dc; ++e) st.add(e, rd(e));
+        for (int e = 0; e < dc; ++e) {
+            const float x = rd(e);
+            wr(e, x, st.c2v(e, x, C.alpha));
         }
     } else {
         float P = 1.0f;
-        for (int p = p0; p < p1; ++p) {
-            const float x = rd(p);
+        for (int e = 0; e < dc; ++e) {
+            const float x = rd(e);
             float rr = P;
-            for (int q = p + 1; q < p1; ++q) rr = rr * tanh_half(rd(q));
+            for (int q = e + 1; q < dc; ++q) rr = rr * tanh_half(rd(q));
             const float t = tanh_half(x);
-            wr(p, x, two_atanh(rr));
+            wr(e, x, two_atanh(rr));
             P = P * t;
         }
     }
 }
 
+// ---------------------------------------------------------------- variable node update
 // Variable update (traditional_decoders.py:235-250): v2c_e = llr + sum_{e'!=e} c_e' added in
 // ascending check order, i.e. acc[e] = P_e (prefix) followed by c_{e+1}, c_{e+2}, ...;
 // the APP is P_DV = llr + c_0 + ... + c_{DV-1}.
 template <int DV>
-__device__ __forceinline__ void var_task(const Ctx &C, const Lane &L, int task, bool write, int &errs) {
-    const int col = tab(C.T.vc_col, task);
-    const int p0 = tab(C.T.vc_ptr, task);
-    float P = L.llr(col, L.k);
+__device__ __forceinline__ void var_task(const Ctx &C, const Lane &L, const int32_t *prog, int col, bool write,
+                                         int &errs) {
+    float P = L.llr_at(col * L.z4 + L.k4);
     if constexpr (DV > 0) {
         float acc[DV];
+        int off[DV];
 #pragma unroll
         for (int j = 0; j < DV; ++j) {
-            const float c = C.lds[tab(C.T.vc_slot, p0 + j) * 64 + L.vidx(tab(C.T.vc_shift, p0 + j))];
+            const int32_t w = tab(prog, j);
+            off[j] = (w & kLowMask) + L.vrot((w >> kShiftBit) & 0xFF);
+            const float c = lds_rd(C.lds, off[j]);
 #pragma unroll
             for (int e = 0; e < j; ++e) acc[e] = acc[e] + c;
             acc[j] = P;
@@ -241,24 +241,26 @@ __device__ __forceinline__ void var_task(const Ctx &C, const Lane &L, int task, 
         }
         if (write) {
 #pragma unroll
-            for (int e = 0; e < DV; ++e) C.lds[tab(C.T.vc_slot, p0 + e) * 64 + L.vidx(tab(C.T.vc_shift, p0 + e))] = acc[e];
+            for (int e = 0; e < DV; ++e) lds_wr(C.lds, off[e], acc[e]);
         }
     }
     if (C.direct_bits || C.ballots) var_decision(C, L, col, P, errs);
 }
 
-__device__ __forceinline__ void var_task_dyn(const Ctx &C, const Lane &L, int task, bool write, int &errs) {
-    const int col = tab(C.T.vc_col, task);
-    const int p0 = tab(C.T.vc_ptr, task), p1 = tab(C.T.vc_ptr, task + 1);
-    const float x = L.llr(col, L.k);
-    float P = x;
-    for (int p = p0; p < p1; ++p) {
-        const int id = tab(C.T.vc_slot, p) * 64 + L.vidx(tab(C.T.vc_shift, p));
-        const float cp = C.lds[id];
+__device__ __forceinline__ void var_task_dyn(const Ctx &C, const Lane &L, const int32_t *prog, int dv, int col,
+                                             bool write, int &errs) {
+    auto off = [&](int e) {
+        const int32_t w = tab(prog, e);
+        return (w & kLowMask) + L.vrot((w >> kShiftBit) & 0xFF);
+    };
+    float P = L.llr_at(col * L.z4 + L.k4);
+    for (int e = 0; e < dv; ++e) {
+        const int o = off(e);
+        const float cp = lds_rd(C.lds, o);
         float acc = P;
-        for (int q = p + 1; q < p1; ++q) acc = acc + C.lds[tab(C.T.vc_slot, q) * 64 + L.vidx(tab(C.T.vc_shift, q))];
+        for (int q = e + 1; q < dv; ++q) acc = acc + lds_rd(C.lds, off(q));
         P = P + cp;
-        if (write) C.lds[id] = acc;
+        if (write) lds_wr(C.lds, o, acc);
     }
     if (C.direct_bits || C.ballots) var_decision(C, L, col, P, errs);
 }
@@ -269,34 +271,75 @@ __device__ __forceinline__ void var_task_dyn(const Ctx &C, const Lane &L, int ta
     X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
     X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24)
 
+// run this wave's check program
 template <int ALGO>
-__device__ __forceinline__ void check_dispatch(const Ctx &C, const Lane &L, int r, int &errs) {
-    const int dc = tab(C.T.row_ptr, r + 1) - tab(C.T.row_ptr, r);
-    switch (dc) {
-        case 0: break;
-#define X(n) case n: check_task<ALGO, n>(C, L, r, errs); break;
-        LDPC_DC_CASES(X)
+__device__ __forceinline__ void check_phase(const Ctx &C, const Lane &L, int wave, int &errs) {
+    const int p1 = tab(C.T.prog_ptr, wave + 1);
+    for (int pc = tab(C.T.prog_ptr, wave); pc < p1;) {
+        const int dc = tab(C.T.chk_prog, pc);
+        const int32_t *prog = C.T.chk_prog + pc + 1;
+        switch (dc) {
+            case 0: break;
+#define X(n) case n: check_task<ALGO, n>(C, L, prog, errs); break;
+            LDPC_DC_CASES(X)
 #undef X
-        default: check_task_dyn<ALGO>(C, L, r, errs); break;
+            default: check_task_dyn<ALGO>(C, L, prog, dc, errs); break;
+        }
+        pc += 1 + dc;
     }
 }
 
-__device__ __forceinline__ void var_dispatch(const Ctx &C, const Lane &L, int task, bool write, int &errs) {
-    const int dv = tab(C.T.vc_ptr, task + 1) - tab(C.T.vc_ptr, task);
-    switch (dv) {
-        case 0: var_task<0>(C, L, task, write, errs); break;
-#define X(n) case n: var_task<n>(C, L, task, write, errs); break;
-        LDPC_DV_CASES(X)
+__device__ __forceinline__ void var_phase(const Ctx &C, const Lane &L, int wave, bool write, int &errs) {
+    const int W1 = C.T.W + 1;
+    const int p1 = tab(C.T.prog_ptr, W1 + wave + 1);
+    for (int pc = tab(C.T.prog_ptr, W1 + wave); pc < p1;) {
+        const int h = tab(C.T.var_prog, pc);
+        const int dv = h & 0xFF, col = h >> 8;
+        const int32_t *prog = C.T.var_prog + pc + 1;
+        switch (dv) {
+            case 0: var_task<0>(C, L, prog, col, write, errs); break;
+#define X(n) case n: var_task<n>(C, L, prog, col, write, errs); break;
+            LDPC_DV_CASES(X)
 #undef X
-        default: var_task_dyn(C, L, task, write, errs); break;
+            default: var_task_dyn(C, L, prog, dv, col, write, errs); break;
+        }
+        pc += 1 + dv;
     }
 }
 
-__device__ __forceinline__ int parity_row(const Ctx &C, const Lane &L, int r) {
-    int p = 0;
-    for (int q = tab(C.T.row_ptr, r); q < tab(C.T.row_ptr, r + 1); ++q)
-        p ^= (int)((C.words[tab(C.T.row_col, q)] >> (L.fz + rot_add(L.k, tab(C.T.row_shift, q), L.Z))) & 1ull);
-    return p;
+// v2c <- llr on every slot (traditional_decoders.py:199-202)
+__device__ __forceinline__ void init_phase(const Ctx &C, const Lane &L, int wave) {
+    const int W1 = C.T.W + 1;
+    const int p1 = tab(C.T.prog_ptr, W1 + wave + 1);
+    for (int pc = tab(C.T.prog_ptr, W1 + wave); pc < p1;) {
+        const int h = tab(C.T.var_prog, pc);
+        const int dv = h & 0xFF, col = h >> 8;
+        const float x = L.llr_at(col * L.z4 + L.k4);
+        for (int e = 0; e < dv; ++e) {
+            const int32_t w = tab(C.T.var_prog, pc + 1 + e);
+            lds_wr(C.lds, (w & kLowMask) + L.vrot((w >> kShiftBit) & 0xFF), x);
+        }
+        pc += 1 + dv;
+    }
+}
+
+// syndrome of this wave's rows from the ballots: 1 if any of its checks fails for this lane
+__device__ __forceinline__ int parity_phase(const Ctx &C, const Lane &L, int wave) {
+    const int W1 = C.T.W + 1;
+    const int p1 = tab(C.T.prog_ptr, 2 * W1 + wave + 1);
+    int inv = 0;
+    for (int pc = tab(C.T.prog_ptr, 2 * W1 + wave); pc < p1;) {
+        const int dc = tab(C.T.par_prog, pc);
+        int p = 0;
+        for (int e = 0; e < dc; ++e) {
+            const int32_t w = tab(C.T.par_prog, pc + 1 + e);
+            const int col = w & kLowMask, s = w >> kShiftBit;
+            p ^= (int)((C.words[col] >> (L.f * L.Z() + ((L.k + s) & (L.Z() - 1)))) & 1ull);
+        }
+        inv |= p;
+        pc += 1 + dc;
+    }
+    return inv;
 }
 
 __device__ __forceinline__ uint64_t frame_valid_mask(uint64_t invalid_lanes, int Z, int FG) {
@@ -309,19 +352,20 @@ __device__ __forceinline__ uint64_t frame_valid_mask(uint64_t invalid_lanes, int
 
 // emit the decisions of frames in `mask` from the ballots (columns spread over the waves)
 __device__ __forceinline__ void emit_from_words(const Ctx &C, const Lane &L, const uint64_t *words, uint64_t mask,
-                                int wave, int &errs) {
+                                                int wave, int &errs) {
     if (!(L.valid && ((mask >> L.f) & 1ull))) return;
-    for (int i = tab(C.T.bw_ptr, wave); i < tab(C.T.bw_ptr, wave + 1); ++i) {
+    const int W1 = C.T.W + 1;
+    for (int i = tab(C.T.prog_ptr, 3 * W1 + wave); i < tab(C.T.prog_ptr, 3 * W1 + wave + 1); ++i) {
         const int col = tab(C.T.bw_task, i);
         const int bit = (int)((words[col] >> L.lane) & 1ull);
-        put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (int64_t)col * L.Z + L.k, bit);
+        put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (int64_t)col * L.Z() + L.k, bit);
         errs += bit;
     }
 }
 
 // per-workgroup reduction of the error counters: {bit errors, frame errors, frames, iter sum}
-__device__ __forceinline__ void reduce_counters(float *lds, const Lane &L, int errs, int my_iters, int nf, int FG,
-                                int Z, uint64_t *counters, int32_t *batch_iters) {
+__device__ __forceinline__ void reduce_counters(void *lds, const Lane &L, int errs, int my_iters, int nf,
+                                                int Z, uint64_t *counters, int32_t *batch_iters) {
     uint32_t *u = reinterpret_cast<uint32_t *>(lds);
     const int nt = blockDim.x;
     __syncthreads();
@@ -357,7 +401,23 @@ __device__ __forceinline__ void reduce_counters(float *lds, const Lane &L, int e
             if (batch_iters) atomicMax(batch_iters, itmax);
         }
     }
-    (void)FG;
+}
+
+__device__ __forceinline__ Lane make_lane(const FloodTables &T, const float *llr, int64_t B) {
+    Lane L;
+    L.lane = threadIdx.x & 63;
+    const int lz = __builtin_ctz((unsigned)T.Z);  // Z is a power of two
+    L.f = L.lane >> lz;
+    L.k = L.lane & (T.Z - 1);
+    L.lane4 = 4 * L.lane;
+    L.fz4 = 4 * (L.f << lz);
+    L.k4 = 4 * L.k;
+    L.z4 = 4 * T.Z;
+    L.zmask4 = 4 * T.Z - 1;
+    L.frame = (int64_t)blockIdx.x * T.FG + L.f;
+    L.valid = L.frame < B;
+    L.llr_row = reinterpret_cast<const char *>(llr ? llr + (L.valid ? L.frame : 0) * (int64_t)T.N : nullptr);
+    return L;
 }
 
 }  // namespace
@@ -371,39 +431,24 @@ __global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *
                                                     int32_t *__restrict__ batch_iters,
                                                     uint64_t *__restrict__ ws_words,
                                                     uint32_t *__restrict__ ws_valid, int nvw) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
+    extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    Lane L;
-    L.lane = tid & 63;
-    L.Z = T.Z;
-    L.f = L.lane / T.Z;
-    L.k = L.lane - L.f * T.Z;
-    L.fz = L.f * T.Z;
-    L.frame = (int64_t)blockIdx.x * T.FG + L.f;
-    L.valid = L.frame < B;
-    L.llr_row = llr + (L.valid ? L.frame : 0) * (int64_t)T.N;
+    const Lane L = make_lane(T, llr, B);
     const int nf = (int)min<int64_t>((int64_t)T.FG, B - (int64_t)blockIdx.x * T.FG);
     const uint64_t exist = nf >= 64 ? ~0ull : ((1ull << nf) - 1ull);
 
     Ctx C;
     C.T = T;
     C.lds = lds;
-    C.words = reinterpret_cast<uint64_t *>(lds + (size_t)T.nslots * 64);
+    C.words = reinterpret_cast<uint64_t *>(lds + (size_t)T.nslots * 256);
     C.alpha = alpha;
     C.out_dtype = out_dtype;
     C.bits = bits;
     C.direct_bits = false;
     C.ballots = ES != LDPC_ES_OFF;
 
-    // v2c <- llr on every slot (traditional_decoders.py:199-202)
-    for (int i = tab(T.vw_ptr, wave); i < tab(T.vw_ptr, wave + 1); ++i) {
-        const int task = tab(T.vw_task, i);
-        const int col = tab(T.vc_col, task);
-        const float x = L.llr(col, L.k);
-        for (int p = tab(T.vc_ptr, task); p < tab(T.vc_ptr, task + 1); ++p)
-            lds[tab(T.vc_slot, p) * 64 + L.vidx(tab(T.vc_shift, p))] = x;
-    }
+    init_phase(C, L, wave);
     __syncthreads();
 
     int errs = 0;
@@ -412,16 +457,14 @@ __global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *
     for (int it = 0; it < max_iter; ++it) {
         const bool last = it == max_iter - 1;
         C.direct_bits = (ES == LDPC_ES_OFF) && last;
-        for (int i = tab(T.cw_ptr, wave); i < tab(T.cw_ptr, wave + 1); ++i) check_dispatch<ALGO>(C, L, tab(T.cw_task, i), errs);
+        check_phase<ALGO>(C, L, wave, errs);
         __syncthreads();
         if (ES != LDPC_ES_OFF && tid == 0) C.words[T.Nb] = 0;
-        for (int i = tab(T.vw_ptr, wave); i < tab(T.vw_ptr, wave + 1); ++i) var_dispatch(C, L, tab(T.vw_task, i), !last, errs);
+        var_phase(C, L, wave, !last, errs);
         __syncthreads();
         if constexpr (ES != LDPC_ES_OFF) {
             // syndrome H x = 0 per frame (traditional_decoders.py:111-134), from the ballots
-            int inv = 0;
-            for (int i = tab(T.cw_ptr, wave); i < tab(T.cw_ptr, wave + 1); ++i) inv |= parity_row(C, L, tab(T.cw_task, i));
-            const uint64_t m = __ballot(inv);
+            const uint64_t m = __ballot(parity_phase(C, L, wave));
             if (L.lane == 0 && m) atomicOr((unsigned long long *)&C.words[T.Nb], (unsigned long long)m);
             __syncthreads();
             const uint64_t vmask = frame_valid_mask(C.words[T.Nb], T.Z, T.FG) & exist;
@@ -454,7 +497,7 @@ __global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *
         if (iters_out && L.valid && L.k == 0) iters_out[L.frame] = max_iter;
     }
     if constexpr (ES != LDPC_ES_BATCH) {
-        if (counters || batch_iters) reduce_counters(lds, L, errs, my_iters, nf, T.FG, T.Z, counters, batch_iters);
+        if (counters || batch_iters) reduce_counters(lds, L, errs, my_iters, nf, T.Z, counters, batch_iters);
     }
 }
 
@@ -476,7 +519,7 @@ __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const ui
                                                          int nvw, int64_t B, int out_dtype, void *bits,
                                                          int32_t *iters_out, int32_t *batch_iters,
                                                          uint64_t *counters) {
-    __shared__ float red[2 * 512];
+    __shared__ uint32_t red[2 * 512];
     int tstar = max_iter - 1;  // first iteration at which every frame was valid
     for (int w = 0; w < nvw; ++w) {
         const uint32_t aw = all_words[w];
@@ -485,16 +528,8 @@ __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const ui
             if (t < max_iter) { tstar = t; break; }
         }
     }
-    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    Lane L;
-    L.lane = tid & 63;
-    L.Z = T.Z;
-    L.f = L.lane / T.Z;
-    L.k = L.lane - L.f * T.Z;
-    L.fz = L.f * T.Z;
-    L.frame = (int64_t)blockIdx.x * T.FG + L.f;
-    L.valid = L.frame < B;
-    L.llr_row = nullptr;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Lane L = make_lane(T, nullptr, B);
     Ctx C;
     C.T = T;
     C.out_dtype = out_dtype;
@@ -503,7 +538,7 @@ __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const ui
     emit_from_words(C, L, ws_words + ((int64_t)blockIdx.x * max_iter + tstar) * T.Nb, ~0ull, wave, errs);
     if (iters_out && L.valid && L.k == 0) iters_out[L.frame] = tstar + 1;
     const int nf = (int)min<int64_t>((int64_t)T.FG, B - (int64_t)blockIdx.x * T.FG);
-    if (counters || batch_iters) reduce_counters(red, L, errs, tstar + 1, nf, T.FG, T.Z, counters, batch_iters);
+    if (counters || batch_iters) reduce_counters(red, L, errs, tstar + 1, nf, T.Z, counters, batch_iters);
 }
 
 __global__ void fill_i32_kernel(int32_t *p, int32_t v) { *p = v; }

@@ -106,47 +106,57 @@ int build(ldpc_graph *g) {
         if (dv[blocks[i].c] >= 2) slot_of[i] = nslots++;
     g->nslots = nslots;
 
-    // row tables
-    std::vector<int32_t> row_ptr(Mb + 1, 0), row_col, row_shift, row_slot;
-    for (size_t i = 0; i < blocks.size(); ++i) {
-        row_col.push_back(blocks[i].c);
-        row_shift.push_back(blocks[i].s);
-        row_slot.push_back(slot_of[i]);
-        row_ptr[blocks[i].r + 1]++;
-    }
-    for (int r = 0; r < Mb; ++r) row_ptr[r + 1] += row_ptr[r];
-
-    // var tasks: columns with degree != 1, blocks in ascending row order
-    std::vector<std::vector<int>> col_blocks(Nb);
-    for (size_t i = 0; i < blocks.size(); ++i) col_blocks[blocks[i].c].push_back((int)i);
-    std::vector<int32_t> vc_ptr(1, 0), vc_col, vc_slot, vc_shift;
-    for (int c = 0; c < Nb; ++c) {
-        if (dv[c] == 1) continue;
-        vc_col.push_back(c);
-        for (int i : col_blocks[c]) {  // blocks were pushed row-major: rows ascending
-            vc_slot.push_back(slot_of[i]);
-            vc_shift.push_back(blocks[i].s);
-        }
-        vc_ptr.push_back((int32_t)vc_slot.size());
-    }
-
-    // schedules (cost in VALU-ish units per lane vector)
-    std::vector<int> rtasks(Mb), vtasks(vc_col.size()), btasks(Nb);
-    std::vector<double> rcost(Mb), vcost(vc_col.size()), bcost(Nb, 1.0);
-    for (int r = 0; r < Mb; ++r) { rtasks[r] = r; rcost[r] = 6.0 * dc[r] + 0.5 * dc[r] * dc[r] + 8; }
-    for (size_t i = 0; i < vc_col.size(); ++i) {
-        const double d = dv[vc_col[i]];
-        vtasks[i] = (int)i;
-        vcost[i] = 0.5 * d * (d + 1) + 4.0 * d + 6;
-    }
-    for (int c = 0; c < Nb; ++c) btasks[c] = c;
-    std::vector<int32_t> cw_ptr, cw_task, vw_ptr, vw_task, bw_ptr, bw_task;
+    // schedules (cost in VALU-ish units per lane vector), LPT over W waves
     int W = 4;
     if (const char *env = std::getenv("LDPC_FLOOD_WAVES")) W = std::atoi(env);
     W = std::max(1, std::min(kMaxWaves, W));
+    std::vector<std::vector<int>> row_blocks(Mb), col_blocks(Nb);
+    for (size_t i = 0; i < blocks.size(); ++i) {
+        row_blocks[blocks[i].r].push_back((int)i);  // c ascending (row-major order)
+        col_blocks[blocks[i].c].push_back((int)i);  // r ascending
+    }
+    std::vector<int> rtasks(Mb), vtasks, btasks(Nb);
+    std::vector<double> rcost(Mb), vcost, bcost(Nb, 1.0);
+    for (int r = 0; r < Mb; ++r) { rtasks[r] = r; rcost[r] = 6.0 * dc[r] + 0.5 * dc[r] * dc[r] + 8; }
+    for (int c = 0; c < Nb; ++c) {
+        if (dv[c] == 1) continue;
+        vtasks.push_back(c);
+        vcost.push_back(0.5 * dv[c] * (dv[c] + 1) + 4.0 * dv[c] + 6);
+    }
+    for (int c = 0; c < Nb; ++c) btasks[c] = c;
+    std::vector<int32_t> cw_ptr, cw_task, vw_ptr, vw_task, bw_ptr, bw_task;
     schedule(rtasks, rcost, W, cw_ptr, cw_task);
     schedule(vtasks, vcost, W, vw_ptr, vw_task);
     schedule(btasks, bcost, W, bw_ptr, bw_task);
+
+    // programs
+    std::vector<int32_t> chk, var, par, prog_ptr(4 * (W + 1), 0);
+    for (int w = 0; w < W; ++w) {
+        for (int q = cw_ptr[w]; q < cw_ptr[w + 1]; ++q) {
+            const int r = cw_task[q];
+            chk.push_back((int32_t)row_blocks[r].size());
+            par.push_back((int32_t)row_blocks[r].size());
+            for (int i : row_blocks[r]) {
+                const Block &bk = blocks[i];
+                if (slot_of[i] >= 0)
+                    chk.push_back((slot_of[i] * 256) | ((4 * bk.s) << kShiftBit));
+                else
+                    chk.push_back(kExtFlag | bk.c | ((4 * bk.s) << kShiftBit));
+                par.push_back(bk.c | (bk.s << kShiftBit));
+            }
+        }
+        prog_ptr[w + 1] = (int32_t)chk.size();
+        prog_ptr[2 * (W + 1) + w + 1] = (int32_t)par.size();
+        for (int q = vw_ptr[w]; q < vw_ptr[w + 1]; ++q) {
+            const int c = vw_task[q];
+            var.push_back((int32_t)col_blocks[c].size() | (c << 8));
+            for (int i : col_blocks[c]) var.push_back((slot_of[i] * 256) | ((4 * blocks[i].s) << kShiftBit));
+        }
+        prog_ptr[(W + 1) + w + 1] = (int32_t)var.size();
+        prog_ptr[3 * (W + 1) + w + 1] = bw_ptr[w + 1];
+    }
+    if ((int64_t)nslots * 256 >= (1 << kShiftBit) || Nb >= (1 << kShiftBit) || g->max_dv >= 256)
+        return fail(LDPC_EUNSUPPORTED, "graph too large for the flood schedule encoding");
 
     // one int32 blob on the device
     std::vector<int32_t> blob;
@@ -156,29 +166,16 @@ int build(ldpc_graph *g) {
         blob.push_back(0);  // keep every table non-empty
         return off;
     };
-    const size_t o_rp = put(row_ptr), o_rc = put(row_col), o_rs = put(row_shift),
-                 o_rsl = put(row_slot), o_vp = put(vc_ptr), o_vc = put(vc_col),
-                 o_vsl = put(vc_slot), o_vs = put(vc_shift), o_cwp = put(cw_ptr),
-                 o_cwt = put(cw_task), o_vwp = put(vw_ptr), o_vwt = put(vw_task),
-                 o_bwp = put(bw_ptr), o_bwt = put(bw_task);
+    const size_t o_c = put(chk), o_v = put(var), o_p = put(par), o_b = put(bw_task), o_pp = put(prog_ptr);
     LDPC_HIP(hipGetDevice(&g->device));
     LDPC_HIP(hipMalloc(&g->d_tab, blob.size() * sizeof(int32_t)));
     LDPC_HIP(hipMemcpy(g->d_tab, blob.data(), blob.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     FloodTables &t = g->ft;
-    t.row_ptr = g->d_tab + o_rp;
-    t.row_col = g->d_tab + o_rc;
-    t.row_shift = g->d_tab + o_rs;
-    t.row_slot = g->d_tab + o_rsl;
-    t.vc_ptr = g->d_tab + o_vp;
-    t.vc_col = g->d_tab + o_vc;
-    t.vc_slot = g->d_tab + o_vsl;
-    t.vc_shift = g->d_tab + o_vs;
-    t.cw_ptr = g->d_tab + o_cwp;
-    t.cw_task = g->d_tab + o_cwt;
-    t.vw_ptr = g->d_tab + o_vwp;
-    t.vw_task = g->d_tab + o_vwt;
-    t.bw_ptr = g->d_tab + o_bwp;
-    t.bw_task = g->d_tab + o_bwt;
+    t.chk_prog = g->d_tab + o_c;
+    t.var_prog = g->d_tab + o_v;
+    t.par_prog = g->d_tab + o_p;
+    t.bw_task = g->d_tab + o_b;
+    t.prog_ptr = g->d_tab + o_pp;
     t.Z = g->Z;
     t.FG = g->FG;
     t.Mb = Mb;

@@ -22,25 +22,24 @@ namespace ldpc {
 constexpr int kMaxWaves = 8;     // waves per flood workgroup (runtime W <= this)
 constexpr int kMaxUnroll = 24;   // check/var degrees handled by unrolled register code
 
-// Device view of the flooding tables (all int32, one allocation).  Passed by value.
+// Device view of the flooding schedule: per-wave "programs" (int32 streams, read through the
+// constant address space so that every word is a scalar load).  Passed by value.
+//   check program, per block-row: header dc, then dc edge words
+//       slot edge:  slot_byte_offset | (4*shift) << 18
+//       degree-1:   0x80000000 | col | (4*shift) << 18      (v2c is the channel LLR)
+//   var program, per column with degree != 1: header dv | col << 8, then dv edge words
+//       slot_byte_offset | (4*shift) << 18                  (blocks in ascending row order)
+//   parity program, per block-row: header dc, then dc words col | shift << 18
+//   bit-emission list: the columns each wave writes out
+// prog_ptr holds 4 x (W+1) offsets: [chk | var | par | bw] per wave.
 struct FloodTables {
-    const int32_t *row_ptr;    // [Mb+1]
-    const int32_t *row_col;    // [nnz] column of each block of the row (ascending)
-    const int32_t *row_shift;  // [nnz]
-    const int32_t *row_slot;   // [nnz] LDS slot, or -1 for a degree-1 column
-    const int32_t *vc_ptr;     // [nvc+1] var tasks: columns with degree != 1
-    const int32_t *vc_col;     // [nvc]
-    const int32_t *vc_slot;    // [nnz_vc] slots of the column's blocks (ascending row)
-    const int32_t *vc_shift;   // [nnz_vc]
-    const int32_t *cw_ptr;     // [W+1] check-phase task list per wave
-    const int32_t *cw_task;    // [Mb]
-    const int32_t *vw_ptr;     // [W+1] var-phase task list per wave
-    const int32_t *vw_task;    // [nvc]
-    const int32_t *bw_ptr;     // [W+1] column list per wave for bit emission
-    const int32_t *bw_task;    // [Nb]
+    const int32_t *chk_prog, *var_prog, *par_prog, *bw_task, *prog_ptr;
     int Z, FG, Mb, Nb, N, nslots;
     int W;  // waves per workgroup
 };
+constexpr int32_t kExtFlag = (int32_t)0x80000000u;
+constexpr int kShiftBit = 18;
+constexpr int32_t kLowMask = (1 << kShiftBit) - 1;
 
 struct Block { int r, c, s; };
 

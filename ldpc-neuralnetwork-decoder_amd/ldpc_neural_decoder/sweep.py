@@ -1,0 +1,144 @@
+"""On-device SNR sweep: the reference's evaluation harness with nothing leaving the GPU.
+
+Replaces the per-(SNR, trial) Python loops of
+  ComparativeEvaluator._evaluate_traditional_decoder  training/comparative_evaluation.py:108-166
+  ComparativeEvaluator.evaluate_all                   training/comparative_evaluation.py:40-106
+  evaluate_message_gnn                                run_comparison_all.py:245-295
+with: fused channel kernel (all-zero codeword -> QPSK -> AWGN -> LLR, Philox keyed by the global
+frame index) -> decoder -> fused integer BER/FER counters.  The only host sync is at the end.
+
+Semantics kept from the reference:
+  * every trial transmits the all-zero codeword (:133) in a batch of `batch_size` frames;
+  * BER/FER per SNR = mean over trials of the per-trial means (equal batch sizes, so it is the
+    global mean of the integer counts);
+  * avg_iterations = mean over trials of the decoder's returned iteration count (batch-global
+    early stop: every frame of a trial reports the trial's count);
+  * results dict keyed as comparative_evaluation.py:86-104.
+
+Multi-GPU: trials are dealt round-robin to ranks (trial t -> rank t % world) so the batch-global
+early-stop rule still sees whole trials; the only collective is one SUM all-reduce of the
+(n_snr, 4) int64 counter matrix at the end (RCCL over xGMI, or gloo in the CPU tests).
+"""
+import torch
+
+COUNTER_FIELDS = ("bit_errors", "frame_errors", "frames", "iteration_sum")
+
+
+def run_sweep(decode_fn, llr_fn, snr_range, batch_size, num_trials, n, rank=0, world=1,
+              device="cpu", all_reduce=None):
+    """Generic sharded sweep.
+
+    llr_fn(batch, n, snr_db, frame_offset) -> (batch, n) float32 LLRs on `device`
+    decode_fn(llr, counters) -> None; adds [bit errs, frame errs, frames, iteration sum] into
+        the int64[4] `counters` (the flood decoders do it inside the kernel epilogue)
+    all_reduce(tensor) -> sums a tensor over ranks in place (None for a single process)
+    Returns the (len(snr_range), 4) int64 counter matrix (summed over ranks).
+    """
+    counts = torch.zeros((len(snr_range), 4), dtype=torch.int64, device=device)
+    for si, snr in enumerate(snr_range):
+        for t in range(rank, num_trials, world):
+            offset = (si * num_trials + t) * batch_size  # global frame index of the trial
+            llr = llr_fn(batch_size, n, snr, offset)
+            decode_fn(llr, counts[si])
+    if all_reduce is not None:
+        all_reduce(counts)
+    return counts
+
+
+def rates(counts, n):
+    """Counter matrix -> (ber list, fer list, avg_iterations list)."""
+    c = counts.double().cpu()
+    frames = c[:, 2].clamp(min=1)
+    ber = (c[:, 0] / (frames * n)).tolist()
+    fer = (c[:, 1] / frames).tolist()
+    avg_it = (c[:, 3] / frames).tolist()
+    return ber, fer, avg_it
+
+
+def _dist_all_reduce():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM), dist.get_rank(), dist.get_world_size()
+    return None, 0, 1
+
+
+class ComparativeEvaluator:
+    """comparative_evaluation.py:10-106 on the GPU (BP and min-sum: 50 iterations, batch-global
+    early stop, alpha 0.75, as :34-35).  ``neural_decoder`` may be a MessageGNNDecoder with its
+    TannerToMessageGraph passed as ``converter``."""
+
+    def __init__(self, H, neural_decoder=None, device=None, converter=None, seed=0):
+        from ldpc_neural_decoder import _native as N
+        from ldpc_neural_decoder.models import BeliefPropagationDecoder, MinSumScaledDecoder
+        self.device = N.device_of(None) if device is None else torch.device(device)
+        self.H = H
+        self.neural_decoder = neural_decoder
+        self.converter = converter
+        self.seed = seed
+        self.bp_decoder = BeliefPropagationDecoder(H, max_iterations=50, early_stopping=True)
+        self.ms_decoder = MinSumScaledDecoder(H, max_iterations=50, scaling_factor=0.75, early_stopping=True)
+        self.results = {}
+
+    def _llr_fn(self):
+        from ldpc_neural_decoder.utils.channel import awgn_llr
+        dev, seed = self.device, self.seed
+        return lambda b, n, snr, off: awgn_llr(b, n, snr, seed=seed, frame_offset=off, device=dev)
+
+    def _flood(self, dec, snr_range, batch_size, num_trials):
+        ar, rank, world = _dist_all_reduce()
+        n = self.H.shape[1]
+
+        def decode(llr, counters):
+            dec.decode(llr, out_dtype=torch.uint8, counters=counters)
+
+        counts = run_sweep(decode, self._llr_fn(), snr_range, batch_size, num_trials, n, rank, world,
+                           self.device, ar)
+        return rates(counts, n)
+
+    def _evaluate_traditional_decoder(self, decoder, snr_range, batch_size, num_trials, variable_bit_length=None):
+        return self._flood(decoder, snr_range, batch_size, num_trials)
+
+    def _evaluate_neural_decoder(self, snr_range, batch_size, num_trials):
+        ber, fer = evaluate_message_gnn(self.neural_decoder, self.converter, snr_range, batch_size,
+                                        num_trials, self.device, seed=self.seed)
+        return ber, fer
+
+    def evaluate_all(self, snr_range, batch_size=32, num_trials=100, variable_bit_length=None,
+                     check_index_tensor=None, var_index_tensor=None):
+        bp = self._flood(self.bp_decoder, snr_range, batch_size, num_trials)
+        ms = self._flood(self.ms_decoder, snr_range, batch_size, num_trials)
+        self.results = {
+            "snr_range": snr_range,
+            "belief_propagation": {"ber": bp[0], "fer": bp[1], "avg_iterations": bp[2]},
+            "min_sum_scaled": {"ber": ms[0], "fer": ms[1], "avg_iterations": ms[2]},
+        }
+        if self.neural_decoder is not None and self.converter is not None:
+            ber, fer = self._evaluate_neural_decoder(snr_range, batch_size, num_trials)
+            self.results["neural_decoder"] = {"ber": ber, "fer": fer}
+        return self.results
+
+
+def evaluate_message_gnn(decoder, converter, snr_range, batch_size, num_trials, device=None, seed=0):
+    """run_comparison_all.py:245-295 on the GPU -> (ber list, fer list)."""
+    from ldpc_neural_decoder import _native as N
+    from ldpc_neural_decoder.utils.channel import awgn_llr, count_errors
+    dev = N.device_of(None) if device is None else torch.device(device)
+    decoder = decoder.to(dev)
+    ar, rank, world = _dist_all_reduce()
+    n = converter.num_variables
+    io = converter.message_to_var_index().to(dev).to(torch.int32)
+    T = decoder.gnn_layers[0].message_type_embeddings.shape[0]
+    from ldpc_neural_decoder.models.message_gnn_decoder import _types_for
+    types = _types_for(converter.get_message_types(), len(converter.messages), T, dev)
+    vg, cg = converter.var_groups, converter.check_groups
+
+    def decode(llr, counters):
+        probs = decoder.native_forward(llr, io, types, vg, cg)
+        count_errors((probs > 0.5).to(torch.uint8), counters=counters)
+
+    def llr_fn(b, nn_, snr, off):
+        return awgn_llr(b, nn_, snr, seed=seed, frame_offset=off, device=dev)
+
+    counts = run_sweep(decode, llr_fn, snr_range, batch_size, num_trials, n, rank, world, dev, ar)
+    ber, fer, _ = rates(counts, n)
+    return ber, fer
