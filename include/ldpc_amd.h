@@ -64,6 +64,10 @@ int ldpc_graph_destroy(ldpc_graph *g);
 /* M, N, E, detected lifting Z, max check degree, max variable degree. */
 int ldpc_graph_info(const ldpc_graph *g, int *M, int *N, int64_t *E, int *Z, int *max_dc,
                     int *max_dv);
+/* Kernel variant for this graph: 0 = auto (a compile-time schedule when the graph is one of the
+ * reference's shipped codes, else table-driven), 1 = always table-driven.  Returns the variant
+ * in use (0 table-driven, 1 BG2 Z=4, 2 BG2 Z=32) or a negative error. */
+int ldpc_graph_set_variant(ldpc_graph *g, int variant);
 /* Check-major edge list of the graph (E entries each) -- the reference's message order. */
 int ldpc_graph_edges(const ldpc_graph *g, int32_t *h_edge_chk, int32_t *h_edge_var);
 

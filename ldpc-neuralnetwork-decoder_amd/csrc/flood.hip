@@ -24,7 +24,10 @@
 #include <cmath>
 #include <cstdint>
 
+#include <utility>
+
 #include "common.hpp"
+#include "gen/fixed_codes.hpp"
 #include "graph.hpp"
 
 namespace ldpc {
@@ -501,6 +504,231 @@ __global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *
     }
 }
 
+// ---------------------------------------------------------------- compile-time schedules
+// flood_fixed_kernel: the same algorithm for a graph whose schedule is known at compile time
+// (gen/fixed_codes.hpp: the reference's two codes).  Every slot offset, shift, degree and task
+// list is a constant: the iteration is straight-line code, LDS addresses fold into immediate
+// offsets, and no program words are decoded.  Bit-identical to flood_kernel.
+namespace {
+
+template <int I>
+using ic = std::integral_constant<int, I>;
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(ic<I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <class G, int ALGO, int R>
+__device__ __forceinline__ void fx_check_row(const Ctx &C, const Lane &L, int &errs) {
+    constexpr int P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+    constexpr int ZM4 = 4 * G::Z - 1;
+    float v[DC];
+    sfor<DC>([&](auto e) {
+        constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
+        constexpr int COL = G::ROW_COL[P0 + E], S4 = 4 * G::ROW_SHIFT[P0 + E];
+        if constexpr (SL >= 0)
+            v[E] = lds_rd(C.lds, SL * 256 + L.lane4);
+        else
+            v[E] = L.llr_at(COL * 4 * G::Z + ((L.k4 + S4) & ZM4));
+    });
+    auto emit = [&](auto e, float o) {
+        constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
+        if constexpr (SL >= 0) {
+            lds_wr(C.lds, SL * 256 + L.lane4, o);
+        } else {
+            if (C.direct_bits || C.ballots)
+                ext_decision(C, L, G::ROW_COL[P0 + E], 4 * G::ROW_SHIFT[P0 + E], v[E] + o, errs);
+        }
+    };
+    if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+        MinSumStats st;
+        sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
+        sfor<DC>([&](auto e) { emit(e, st.c2v(decltype(e)::value, v[decltype(e)::value], C.alpha)); });
+    } else {
+        float acc[DC];
+        float P = 1.0f;
+        sfor<DC>([&](auto jj) {
+            constexpr int J = decltype(jj)::value;
+            const float t = tanh_half(v[J]);
+            sfor<J>([&](auto e) { acc[decltype(e)::value] = acc[decltype(e)::value] * t; });
+            acc[J] = P;
+            P = P * t;
+        });
+        sfor<DC>([&](auto e) { emit(e, two_atanh(acc[decltype(e)::value])); });
+    }
+}
+
+template <class G, int COL>
+__device__ __forceinline__ void fx_var_col(const Ctx &C, const Lane &L, bool write, int &errs) {
+    constexpr int P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
+    constexpr int ZM4 = 4 * G::Z - 1;
+    float P = L.llr_at(COL * 4 * G::Z + L.k4);
+    if constexpr (DV > 0) {
+        float acc[DV];
+        sfor<DV>([&](auto jj) {
+            constexpr int J = decltype(jj)::value;
+            constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
+            const float c = lds_rd(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4));
+            sfor<J>([&](auto e) { acc[decltype(e)::value] = acc[decltype(e)::value] + c; });
+            acc[J] = P;
+            P = P + c;
+        });
+        if (write) {
+            sfor<DV>([&](auto jj) {
+                constexpr int J = decltype(jj)::value;
+                constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
+                lds_wr(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4), acc[J]);
+            });
+        }
+    }
+    if (C.direct_bits || C.ballots) var_decision(C, L, COL, P, errs);
+}
+
+template <class G, int COL>
+__device__ __forceinline__ void fx_init_col(const Ctx &C, const Lane &L) {
+    constexpr int P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
+    constexpr int ZM4 = 4 * G::Z - 1;
+    const float x = L.llr_at(COL * 4 * G::Z + L.k4);
+    sfor<DV>([&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
+        lds_wr(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4), x);
+    });
+}
+
+template <class G, int R>
+__device__ __forceinline__ int fx_parity_row(const Ctx &C, const Lane &L) {
+    constexpr int P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+    int p = 0;
+    sfor<DC>([&](auto e) {
+        constexpr int E = decltype(e)::value;
+        constexpr int COL = G::ROW_COL[P0 + E], S = G::ROW_SHIFT[P0 + E];
+        p ^= (int)((C.words[COL] >> (L.f * G::Z + ((L.k + S) & (G::Z - 1)))) & 1ull);
+    });
+    return p;
+}
+
+// the four per-wave bodies, selected once per phase by the (uniform) wave index
+template <class G, int WV, class F>
+__device__ __forceinline__ void fx_rows(F &&f) {
+    sfor<G::CHK_PTR[WV + 1] - G::CHK_PTR[WV]>([&](auto i) { f(ic<G::CHK_ROWS[G::CHK_PTR[WV] + decltype(i)::value]>{}); });
+}
+template <class G, int WV, class F>
+__device__ __forceinline__ void fx_cols(F &&f) {
+    sfor<G::VAR_PTR[WV + 1] - G::VAR_PTR[WV]>([&](auto i) { f(ic<G::VAR_COLS[G::VAR_PTR[WV] + decltype(i)::value]>{}); });
+}
+template <class G, class F>
+__device__ __forceinline__ void fx_by_wave(int wave, F &&f) {
+    static_assert(G::W == 4, "fixed schedules are generated for 4 waves");
+    switch (wave) {
+        case 0: f(ic<0>{}); break;
+        case 1: f(ic<1>{}); break;
+        case 2: f(ic<2>{}); break;
+        default: f(ic<3>{}); break;
+    }
+}
+
+}  // namespace
+
+template <class G, int ALGO, int ES>
+__global__ __launch_bounds__(256, 4) void flood_fixed_kernel(FloodTables T, const float *__restrict__ llr,
+                                                          int64_t B, int max_iter, float alpha,
+                                                          int out_dtype, void *__restrict__ bits,
+                                                          int32_t *__restrict__ iters_out,
+                                                          uint64_t *__restrict__ counters,
+                                                          int32_t *__restrict__ batch_iters,
+                                                          uint64_t *__restrict__ ws_words,
+                                                          uint32_t *__restrict__ ws_valid, int nvw) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const Lane L0 = make_lane(T, llr, B);
+    const Lane &L = L0;
+    const int nf = (int)min<int64_t>((int64_t)T.FG, B - (int64_t)blockIdx.x * T.FG);
+    const uint64_t exist = nf >= 64 ? ~0ull : ((1ull << nf) - 1ull);
+
+    Ctx C;
+    C.T = T;
+    C.lds = lds;
+    C.words = reinterpret_cast<uint64_t *>(lds + (size_t)G::NSLOTS * 256);
+    C.alpha = alpha;
+    C.out_dtype = out_dtype;
+    C.bits = bits;
+    C.direct_bits = false;
+    C.ballots = ES != LDPC_ES_OFF;
+
+    fx_by_wave<G>(wave, [&](auto wv) {
+        fx_cols<G, decltype(wv)::value>([&](auto col) { fx_init_col<G, decltype(col)::value>(C, L); });
+    });
+    __syncthreads();
+
+    int errs = 0;
+    int my_iters = max_iter;
+    uint64_t done = 0;
+    for (int it = 0; it < max_iter; ++it) {
+        const bool last = it == max_iter - 1;
+        C.direct_bits = (ES == LDPC_ES_OFF) && last;
+        // Every address below is loop-invariant; left alone the compiler hoists all of them
+        // out of the iteration loop and runs out of VGPRs.  An empty asm "redefines" the lane
+        // bases each iteration so the addresses are rebuilt next to their use.
+        Lane L = L0;
+        asm volatile("" : "+v"(L.k4), "+v"(L.fz4), "+v"(L.lane4));
+        asm volatile("" : "+v"(L.llr_row), "+v"(L.frame));
+        fx_by_wave<G>(wave, [&](auto wv) {
+            fx_rows<G, decltype(wv)::value>([&](auto r) { fx_check_row<G, ALGO, decltype(r)::value>(C, L, errs); });
+        });
+        __syncthreads();
+        if (ES != LDPC_ES_OFF && tid == 0) C.words[G::Nb] = 0;
+        fx_by_wave<G>(wave, [&](auto wv) {
+            fx_cols<G, decltype(wv)::value>([&](auto col) { fx_var_col<G, decltype(col)::value>(C, L, !last, errs); });
+        });
+        __syncthreads();
+        if constexpr (ES != LDPC_ES_OFF) {
+            int inv = 0;
+            fx_by_wave<G>(wave, [&](auto wv) {
+                fx_rows<G, decltype(wv)::value>([&](auto r) { inv |= fx_parity_row<G, decltype(r)::value>(C, L); });
+            });
+            const uint64_t m = __ballot(inv);
+            if (L.lane == 0 && m) atomicOr((unsigned long long *)&C.words[G::Nb], (unsigned long long)m);
+            __syncthreads();
+            const uint64_t vmask = frame_valid_mask(C.words[G::Nb], G::Z, T.FG) & exist;
+            if constexpr (ES == LDPC_ES_BATCH) {
+                if (L.valid && L.k == 0 && ((vmask >> L.f) & 1ull))
+                    ws_valid[L.frame * nvw + (it >> 5)] |= 1u << (it & 31);
+                uint64_t *dst = ws_words + ((int64_t)blockIdx.x * max_iter + it) * G::Nb;
+                for (int c = tid; c < G::Nb; c += blockDim.x) dst[c] = C.words[c];
+            } else {
+                const uint64_t newly = vmask & ~done;
+                if (newly) {
+                    emit_from_words(C, L, C.words, newly, wave, errs);
+                    if ((newly >> L.f) & 1ull) my_iters = it + 1;
+                    if (iters_out && L.valid && L.k == 0 && ((newly >> L.f) & 1ull)) iters_out[L.frame] = it + 1;
+                    done |= newly;
+                }
+            }
+            __syncthreads();
+            if (ES == LDPC_ES_FRAME && done == exist) break;
+        }
+    }
+    if constexpr (ES == LDPC_ES_FRAME) {
+        const uint64_t rest = exist & ~done;
+        if (rest) {
+            emit_from_words(C, L, C.words, rest, wave, errs);
+            if (iters_out && L.valid && L.k == 0 && ((rest >> L.f) & 1ull)) iters_out[L.frame] = max_iter;
+        }
+    }
+    if constexpr (ES == LDPC_ES_OFF) {
+        if (iters_out && L.valid && L.k == 0) iters_out[L.frame] = max_iter;
+    }
+    if constexpr (ES != LDPC_ES_BATCH) {
+        if (counters || batch_iters) reduce_counters(lds, L, errs, my_iters, nf, G::Z, counters, batch_iters);
+    }
+}
+
 // ---------------------------------------------------------------- batch-global early stop
 __global__ void batch_and_kernel(const uint32_t *__restrict__ ws_valid, int64_t B, int nvw,
                                  uint32_t *__restrict__ all_words) {
@@ -581,6 +809,8 @@ int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter,
                  uint64_t *ws_words, uint32_t *ws_valid, int nvw, hipStream_t s) {
     const size_t lds = flood_lds_bytes(g, ES);
     auto kern = flood_kernel<ALGO, ES>;
+    if (g->fixed_id == 1) kern = flood_fixed_kernel<fixed::BG2_Z4, ALGO, ES>;
+    if (g->fixed_id == 2) kern = flood_fixed_kernel<fixed::BG2_Z32, ALGO, ES>;
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t nwg = (B + g->FG - 1) / g->FG;

@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "common.hpp"
+#include "gen/fixed_codes.hpp"
 #include "graph.hpp"
 
 namespace ldpc {
@@ -184,6 +185,19 @@ int build(ldpc_graph *g) {
     t.nslots = nslots;
     t.W = W;
 
+    // compile-time schedule available for this exact graph (and the default 4 waves)?
+    auto matches = [&](auto tag) {
+        using G = decltype(tag);
+        if (g->Z != G::Z || Mb != G::Mb || Nb != G::Nb || (int)blocks.size() != G::NBLOCKS || W != G::W) return false;
+        for (int i = 0; i < G::NBLOCKS; ++i)
+            if (blocks[i].r != G::BLK_ROW[i] || blocks[i].c != G::BLK_COL[i] || blocks[i].s != G::BLK_SHIFT[i])
+                return false;
+        return true;
+    };
+    g->fixed_match = matches(fixed::BG2_Z4{}) ? 1 : (matches(fixed::BG2_Z32{}) ? 2 : 0);
+    const char *fx = std::getenv("LDPC_FLOOD_FIXED");
+    g->fixed_id = (fx && std::atoi(fx) == 0) ? 0 : g->fixed_match;
+
     LDPC_HIP(hipDeviceSynchronize());
     return LDPC_OK;
 }
@@ -261,6 +275,13 @@ extern "C" int ldpc_graph_info(const ldpc_graph *g, int *M, int *N, int64_t *E, 
     if (max_dc) *max_dc = g->max_dc;
     if (max_dv) *max_dv = g->max_dv;
     return LDPC_OK;
+}
+
+extern "C" int ldpc_graph_set_variant(ldpc_graph *g, int variant) {
+    if (!g) return fail(LDPC_EINVAL, "graph is NULL");
+    if (variant < 0 || variant > 1) return fail(LDPC_EINVAL, "variant must be 0 (auto) or 1 (table-driven)");
+    g->fixed_id = variant == 1 ? 0 : g->fixed_match;
+    return g->fixed_id;
 }
 
 extern "C" int ldpc_graph_edges(const ldpc_graph *g, int32_t *h_edge_chk, int32_t *h_edge_var) {

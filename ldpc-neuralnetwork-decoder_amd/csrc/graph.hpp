@@ -56,4 +56,6 @@ struct ldpc_graph {
     std::vector<ldpc::Block> blocks;            // row-major (r asc, c asc)
     int32_t *d_tab = nullptr;
     ldpc::FloodTables ft{};
+    int fixed_id = 0;      // 0: table-driven kernel; 1/2: compile-time schedule BG2_Z4 / BG2_Z32
+    int fixed_match = 0;   // what the graph matched (kept when the variant is forced off)
 };

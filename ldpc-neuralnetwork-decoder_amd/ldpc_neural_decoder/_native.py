@@ -29,6 +29,7 @@ SIGNATURES = {
     "ldpc_graph_destroy": (ctypes.c_int, [_P]),
     "ldpc_graph_info": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "ldpc_graph_edges": (ctypes.c_int, [_P, _P, _P]),
+    "ldpc_graph_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
     "ldpc_flood_workspace_size": (_I64, [_P, _I64, ctypes.c_int, ctypes.c_int]),
     "ldpc_flood_decode": (ctypes.c_int, [_P, ctypes.c_int, _P, _I64, ctypes.c_int, _F32, ctypes.c_int,
                                          ctypes.c_int, _P, _P, _P, _P, _P, _I64, _P]),
@@ -115,6 +116,11 @@ class NativeGraph:
     @property
     def handle(self):
         return self._h
+
+    def set_variant(self, variant):
+        """0 = auto (compile-time schedule for the reference's codes), 1 = table-driven.
+        Returns the kernel in use: 0 table-driven, 1 BG2 Z=4, 2 BG2 Z=32."""
+        return check(lib().ldpc_graph_set_variant(self._h, int(variant)))
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -32,10 +32,25 @@ def H32():
 
 
 def test_lifting_detected(cuda, H4, H32):
-    for H, z in ((H4, 4), (H32, 32)):
+    for H, z, fixed in ((H4, 4, 1), (H32, 32, 2)):
         dec = MinSumScaledDecoder(H, max_iterations=5)
         g = dec.graph(cuda)
         assert g.Z == z and g.E == 788 * z // 4 and g.max_dc == 10 and g.max_dv == 23
+        assert g.set_variant(0) == fixed  # the reference's codes get the compile-time schedule
+
+
+@pytest.mark.parametrize("algo", ["minsum", "bp"])
+@pytest.mark.parametrize("es", [False, True, "frame"])
+def test_fixed_and_table_driven_agree(cuda, H32, algo, es):
+    """The compile-time-schedule kernel and the table-driven kernel are bit-identical."""
+    llr = torch.from_numpy(golden("trad_z32_low.npz")["llrs"].reshape(-1, 1664)).to(cuda)
+    mk = (lambda: MinSumScaledDecoder(H32, 7, 0.75, early_stopping=es)) if algo == "minsum" \
+        else (lambda: BeliefPropagationDecoder(H32, 7, early_stopping=es))
+    d_fix, d_tab = mk(), mk()
+    assert d_tab.graph(cuda).set_variant(1) == 0
+    b1, i1, f1 = d_fix.decode(llr, return_frame_iters=True)
+    b2, i2, f2 = d_tab.decode(llr, return_frame_iters=True)
+    assert torch.equal(b1, b2) and i1 == i2 and torch.equal(f1, f2)
 
 
 @pytest.mark.parametrize("alpha,key", [(0.75, "ms_a0.75"), (0.8, "ms_a0.8")])
