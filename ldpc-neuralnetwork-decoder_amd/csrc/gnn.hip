@@ -23,6 +23,7 @@
 //   gnn_output_kernel       probs = sigmoid(var_sum + llr).
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -43,7 +44,13 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMfmaH = 64;
-constexpr int kMlpThreads = 256;
+int mlp_threads() {
+    static int t = [] {
+        const char *e = std::getenv("LDPC_GNN_MLP_THREADS");
+        return (e && std::atoi(e) == 512) ? 512 : 256;
+    }();
+    return t;
+}
 
 struct GnnLayer {
     // input features: x_in (B, E, H) or, for layer 0, the embedding of the LLRs
@@ -101,6 +108,50 @@ __global__ __launch_bounds__(256) void gnn_group_mean_kernel(GnnLayer P, int H) 
     }
 }
 
+// H = 64 fp32: 16 lanes per group (float4 each), 4 groups per wave, members unrolled by 4 so
+// every lane keeps 4 x 16 B in flight (the plain kernel above is latency-bound at ~1.7 TB/s).
+__global__ __launch_bounds__(256) void gnn_group_mean_h64_kernel(GnnLayer P) {
+    const int lane = threadIdx.x & 63, q = lane & 15;
+    const int64_t gid = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
+    const int64_t G = P.Gv + P.Gc;
+    if (gid >= P.B * G) return;
+    const int64_t b = gid / G;
+    const int g = (int)(gid - b * G);
+    const bool isv = g < P.Gv;
+    const int gg = isv ? g : g - P.Gv;
+    const int32_t *ptr = isv ? P.vg_ptr : P.cg_ptr;
+    const int32_t *mem = isv ? P.vg_mem : P.cg_mem;
+    const float inv = isv ? P.inv_v[gg] : P.inv_c[gg];
+    float4 *dst = reinterpret_cast<float4 *>(isv ? P.Mv + (b * P.Gv + gg) * 64 : P.Mc + (b * P.Gc + gg) * 64) + q;
+    const int p0 = ptr[gg], p1 = ptr[gg + 1];
+    auto feat = [&](int m) -> float4 {
+        const float4 e = reinterpret_cast<const float4 *>(P.emb + P.msg_type[m] * 64)[q];
+        float4 x;
+        if (P.x_in) {
+            x = reinterpret_cast<const float4 *>(P.x_in + (b * P.E + m) * 64)[q];
+        } else {
+            const float l = P.llr[b * P.N + P.msg_var[m]];
+            const float4 w = reinterpret_cast<const float4 *>(P.w_in)[q], bb = reinterpret_cast<const float4 *>(P.b_in)[q];
+            x = make_float4(l * w.x + bb.x, l * w.y + bb.y, l * w.z + bb.z, l * w.w + bb.w);
+        }
+        return make_float4(x.x + e.x, x.y + e.y, x.z + e.z, x.w + e.w);
+    };
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    int p = p0;
+    for (; p + 4 <= p1; p += 4) {
+        const float4 a = feat(mem[p]), bq = feat(mem[p + 1]), c = feat(mem[p + 2]), d = feat(mem[p + 3]);
+        acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+        acc.x += bq.x; acc.y += bq.y; acc.z += bq.z; acc.w += bq.w;
+        acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
+        acc.x += d.x; acc.y += d.y; acc.z += d.z; acc.w += d.w;
+    }
+    for (; p < p1; ++p) {
+        const float4 a = feat(mem[p]);
+        acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    *dst = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+}
+
 // ------------------------------------------------------------------------ fused MLP, H = 64
 // LDS image (floats): W1vT[128][64] W2vT[64][64] W1cT[128][64] W2cT[64][64]
 //                     b1v b2v b1c b2c wo [64 each]  emb[T][64]
@@ -111,7 +162,8 @@ constexpr int kOffEmb = kOffBias + 5 * 64;
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
-__global__ __launch_bounds__(kMlpThreads, 1) void gnn_mlp_mfma_kernel(GnnLayer P) {
+template <int kMlpThreads>
+__global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int H = kMfmaH;
     const int tid = threadIdx.x;
@@ -178,6 +230,9 @@ __global__ __launch_bounds__(kMlpThreads, 1) void gnn_mlp_mfma_kernel(GnnLayer P
             grp = reinterpret_cast<const float4 *>(P.Mc + (b * P.Gc + P.cgroup[m]) * H);
         }
         f32x16 y0 = {}, y1 = {};
+        // per-lane weight offsets, made opaque so the loop-invariant LDS reads are not hoisted
+        int w1lane = half * 64 * 64 + j, w2lane = j;
+        asm volatile("" : "+v"(w1lane), "+v"(w2lane));
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             if (side == 1 && half == 1) {
@@ -194,9 +249,9 @@ __global__ __launch_bounds__(kMlpThreads, 1) void gnn_mlp_mfma_kernel(GnnLayer P
             f32x16 h0 = {}, h1 = {};
 #pragma unroll
             for (int kk = 0; kk < 64; ++kk) {
-                const float *wr = W1 + (half * 64 + kk) * 64;
-                h0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[j], in[kk], h0, 0, 0, 0);
-                h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32 + j], in[kk], h1, 0, 0, 0);
+                const float *wr = W1 + w1lane + kk * 64;
+                h0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[0], in[kk], h0, 0, 0, 0);
+                h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32], in[kk], h1, 0, 0, 0);
             }
             // bias + ReLU; register r of row tile rt holds unit 32*rt + crow(r, half)
 #pragma unroll
@@ -208,12 +263,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void gnn_mlp_mfma_kernel(GnnLayer P
             // crow(r,0) (half 0) with crow(r,1) (half 1) -- exactly the registers each lane holds
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float *wa = W2 + (crow(r, half)) * 64;
-                const float *wb = W2 + (32 + crow(r, half)) * 64;
-                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[j], h0[r], y0, 0, 0, 0);
-                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[32 + j], h0[r], y1, 0, 0, 0);
-                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[j], h1[r], y0, 0, 0, 0);
-                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[32 + j], h1[r], y1, 0, 0, 0);
+                const float *wa = W2 + w2lane + (crow(r, half)) * 64;
+                const float *wb = W2 + w2lane + (32 + crow(r, half)) * 64;
+                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[0], h0[r], y0, 0, 0, 0);
+                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[32], h0[r], y1, 0, 0, 0);
+                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[0], h1[r], y0, 0, 0, 0);
+                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[32], h1[r], y1, 0, 0, 0);
             }
         }
         // epilogue: + b2v + b2c (+ residual); lane holds units 32*ot + crow(r, half) of message j
@@ -246,6 +301,206 @@ __global__ __launch_bounds__(kMlpThreads, 1) void gnn_mlp_mfma_kernel(GnnLayer P
         if (P.last) {
             part += __shfl_xor(part, 32, 64);
             if (ok && half == 0) atomicAdd(&P.var_sum[b * P.N + P.msg_var[m]], part + bo);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------ bf16 path (H = 64)
+// precision 1: features x and group means stored as bf16 (half the HBM bytes), MLP operands
+// bf16 on v_mfma_f32_32x32x16_bf16, every accumulation (group sums, GEMMs, bias, residual) fp32.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+struct GnnLayerBf16 {
+    GnnLayer P;          // fp32 pointers unused for x_in / x_out / Mv / Mc
+    const __bf16 *x_in;  // (B, E, 64) or null for layer 0
+    __bf16 *x_out;
+    __bf16 *Mv, *Mc;     // (B, G, 64)
+};
+
+// one wave = two groups (lane half h -> group 2w + h), each lane two feature units
+__global__ __launch_bounds__(256) void gnn_group_mean_bf16_kernel(GnnLayerBf16 Q) {
+    const GnnLayer &P = Q.P;
+    const int lane = threadIdx.x & 63, h = lane >> 5, u = 2 * (lane & 31);
+    const int64_t gid = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + h;
+    const int64_t G = P.Gv + P.Gc;
+    if (gid >= P.B * G) return;
+    const int64_t b = gid / G;
+    const int g = (int)(gid - b * G);
+    const bool isv = g < P.Gv;
+    const int gg = isv ? g : g - P.Gv;
+    const int32_t *ptr = isv ? P.vg_ptr : P.cg_ptr;
+    const int32_t *mem = isv ? P.vg_mem : P.cg_mem;
+    const float inv = isv ? P.inv_v[gg] : P.inv_c[gg];
+    __bf16 *dst = (isv ? Q.Mv + (b * P.Gv + gg) * 64 : Q.Mc + (b * P.Gc + gg) * 64) + u;
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll 4
+    for (int p = ptr[gg]; p < ptr[gg + 1]; ++p) {
+        const int m = mem[p];
+        const float *e = P.emb + P.msg_type[m] * 64 + u;
+        float x0, x1;
+        if (Q.x_in) {
+            const bf16x2 v = *reinterpret_cast<const bf16x2 *>(Q.x_in + (b * P.E + m) * 64 + u);
+            x0 = (float)v[0];
+            x1 = (float)v[1];
+        } else {
+            const float l = P.llr[b * P.N + P.msg_var[m]];
+            x0 = l * P.w_in[u] + P.b_in[u];
+            x1 = l * P.w_in[u + 1] + P.b_in[u + 1];
+        }
+        s0 += x0 + e[0];
+        s1 += x1 + e[1];
+    }
+    bf16x2 o;
+    o[0] = (__bf16)(s0 * inv);
+    o[1] = (__bf16)(s1 * inv);
+    *reinterpret_cast<bf16x2 *>(dst) = o;
+}
+
+// LDS image (bytes): W1v, W1c as bf16 [64 u][136] (row = 128 k + 8 pad: conflict-free b128 reads)
+//                    W2v, W2c as bf16 [64 o][72], columns permuted to GEMM1's accumulator order
+//                    b1v b2v b1c b2c wo fp32 [64 each], emb fp32 [T][64]
+constexpr int kB_W1 = 64 * 136 * 2, kB_W2 = 64 * 72 * 2;
+constexpr int kB_OffW1v = 0, kB_OffW1c = kB_W1, kB_OffW2v = 2 * kB_W1, kB_OffW2c = 2 * kB_W1 + kB_W2;
+constexpr int kB_OffBias = 2 * kB_W1 + 2 * kB_W2;   // bytes
+constexpr int kB_OffEmb = kB_OffBias + 5 * 64 * 4;
+
+// unit held by element kk of k-step s of row tile rt in GEMM1's accumulator (cdna_hip §3)
+__host__ __device__ __forceinline__ int acc_unit(int rt, int s, int kk) {
+    return 32 * rt + 16 * s + 8 * ((kk & 7) >> 2) + 4 * (kk >> 3) + (kk & 3);
+}
+
+__device__ __forceinline__ bf16x8 ld_bf16x8(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
+
+// relu(acc[8s .. 8s+7] + bias) as one bf16 fragment (whole-vector construction keeps it in VGPRs)
+__device__ __forceinline__ bf16x8 relu_pack(const f32x16 &acc, int s, const float *b1, int ubase, int h) {
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = 8 * s + i;
+        const int u = ubase + (r & 3) + 8 * (r >> 2) + 4 * h;
+        o[i] = (__bf16)fmaxf(acc[r] + b1[u], 0.0f);
+    }
+    return o;
+}
+
+__global__ __launch_bounds__(256, 2) void gnn_mlp_bf16_kernel(GnnLayerBf16 Q) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const GnnLayer &P = Q.P;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 64 * 128; i += 256) {
+        const int o = i >> 7, k = i & 127;
+        reinterpret_cast<__bf16 *>(smem + kB_OffW1v)[o * 136 + k] = (__bf16)P.w1v[i];
+        reinterpret_cast<__bf16 *>(smem + kB_OffW1c)[o * 136 + k] = (__bf16)P.w1c[i];
+    }
+    for (int i = tid; i < 64 * 64; i += 256) {
+        const int o = i >> 6, q = i & 63;
+        const int rt = q >> 5, s = (q >> 4) & 1, kk = q & 15;
+        const int u = acc_unit(rt, s, kk);
+        reinterpret_cast<__bf16 *>(smem + kB_OffW2v)[o * 72 + q] = (__bf16)P.w2v[o * 64 + u];
+        reinterpret_cast<__bf16 *>(smem + kB_OffW2c)[o * 72 + q] = (__bf16)P.w2c[o * 64 + u];
+    }
+    float *bias = reinterpret_cast<float *>(smem + kB_OffBias);
+    if (tid < 64) {
+        bias[tid] = P.b1v[tid];
+        bias[64 + tid] = P.b2v[tid];
+        bias[128 + tid] = P.b1c[tid];
+        bias[192 + tid] = P.b2c[tid];
+        bias[256 + tid] = P.last ? P.wo[tid] : 0.0f;
+    }
+    float *embl = reinterpret_cast<float *>(smem + kB_OffEmb);
+    for (int i = tid; i < P.T * 64; i += 256) embl[i] = P.emb[i];
+    __syncthreads();
+
+    const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
+    const int64_t R = P.B * P.E;
+    const int64_t ntiles = (R + 31) / 32;
+    const float bo = P.last ? P.bo[0] : 0.0f;
+    for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+        const int64_t row = t * 32 + j;
+        const bool ok = row < R;
+        const int64_t rr = ok ? row : R - 1;
+        const int64_t b = rr / P.E, m = rr - b * P.E;
+        // B fragments: k-step s < 4 -> features 16s + 8h .. +7 of c; s >= 4 -> of a (var) / b (chk)
+        const float *e = embl + P.msg_type[m] * 64;
+        const char *ma = reinterpret_cast<const char *>(Q.Mv + (b * P.Gv + P.vgroup[m]) * 64);
+        const char *mb = reinterpret_cast<const char *>(Q.Mc + (b * P.Gc + P.cgroup[m]) * 64);
+        const float l = Q.x_in ? 0.0f : P.llr[b * P.N + P.msg_var[m]];
+        auto cfrag = [&](int s) {
+            const int f0 = 16 * s + 8 * h;
+            bf16x8 o;
+            if (Q.x_in) {
+                const bf16x8 xv = ld_bf16x8(reinterpret_cast<const char *>(Q.x_in + rr * 64 + f0));
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((float)xv[i] + e[f0 + i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((l * P.w_in[f0 + i] + P.b_in[f0 + i]) + e[f0 + i]);
+            }
+            return o;
+        };
+        const bf16x8 c0 = cfrag(0), c1 = cfrag(1), c2 = cfrag(2), c3 = cfrag(3);
+        f32x16 y0 = {}, y1 = {};
+        // the weight-fragment addresses are loop-invariant: without this the compiler hoists all
+        // 48 fragment loads (192 VGPRs) out of the tile loop and spills
+        int wbase = j * 272 + 16 * h, w2base = j * 144 + 16 * h;
+        asm volatile("" : "+v"(wbase), "+v"(w2base));
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const char *W1 = smem + (side == 0 ? kB_OffW1v : kB_OffW1c);
+            const char *W2 = smem + (side == 0 ? kB_OffW2v : kB_OffW2c);
+            const float *b1 = bias + (side == 0 ? 0 : 128);
+            const char *g = side == 0 ? ma : mb;
+            f32x16 h0 = {}, h1 = {};
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const bf16x8 bop = s == 0 ? c0 : s == 1 ? c1 : s == 2 ? c2 : s == 3 ? c3
+                                 : ld_bf16x8(g + 2 * (16 * (s - 4) + 8 * h));
+                const int kb = wbase + 32 * s;
+                h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W1 + kb), bop, h0, 0, 0, 0);
+                h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W1 + 32 * 272 + kb), bop, h1, 0, 0, 0);
+            }
+            const bf16x8 p00 = relu_pack(h0, 0, b1, 0, h), p01 = relu_pack(h0, 1, b1, 0, h);
+            const bf16x8 p10 = relu_pack(h1, 0, b1, 32, h), p11 = relu_pack(h1, 1, b1, 32, h);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rt = q >> 1, s = q & 1;
+                const bf16x8 bop = q == 0 ? p00 : q == 1 ? p01 : q == 2 ? p10 : p11;
+                const int qb = w2base + 2 * (32 * rt + 16 * s);
+                y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W2 + qb), bop, y0, 0, 0, 0);
+                y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W2 + 32 * 144 + qb), bop, y1, 0, 0, 0);
+            }
+        }
+        const float *b2v = bias + 64, *b2c = bias + 192, *wo = bias + 256;
+        float part = 0.0f;
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int o0 = 32 * ot + 8 * q + 4 * h;
+                float v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = ((ot == 0 ? y0[4 * q + i] : y1[4 * q + i]) + b2v[o0 + i]) + b2c[o0 + i];
+                if (P.residual) {
+                    const bf16x4 xr = *reinterpret_cast<const bf16x4 *>(Q.x_in + rr * 64 + o0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[i] += (float)xr[i];
+                }
+                if (P.last) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) part += v[i] * wo[o0 + i];
+                } else if (ok) {
+                    bf16x4 o;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[i] = (__bf16)v[i];
+                    *reinterpret_cast<bf16x4 *>(Q.x_out + row * 64 + o0) = o;
+                }
+            }
+        }
+        if (P.last) {
+            part += __shfl_xor(part, 32, 64);
+            if (ok && h == 0) atomicAdd(&P.var_sum[b * P.N + P.msg_var[m]], part + bo);
         }
     }
 }
@@ -313,12 +568,13 @@ struct Ws {
     int64_t bytes;
 };
 
-Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, void *base) {
+Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precision, void *base) {
     Ws w{};
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
-    const int64_t xb = layers > 1 ? al(B * p->E * H * 4) : 0;
+    const int64_t es = precision == 1 ? 2 : 4;  // bytes per stored feature
+    const int64_t xb = layers > 1 ? al(B * p->E * H * es) : 0;
     const int64_t xb2 = layers > 2 ? xb : 0;
-    const int64_t mv = al(B * (int64_t)p->Gv * H * 4), mc = al(B * (int64_t)p->Gc * H * 4);
+    const int64_t mv = al(B * (int64_t)p->Gv * H * es), mc = al(B * (int64_t)p->Gc * H * es);
     const int64_t vs = al(B * (int64_t)N * 4);
     char *c = static_cast<char *>(base);
     w.xa = reinterpret_cast<float *>(c);
@@ -419,8 +675,7 @@ extern "C" int64_t ldpc_gnn_weights_size(int hidden, int types, int layers) {
 extern "C" int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers,
                                            int precision) {
     if (!p || hidden <= 0 || N <= 0 || B < 0 || layers <= 0) return fail(LDPC_EINVAL, "bad arguments");
-    (void)precision;
-    return carve(p, hidden, N, B, layers, nullptr).bytes;
+    return carve(p, hidden, N, B, layers, precision, nullptr).bytes;
 }
 
 extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
@@ -429,11 +684,12 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
                                 void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     if (hidden <= 0 || types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
-    if (precision != 0) return fail(LDPC_EUNSUPPORTED, "precision 1 (bf16) not built yet");
+    if (precision != 0 && precision != 1) return fail(LDPC_EINVAL, "precision must be 0 (fp32) or 1 (bf16)");
+    if (precision == 1 && hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "bf16 path needs hidden_dim 64");
     if (B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
     const int H = hidden;
-    Ws w = carve(p, H, N, B, layers, d_work);
+    Ws w = carve(p, H, N, B, layers, precision, d_work);
     if (!d_work || work_bytes < w.bytes)
         return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -461,9 +717,10 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
     if (!mfma && H > 128) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be 64 (MFMA path) or <= 128");
     const size_t mfma_lds = (size_t)(kOffEmb + types * 64) * 4;
     if (mfma && mfma_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
-    if (mfma)
-        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp_mfma_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mfma_lds));
+    const int mt = mlp_threads();
+    const void *mfma_fn = mt == 512 ? reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<512>)
+                                    : reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<256>);
+    if (mfma) LDPC_HIP(hipFuncSetAttribute(mfma_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mfma_lds));
     const float *x_in = nullptr;
     for (int l = 0; l < layers; ++l) {
         const float *lw = d_weights + 2 * H + (int64_t)l * layer_floats(H, types);
@@ -484,13 +741,39 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
         L.x_out = (l % 2 == 0) ? w.xa : w.xb;
         L.var_sum = w.var_sum;
         const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
-        hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);
+        if (precision == 1) {
+            GnnLayerBf16 Q{};
+            Q.P = L;
+            Q.x_in = reinterpret_cast<const __bf16 *>(x_in);
+            Q.x_out = reinterpret_cast<__bf16 *>(L.x_out);
+            Q.Mv = reinterpret_cast<__bf16 *>(w.Mv);
+            Q.Mc = reinterpret_cast<__bf16 *>(w.Mc);
+            hipLaunchKernelGGL(gnn_group_mean_bf16_kernel, dim3((unsigned)((waves + 7) / 8)), dim3(256), 0, s, Q);
+            LDPC_CHECK_LAUNCH("gnn_group_mean_bf16_kernel");
+            const size_t lds = (size_t)kB_OffEmb + (size_t)types * 64 * 4;
+            if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
+            LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp_bf16_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            const int64_t tiles = (B * p->E + 31) / 32;
+            const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)g_num_cus * 2);
+            hipLaunchKernelGGL(gnn_mlp_bf16_kernel, dim3(grid), dim3(256), lds, s, Q);
+            LDPC_CHECK_LAUNCH("gnn_mlp_bf16_kernel");
+            x_in = L.x_out;
+            continue;
+        }
+        if (H == 64)
+            hipLaunchKernelGGL(gnn_group_mean_h64_kernel, dim3((unsigned)((waves + 15) / 16)), dim3(256), 0, s, L);
+        else
+            hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);
         LDPC_CHECK_LAUNCH("gnn_group_mean_kernel");
         if (mfma) {
             const int64_t tiles = (B * p->E + 31) / 32;
-            const int64_t want = (tiles + kMlpThreads / 64 - 1) / (kMlpThreads / 64);
+            const int64_t want = (tiles + mt / 64 - 1) / (mt / 64);
             const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus);
-            hipLaunchKernelGGL(gnn_mlp_mfma_kernel, dim3(grid), dim3(kMlpThreads), mfma_lds, s, L);
+            if (mt == 512)
+                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<512>, dim3(grid), dim3(512), mfma_lds, s, L);
+            else
+                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<256>, dim3(grid), dim3(256), mfma_lds, s, L);
             LDPC_CHECK_LAUNCH("gnn_mlp_mfma_kernel");
         } else {
             const int64_t want = (B * p->E + 3) / 4;
