@@ -14,6 +14,7 @@ Workloads (BASELINE.json configs):
   bp-z4       cfg1 sizes on the GPU: BG2 Z=4, BP, 5 iterations, B=64 (x --batch)
   gnn-z4      cfg2: BG2 Z=4, MessageGNN 5 layers, H=64, T=4, B=4096, fp32
   gnn-z32     cfg4 per GPU: BG2 Z=32, MessageGNN 10 layers, H=64, T=32, B=32768/GPU, fp32
+  gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate)
 """
 import argparse
 import json
@@ -31,6 +32,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X fp32 matrix (spec), same guide
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X bf16 dense MFMA (spec, no sparsity)
 
 WORKLOADS = {
     # name: (decoder, Z, iterations, default batch per GPU, SNR dB)
@@ -38,6 +40,8 @@ WORKLOADS = {
     "bp-z4": ("bp", 4, 5, 64, 2.0),
     "gnn-z4": ("gnn", 4, 5, 4096, 2.0),
     "gnn-z32": ("gnn", 32, 10, 32768, 2.0),
+    "gnn-z32-bf16": ("gnn-bf16", 32, 15, 32768, 2.0),
+    "gnn-z4-bf16": ("gnn-bf16", 4, 5, 4096, 2.0),
 }
 
 
@@ -45,6 +49,21 @@ def flood_bytes_per_cw(E, N, iters):
     """every edge message read + written once per iteration (fp32), every APP read
     + written once per iteration, the LLR read once (4N) and the decision written once (N)."""
     return iters * 8 * (E + N) + 5 * N
+
+
+def roofline_notes(kind, B, n, kern_ms, traffic):
+    """The flood decoder keeps every message in LDS, so SURVEY §8(d)'s streaming byte model
+    (algorithmic bytes) overstates what reaches HBM; report the compulsory bytes beside it."""
+    if kind not in ("minsum", "bp"):
+        return None
+    comp = 5 * n * B  # LLR read (4N) + uint8 decision written (N)
+    return {"model": "SURVEY 8(d) algorithmic bytes = messages streamed through HBM every iteration; "
+                     "this decoder is LDS-resident, hence frac > 1",
+            "compulsory_bytes_per_launch": comp,
+            "compulsory_GBps": comp / (kern_ms * 1e-3) / 1e9,
+            "compulsory_frac_of_hbm_peak": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "traffic_over_compulsory": (traffic / comp) if traffic else None,
+            "actual_bound": "LDS/VALU issue (profiles/r01_pmc_minsum_z32.json)"}
 
 
 def parse():
@@ -95,7 +114,7 @@ def cpu_baseline(workload, z, iters, target_s):
         noise = rng.normal(0.0, np.sqrt(1 / (2 * s)), size=(b, g.N))
         return (2 * s * (1 / np.sqrt(2) + noise)).astype(np.float32)
 
-    if kind == "gnn":
+    if kind.startswith("gnn"):
         return None
     algo = "minsum" if kind == "minsum" else "bp"
     b = 4
@@ -153,6 +172,8 @@ def main():
         gdec, conv = create_message_gnn_decoder(H, num_iterations=iters, hidden_dim=64,
                                                 base_graph=base, Z=z)
         gdec = gdec.to(dev)
+        if kind == "gnn-bf16":
+            gdec.precision = "bf16"
         types = conv.get_message_types(base, z).to(dev).to(torch.int32)
         io = conv.message_to_var_index().to(dev).to(torch.int32)
         probs = torch.empty((B, n), dtype=torch.float32, device=dev)
@@ -164,10 +185,11 @@ def main():
                 from ldpc_neural_decoder.utils import count_errors
                 count_errors((p > 0.5).to(torch.uint8), counters=counters)
 
-        dtype = "f32"
+        dtype = "bf16" if kind == "gnn-bf16" else "f32"
         E = len(conv.messages)
         per_launch_alg = 12 * 64 * 64 * E * B * iters  # useful MLP FLOPs per forward
-        bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
+        bound, unit = "mfma", "TFLOP/s"
+        peak = BF16_MFMA_PEAK_TFS if kind == "gnn-bf16" else FP32_MFMA_PEAK_TFS
         dominant = "gnn forward (all layers)"
 
     for _ in range(a.warmup):
@@ -200,9 +222,13 @@ def main():
         value = total_frames / elapsed
         achieved = per_launch_alg / (kern_ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
         traffic = None
-        tj = a.traffic_json
-        if tj and os.path.exists(tj):
-            traffic = json.load(open(tj)).get("bytes_per_launch")
+        tj = a.traffic_json or os.path.join(ROOT, "profiles", f"r01_pmc_{a.workload.replace('-', '_')}.json")
+        if os.path.exists(tj):
+            tjd = json.load(open(tj))
+            # the PMC pass ran the same workload at the default batch; scale per launch to this B
+            traffic = tjd.get("bytes_per_launch")
+            if traffic is not None and tjd.get("batch") and tjd["batch"] != B:
+                traffic = traffic * B / tjd["batch"]
         cpu = None
         if world == 1 and a.cpu_baseline_seconds > 0:
             cpu = cpu_baseline(a.workload, z, iters, a.cpu_baseline_seconds)
@@ -230,6 +256,7 @@ def main():
                          "unit": unit, "frac": achieved / peak, "traffic": traffic,
                          "kernel_ms": kern_ms,
                          "algorithmic_per_launch": per_launch_alg},
+            "roofline_notes": roofline_notes(kind, B, n, kern_ms, traffic),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -98,3 +98,31 @@ def test_state_dict_keys_match_reference():
     f = golden("gnn_z4.npz")
     dec = MessageGNNDecoder(788, 5, 64, 4)
     assert list(dec.state_dict().keys()) == list(f["state_keys"])
+
+
+@pytest.mark.parametrize("z,layers", [(4, 5), (32, 3)])
+def test_bf16_path_within_tolerance(cuda, oracle_mod, z, layers):
+    """precision="bf16" (cfg5): bf16 feature storage and MFMA operands, fp32 accumulation.
+    Stated tolerance vs the fp32 oracle: mean |dp| <= 5e-3, max |dp| <= 0.1, and >= 99.5 % of the
+    decisions with |p - 0.5| > 0.05 unchanged."""
+    torch.manual_seed(3)
+    base = load_base_matrix(code_path(z))
+    H = expand_base_matrix(base, z)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=layers, hidden_dim=64, base_graph=base, Z=z)
+    with torch.no_grad():
+        for p in dec.parameters():
+            p.mul_(0.5)
+    dec = dec.to(cuda)
+    dec.precision = "bf16"
+    types = conv.get_message_types(base, z)
+    llr = (torch.randn(16, H.shape[1]) * 2 + 1.5).to(cuda)
+    p = dec(llr, conv.message_to_var_index(), types, conv.var_to_check_adjacency,
+            conv.check_to_var_adjacency).cpu().numpy()
+    sd = {k: v.cpu() for k, v in dec.state_dict().items()}
+    ref = oracle_mod.gnn_forward(sd, llr.cpu(), conv.edge_var, conv.edge_var, conv.edge_chk,
+                                 H.shape[1], H.shape[0], types).numpy()
+    d = np.abs(p - ref)
+    sure = np.abs(ref - 0.5) > 0.05
+    agree = ((p > 0.5) == (ref > 0.5))[sure].mean()
+    print(f"bf16 z={z}: mean {d.mean():.2e} max {d.max():.2e} agree {agree:.5f}")
+    assert d.mean() <= 5e-3 and d.max() <= 0.1 and agree >= 0.995

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (tools/gpu_profile.sh output) into profiles/<tag>_pmc_<w>.json.
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE on gfx950 reads exactly half
+the bytes of a wide coalesced streaming read, so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+(the counters are in KB).  Here the doubling is checked against a known byte count: the LLR
+input of the flood decoder is B*N*4 bytes and it is read exactly once.
+
+    python tools/pmc_summary.py gpurun_out/prof_<tag>_<w> <kernel-substring> <out.json> [expected_read_bytes]
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def main(d, kern, out, expected_read=None):
+    agg = collections.defaultdict(list)
+    for sub in sorted(os.listdir(d)):
+        f = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            if kern in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    res = {k: sum(v) / len(v) for k, v in agg.items()}
+    waves = res.get("SQ_WAVES")
+    out_d = {"kernel_substring": kern, "counters_per_launch": res}
+    if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
+        read_b = 2 * res["FETCH_SIZE"] * 1024
+        write_b = res["WRITE_SIZE"] * 1024
+        out_d.update({"read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
+                      "bytes_per_launch": read_b + write_b,
+                      "correction": "FETCH_SIZE x2 (gfx950 half-count for wide streaming reads), KB->B"})
+        if expected_read:
+            out_d["expected_read_bytes"] = float(expected_read)
+            out_d["read_vs_expected"] = read_b / float(expected_read)
+    if waves:
+        out_d["per_wave"] = {k: v / waves for k, v in res.items() if k.startswith("SQ_")}
+    json.dump(out_d, open(out, "w"), indent=1)
+    print(json.dumps(out_d, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
