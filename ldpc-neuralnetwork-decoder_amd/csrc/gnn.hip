@@ -47,7 +47,7 @@ constexpr int kMfmaH = 64;
 int mlp_threads() {
     static int t = [] {
         const char *e = std::getenv("LDPC_GNN_MLP_THREADS");
-        return (e && std::atoi(e) == 512) ? 512 : 256;
+        return (e && std::atoi(e) == 256) ? 256 : 512;
     }();
     return t;
 }
@@ -75,6 +75,29 @@ struct GnnLayer {
     float *var_sum;  // (B, N), last layer only
     int residual, last;
 };
+
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): blocks that share an
+// XCD (equal blockIdx % 8 under round-robin dispatch) get one contiguous range of frames, so a
+// frame's features and group means are pulled into one XCD's L2 instead of all eight.
+// Placement only changes speed, never results.
+__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nblk) {
+    const int64_t x = bid % 8, q = nblk / 8, r = nblk % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// Tile order for the persistent MLP kernels: the tiles are split into 8 contiguous ranges, one
+// per XCD group (blockIdx % 8), and the waves of that group's blocks walk their range
+// interleaved, so at any moment one XCD works on a few consecutive frames and their group-mean
+// rows stay in its L2.  Returns this wave's first tile and stride; tiles stop at t_end.
+struct TileWalk { int64_t first, stride, end; };
+__device__ __forceinline__ TileWalk xcd_tiles(int64_t ntiles, int waves_per_block, int wave) {
+    const int64_t nb = gridDim.x, x = blockIdx.x % 8, i = blockIdx.x / 8;
+    const int64_t q = nb / 8, r = nb % 8;
+    const int64_t nbx = q + (x < r ? 1 : 0);              // blocks in this XCD group
+    const int64_t before = x * q + min<int64_t>(x, r);     // blocks in earlier groups
+    const int64_t t0 = ntiles * before / nb, t1 = ntiles * (before + nbx) / nb;
+    return {t0 + i * waves_per_block + wave, nbx * waves_per_block, t1};
+}
 
 // feature u of message m of frame b *before* the type embedding
 __device__ __forceinline__ float x_feat(const GnnLayer &P, int64_t b, int64_t m, int u, int H) {
@@ -112,7 +135,7 @@ __global__ __launch_bounds__(256) void gnn_group_mean_kernel(GnnLayer P, int H) 
 // every lane keeps 4 x 16 B in flight (the plain kernel above is latency-bound at ~1.7 TB/s).
 __global__ __launch_bounds__(256) void gnn_group_mean_h64_kernel(GnnLayer P) {
     const int lane = threadIdx.x & 63, q = lane & 15;
-    const int64_t gid = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
+    const int64_t gid = (xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
     const int64_t G = P.Gv + P.Gc;
     if (gid >= P.B * G) return;
     const int64_t b = gid / G;
@@ -159,6 +182,9 @@ constexpr int kW1 = 128 * 64, kW2 = 64 * 64;
 constexpr int kOffW1v = 0, kOffW2v = kW1, kOffW1c = kW1 + kW2, kOffW2c = 2 * kW1 + kW2;
 constexpr int kOffBias = 2 * kW1 + 2 * kW2;  // b1v, b2v, b1c, b2c, wo
 constexpr int kOffEmb = kOffBias + 5 * 64;
+// type-embedding rows padded to 68 floats: lanes of one tile read the rows of different types at
+// the same column, and a 256-B row stride would put all of them on one LDS bank
+constexpr int kEmbStride = 68;
 
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
@@ -185,7 +211,7 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
         lds[kOffBias + 192 + tid] = P.b2c[tid];
         lds[kOffBias + 256 + tid] = P.last ? P.wo[tid] : 0.0f;
     }
-    for (int i = tid; i < P.T * 64; i += kMlpThreads) lds[kOffEmb + i] = P.emb[i];
+    for (int i = tid; i < P.T * 64; i += kMlpThreads) lds[kOffEmb + (i >> 6) * kEmbStride + (i & 63)] = P.emb[i];
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5;
@@ -193,8 +219,8 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
     const int64_t R = P.B * P.E;
     const int64_t ntiles = (R + 31) / 32;
     const float bo = P.last ? P.bo[0] : 0.0f;
-    for (int64_t t = (int64_t)blockIdx.x * (kMlpThreads / 64) + wave; t < ntiles;
-         t += (int64_t)gridDim.x * (kMlpThreads / 64)) {
+    const TileWalk tw = xcd_tiles(ntiles, kMlpThreads / 64, wave);
+    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
         const int64_t row = t * 32 + j;
         const bool ok = row < R;
         const int64_t rr = ok ? row : R - 1;
@@ -204,7 +230,7 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
         const float4 *grp = nullptr;  // half 1: the group-mean row of the current side
         if (half == 0) {
             const int ty = P.msg_type[m];
-            const float *e = lds + kOffEmb + ty * 64;
+            const float *e = lds + kOffEmb + ty * kEmbStride;
             if (P.x_in) {
                 const float4 *xr = reinterpret_cast<const float4 *>(P.x_in + rr * H);
 #pragma unroll
@@ -319,11 +345,12 @@ struct GnnLayerBf16 {
     __bf16 *Mv, *Mc;     // (B, G, 64)
 };
 
-// one wave = two groups (lane half h -> group 2w + h), each lane two feature units
+// 8 lanes per group (16 B = 8 bf16 features each), 8 groups per wave, members unrolled by 4:
+// enough bytes in flight per lane to stream, fp32 sums, one bf16 row out.
 __global__ __launch_bounds__(256) void gnn_group_mean_bf16_kernel(GnnLayerBf16 Q) {
     const GnnLayer &P = Q.P;
-    const int lane = threadIdx.x & 63, h = lane >> 5, u = 2 * (lane & 31);
-    const int64_t gid = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + h;
+    const int lane = threadIdx.x & 63, q = lane & 7, u = 8 * q;
+    const int64_t gid = (xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);
     const int64_t G = P.Gv + P.Gc;
     if (gid >= P.B * G) return;
     const int64_t b = gid / G;
@@ -334,28 +361,37 @@ __global__ __launch_bounds__(256) void gnn_group_mean_bf16_kernel(GnnLayerBf16 Q
     const int32_t *mem = isv ? P.vg_mem : P.cg_mem;
     const float inv = isv ? P.inv_v[gg] : P.inv_c[gg];
     __bf16 *dst = (isv ? Q.Mv + (b * P.Gv + gg) * 64 : Q.Mc + (b * P.Gc + gg) * 64) + u;
-    float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll 4
-    for (int p = ptr[gg]; p < ptr[gg + 1]; ++p) {
-        const int m = mem[p];
-        const float *e = P.emb + P.msg_type[m] * 64 + u;
-        float x0, x1;
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+    auto add = [&](int m) {
+        const float4 e0 = reinterpret_cast<const float4 *>(P.emb + P.msg_type[m] * 64 + u)[0];
+        const float4 e1 = reinterpret_cast<const float4 *>(P.emb + P.msg_type[m] * 64 + u)[1];
+        const float e[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
         if (Q.x_in) {
-            const bf16x2 v = *reinterpret_cast<const bf16x2 *>(Q.x_in + (b * P.E + m) * 64 + u);
-            x0 = (float)v[0];
-            x1 = (float)v[1];
+            const bf16x8 v = *reinterpret_cast<const bf16x8 *>(Q.x_in + (b * P.E + m) * 64 + u);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] += (float)v[i] + e[i];
         } else {
             const float l = P.llr[b * P.N + P.msg_var[m]];
-            x0 = l * P.w_in[u] + P.b_in[u];
-            x1 = l * P.w_in[u + 1] + P.b_in[u + 1];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] += (l * P.w_in[u + i] + P.b_in[u + i]) + e[i];
         }
-        s0 += x0 + e[0];
-        s1 += x1 + e[1];
+    };
+    const int p0 = ptr[gg], p1 = ptr[gg + 1];
+    int p = p0;
+    for (; p + 4 <= p1; p += 4) {
+        const int m0 = mem[p], m1 = mem[p + 1], m2 = mem[p + 2], m3 = mem[p + 3];
+        add(m0);
+        add(m1);
+        add(m2);
+        add(m3);
     }
-    bf16x2 o;
-    o[0] = (__bf16)(s0 * inv);
-    o[1] = (__bf16)(s1 * inv);
-    *reinterpret_cast<bf16x2 *>(dst) = o;
+    for (; p < p1; ++p) add(mem[p]);
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (__bf16)(acc[i] * inv);
+    *reinterpret_cast<bf16x8 *>(dst) = o;
 }
 
 // LDS image (bytes): W1v, W1c as bf16 [64 u][136] (row = 128 k + 8 pad: conflict-free b128 reads)
@@ -410,33 +446,68 @@ __global__ __launch_bounds__(256, 2) void gnn_mlp_bf16_kernel(GnnLayerBf16 Q) {
         bias[256 + tid] = P.last ? P.wo[tid] : 0.0f;
     }
     float *embl = reinterpret_cast<float *>(smem + kB_OffEmb);
-    for (int i = tid; i < P.T * 64; i += 256) embl[i] = P.emb[i];
+    for (int i = tid; i < P.T * 64; i += 256) embl[(i >> 6) * kEmbStride + (i & 63)] = P.emb[i];
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
     const int64_t R = P.B * P.E;
     const int64_t ntiles = (R + 31) / 32;
     const float bo = P.last ? P.bo[0] : 0.0f;
-    for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+    const TileWalk tw = xcd_tiles(ntiles, 4, wave);
+    const int64_t t1 = tw.end, st = tw.stride;
+    // Two-stage software pipeline across this wave's tiles: the per-message indices of tile
+    // t+8 and the feature / group-mean rows of tile t+4 are in flight while tile t computes
+    // (one dependent global round trip each; without it a wave idles ~90 % of the time).
+    struct Idx { int64_t rr, b, m; int ty, vg, cg, mv; };
+    struct In { bf16x8 x[4], a[4], c[4]; float l; };
+    auto load_idx = [&](int64_t t) {
+        Idx I;
+        const int64_t row = t * 32 + j;
+        I.rr = row < R ? row : R - 1;
+        I.b = I.rr / P.E;
+        I.m = I.rr - I.b * P.E;
+        I.ty = P.msg_type[I.m];
+        I.vg = P.vgroup[I.m];
+        I.cg = P.cgroup[I.m];
+        I.mv = P.msg_var[I.m];
+        return I;
+    };
+    auto load_in = [&](const Idx &I) {
+        In D;
+        const char *ma = reinterpret_cast<const char *>(Q.Mv + (I.b * P.Gv + I.vg) * 64);
+        const char *mb = reinterpret_cast<const char *>(Q.Mc + (I.b * P.Gc + I.cg) * 64);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int f0 = 16 * s + 8 * h;
+            D.a[s] = ld_bf16x8(ma + 2 * f0);
+            D.c[s] = ld_bf16x8(mb + 2 * f0);
+            if (Q.x_in) D.x[s] = ld_bf16x8(reinterpret_cast<const char *>(Q.x_in + I.rr * 64 + f0));
+        }
+        D.l = Q.x_in ? 0.0f : P.llr[I.b * P.N + I.mv];
+        return D;
+    };
+    Idx Icur = load_idx(tw.first), Inext = load_idx(tw.first + st < t1 ? tw.first + st : tw.first);
+    In Dcur = load_in(Icur);
+    for (int64_t t = tw.first; t < t1; t += st) {
+        const In Dnext = load_in(Inext);
+        const Idx Inext2 = load_idx(t + 2 * st < t1 ? t + 2 * st : t);
+        const Idx I = Icur;
+        const In D = Dcur;
         const int64_t row = t * 32 + j;
         const bool ok = row < R;
-        const int64_t rr = ok ? row : R - 1;
-        const int64_t b = rr / P.E, m = rr - b * P.E;
+        const int64_t rr = I.rr, b = I.b, m = I.m;
+        (void)m;
         // B fragments: k-step s < 4 -> features 16s + 8h .. +7 of c; s >= 4 -> of a (var) / b (chk)
-        const float *e = embl + P.msg_type[m] * 64;
-        const char *ma = reinterpret_cast<const char *>(Q.Mv + (b * P.Gv + P.vgroup[m]) * 64);
-        const char *mb = reinterpret_cast<const char *>(Q.Mc + (b * P.Gc + P.cgroup[m]) * 64);
-        const float l = Q.x_in ? 0.0f : P.llr[b * P.N + P.msg_var[m]];
+        const float *e = embl + I.ty * kEmbStride;
         auto cfrag = [&](int s) {
             const int f0 = 16 * s + 8 * h;
             bf16x8 o;
             if (Q.x_in) {
-                const bf16x8 xv = ld_bf16x8(reinterpret_cast<const char *>(Q.x_in + rr * 64 + f0));
 #pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((float)xv[i] + e[f0 + i]);
+                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((float)D.x[s][i] + e[f0 + i]);
             } else {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((l * P.w_in[f0 + i] + P.b_in[f0 + i]) + e[f0 + i]);
+                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((D.l * P.w_in[f0 + i] + P.b_in[f0 + i]) + e[f0 + i]);
             }
             return o;
         };
@@ -451,12 +522,11 @@ __global__ __launch_bounds__(256, 2) void gnn_mlp_bf16_kernel(GnnLayerBf16 Q) {
             const char *W1 = smem + (side == 0 ? kB_OffW1v : kB_OffW1c);
             const char *W2 = smem + (side == 0 ? kB_OffW2v : kB_OffW2c);
             const float *b1 = bias + (side == 0 ? 0 : 128);
-            const char *g = side == 0 ? ma : mb;
             f32x16 h0 = {}, h1 = {};
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 const bf16x8 bop = s == 0 ? c0 : s == 1 ? c1 : s == 2 ? c2 : s == 3 ? c3
-                                 : ld_bf16x8(g + 2 * (16 * (s - 4) + 8 * h));
+                                 : (side == 0 ? D.a[s - 4] : D.c[s - 4]);
                 const int kb = wbase + 32 * s;
                 h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W1 + kb), bop, h0, 0, 0, 0);
                 h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W1 + 32 * 272 + kb), bop, h1, 0, 0, 0);
@@ -500,8 +570,11 @@ __global__ __launch_bounds__(256, 2) void gnn_mlp_bf16_kernel(GnnLayerBf16 Q) {
         }
         if (P.last) {
             part += __shfl_xor(part, 32, 64);
-            if (ok && h == 0) atomicAdd(&P.var_sum[b * P.N + P.msg_var[m]], part + bo);
+            if (ok && h == 0) atomicAdd(&P.var_sum[b * P.N + I.mv], part + bo);
         }
+        Icur = Inext;
+        Inext = Inext2;
+        Dcur = Dnext;
     }
 }
 
@@ -715,7 +788,7 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
     L.Mv = w.Mv; L.Mc = w.Mc;
     const bool mfma = H == kMfmaH;
     if (!mfma && H > 128) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be 64 (MFMA path) or <= 128");
-    const size_t mfma_lds = (size_t)(kOffEmb + types * 64) * 4;
+    const size_t mfma_lds = (size_t)(kOffEmb + types * kEmbStride) * 4;
     if (mfma && mfma_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
     const int mt = mlp_threads();
     const void *mfma_fn = mt == 512 ? reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<512>)
@@ -748,9 +821,9 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
             Q.x_out = reinterpret_cast<__bf16 *>(L.x_out);
             Q.Mv = reinterpret_cast<__bf16 *>(w.Mv);
             Q.Mc = reinterpret_cast<__bf16 *>(w.Mc);
-            hipLaunchKernelGGL(gnn_group_mean_bf16_kernel, dim3((unsigned)((waves + 7) / 8)), dim3(256), 0, s, Q);
+            hipLaunchKernelGGL(gnn_group_mean_bf16_kernel, dim3((unsigned)((waves + 31) / 32)), dim3(256), 0, s, Q);
             LDPC_CHECK_LAUNCH("gnn_group_mean_bf16_kernel");
-            const size_t lds = (size_t)kB_OffEmb + (size_t)types * 64 * 4;
+            const size_t lds = (size_t)kB_OffEmb + (size_t)types * kEmbStride * 4;
             if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
             LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp_bf16_kernel),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
