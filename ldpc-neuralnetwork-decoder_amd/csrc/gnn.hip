@@ -21,22 +21,16 @@
 //                           layer) the output projection + per-variable scatter are fused.
 //   gnn_mlp_generic_kernel  any H (VALU); used for H != 64 (e.g. the small-H test fixtures).
 //   gnn_output_kernel       probs = sigmoid(var_sum + llr).
+// precision 1 (bf16 features, bf16 MFMA) lives in gnn_bf16.hip.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
+#include "gnn.hpp"
 
-struct ldpc_gnn_plan {
-    int device = 0;
-    int64_t E = 0;
-    int Gv = 0, Gc = 0;
-    int32_t *d_tab = nullptr;  // vgroup[E] cgroup[E] vg_ptr[Gv+1] vg_mem[E] cg_ptr[Gc+1] cg_mem[E]
-    float *d_inv = nullptr;    // 1/|group|: inv_v[Gv] inv_c[Gc]
-    const int32_t *vgroup, *cgroup, *vg_ptr, *vg_mem, *cg_ptr, *cg_mem;
-    const float *inv_v, *inv_c;
-};
 
 namespace ldpc {
 namespace {
@@ -75,29 +69,6 @@ struct GnnLayer {
     float *var_sum;  // (B, N), last layer only
     int residual, last;
 };
-
-// XCD-aware block order (cdna_hip_programming.md T1, bijective form): blocks that share an
-// XCD (equal blockIdx % 8 under round-robin dispatch) get one contiguous range of frames, so a
-// frame's features and group means are pulled into one XCD's L2 instead of all eight.
-// Placement only changes speed, never results.
-__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nblk) {
-    const int64_t x = bid % 8, q = nblk / 8, r = nblk % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-}
-
-// Tile order for the persistent MLP kernels: the tiles are split into 8 contiguous ranges, one
-// per XCD group (blockIdx % 8), and the waves of that group's blocks walk their range
-// interleaved, so at any moment one XCD works on a few consecutive frames and their group-mean
-// rows stay in its L2.  Returns this wave's first tile and stride; tiles stop at t_end.
-struct TileWalk { int64_t first, stride, end; };
-__device__ __forceinline__ TileWalk xcd_tiles(int64_t ntiles, int waves_per_block, int wave) {
-    const int64_t nb = gridDim.x, x = blockIdx.x % 8, i = blockIdx.x / 8;
-    const int64_t q = nb / 8, r = nb % 8;
-    const int64_t nbx = q + (x < r ? 1 : 0);              // blocks in this XCD group
-    const int64_t before = x * q + min<int64_t>(x, r);     // blocks in earlier groups
-    const int64_t t0 = ntiles * before / nb, t1 = ntiles * (before + nbx) / nb;
-    return {t0 + i * waves_per_block + wave, nbx * waves_per_block, t1};
-}
 
 // feature u of message m of frame b *before* the type embedding
 __device__ __forceinline__ float x_feat(const GnnLayer &P, int64_t b, int64_t m, int u, int H) {
@@ -331,253 +302,6 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
     }
 }
 
-// ------------------------------------------------------------------------ bf16 path (H = 64)
-// precision 1: features x and group means stored as bf16 (half the HBM bytes), MLP operands
-// bf16 on v_mfma_f32_32x32x16_bf16, every accumulation (group sums, GEMMs, bias, residual) fp32.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
-struct GnnLayerBf16 {
-    GnnLayer P;          // fp32 pointers unused for x_in / x_out / Mv / Mc
-    const __bf16 *x_in;  // (B, E, 64) or null for layer 0
-    __bf16 *x_out;
-    __bf16 *Mv, *Mc;     // (B, G, 64)
-};
-
-// 8 lanes per group (16 B = 8 bf16 features each), 8 groups per wave, members unrolled by 4:
-// enough bytes in flight per lane to stream, fp32 sums, one bf16 row out.
-__global__ __launch_bounds__(256) void gnn_group_mean_bf16_kernel(GnnLayerBf16 Q) {
-    const GnnLayer &P = Q.P;
-    const int lane = threadIdx.x & 63, q = lane & 7, u = 8 * q;
-    const int64_t gid = (xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);
-    const int64_t G = P.Gv + P.Gc;
-    if (gid >= P.B * G) return;
-    const int64_t b = gid / G;
-    const int g = (int)(gid - b * G);
-    const bool isv = g < P.Gv;
-    const int gg = isv ? g : g - P.Gv;
-    const int32_t *ptr = isv ? P.vg_ptr : P.cg_ptr;
-    const int32_t *mem = isv ? P.vg_mem : P.cg_mem;
-    const float inv = isv ? P.inv_v[gg] : P.inv_c[gg];
-    __bf16 *dst = (isv ? Q.Mv + (b * P.Gv + gg) * 64 : Q.Mc + (b * P.Gc + gg) * 64) + u;
-    float acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
-    auto add = [&](int m) {
-        const float4 e0 = reinterpret_cast<const float4 *>(P.emb + P.msg_type[m] * 64 + u)[0];
-        const float4 e1 = reinterpret_cast<const float4 *>(P.emb + P.msg_type[m] * 64 + u)[1];
-        const float e[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-        if (Q.x_in) {
-            const bf16x8 v = *reinterpret_cast<const bf16x8 *>(Q.x_in + (b * P.E + m) * 64 + u);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) acc[i] += (float)v[i] + e[i];
-        } else {
-            const float l = P.llr[b * P.N + P.msg_var[m]];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) acc[i] += (l * P.w_in[u + i] + P.b_in[u + i]) + e[i];
-        }
-    };
-    const int p0 = ptr[gg], p1 = ptr[gg + 1];
-    int p = p0;
-    for (; p + 4 <= p1; p += 4) {
-        const int m0 = mem[p], m1 = mem[p + 1], m2 = mem[p + 2], m3 = mem[p + 3];
-        add(m0);
-        add(m1);
-        add(m2);
-        add(m3);
-    }
-    for (; p < p1; ++p) add(mem[p]);
-    bf16x8 o;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (__bf16)(acc[i] * inv);
-    *reinterpret_cast<bf16x8 *>(dst) = o;
-}
-
-// LDS image (bytes): W1v, W1c as bf16 [64 u][136] (row = 128 k + 8 pad: conflict-free b128 reads)
-//                    W2v, W2c as bf16 [64 o][72], columns permuted to GEMM1's accumulator order
-//                    b1v b2v b1c b2c wo fp32 [64 each], emb fp32 [T][64]
-constexpr int kB_W1 = 64 * 136 * 2, kB_W2 = 64 * 72 * 2;
-constexpr int kB_OffW1v = 0, kB_OffW1c = kB_W1, kB_OffW2v = 2 * kB_W1, kB_OffW2c = 2 * kB_W1 + kB_W2;
-constexpr int kB_OffBias = 2 * kB_W1 + 2 * kB_W2;   // bytes
-constexpr int kB_OffEmb = kB_OffBias + 5 * 64 * 4;
-
-// unit held by element kk of k-step s of row tile rt in GEMM1's accumulator (cdna_hip §3)
-__host__ __device__ __forceinline__ int acc_unit(int rt, int s, int kk) {
-    return 32 * rt + 16 * s + 8 * ((kk & 7) >> 2) + 4 * (kk >> 3) + (kk & 3);
-}
-
-__device__ __forceinline__ bf16x8 ld_bf16x8(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
-
-// relu(acc[8s .. 8s+7] + bias) as one bf16 fragment (whole-vector construction keeps it in VGPRs)
-__device__ __forceinline__ bf16x8 relu_pack(const f32x16 &acc, int s, const float *b1, int ubase, int h) {
-    bf16x8 o;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int r = 8 * s + i;
-        const int u = ubase + (r & 3) + 8 * (r >> 2) + 4 * h;
-        o[i] = (__bf16)fmaxf(acc[r] + b1[u], 0.0f);
-    }
-    return o;
-}
-
-__global__ __launch_bounds__(256, 2) void gnn_mlp_bf16_kernel(GnnLayerBf16 Q) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const GnnLayer &P = Q.P;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < 64 * 128; i += 256) {
-        const int o = i >> 7, k = i & 127;
-        reinterpret_cast<__bf16 *>(smem + kB_OffW1v)[o * 136 + k] = (__bf16)P.w1v[i];
-        reinterpret_cast<__bf16 *>(smem + kB_OffW1c)[o * 136 + k] = (__bf16)P.w1c[i];
-    }
-    for (int i = tid; i < 64 * 64; i += 256) {
-        const int o = i >> 6, q = i & 63;
-        const int rt = q >> 5, s = (q >> 4) & 1, kk = q & 15;
-        const int u = acc_unit(rt, s, kk);
-        reinterpret_cast<__bf16 *>(smem + kB_OffW2v)[o * 72 + q] = (__bf16)P.w2v[o * 64 + u];
-        reinterpret_cast<__bf16 *>(smem + kB_OffW2c)[o * 72 + q] = (__bf16)P.w2c[o * 64 + u];
-    }
-    float *bias = reinterpret_cast<float *>(smem + kB_OffBias);
-    if (tid < 64) {
-        bias[tid] = P.b1v[tid];
-        bias[64 + tid] = P.b2v[tid];
-        bias[128 + tid] = P.b1c[tid];
-        bias[192 + tid] = P.b2c[tid];
-        bias[256 + tid] = P.last ? P.wo[tid] : 0.0f;
-    }
-    float *embl = reinterpret_cast<float *>(smem + kB_OffEmb);
-    for (int i = tid; i < P.T * 64; i += 256) embl[(i >> 6) * kEmbStride + (i & 63)] = P.emb[i];
-    __syncthreads();
-
-    const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
-    const int64_t R = P.B * P.E;
-    const int64_t ntiles = (R + 31) / 32;
-    const float bo = P.last ? P.bo[0] : 0.0f;
-    const TileWalk tw = xcd_tiles(ntiles, 4, wave);
-    const int64_t t1 = tw.end, st = tw.stride;
-    // Two-stage software pipeline across this wave's tiles: the per-message indices of tile
-    // t+8 and the feature / group-mean rows of tile t+4 are in flight while tile t computes
-    // (one dependent global round trip each; without it a wave idles ~90 % of the time).
-    struct Idx { int64_t rr, b, m; int ty, vg, cg, mv; };
-    struct In { bf16x8 x[4], a[4], c[4]; float l; };
-    auto load_idx = [&](int64_t t) {
-        Idx I;
-        const int64_t row = t * 32 + j;
-        I.rr = row < R ? row : R - 1;
-        I.b = I.rr / P.E;
-        I.m = I.rr - I.b * P.E;
-        I.ty = P.msg_type[I.m];
-        I.vg = P.vgroup[I.m];
-        I.cg = P.cgroup[I.m];
-        I.mv = P.msg_var[I.m];
-        return I;
-    };
-    auto load_in = [&](const Idx &I) {
-        In D;
-        const char *ma = reinterpret_cast<const char *>(Q.Mv + (I.b * P.Gv + I.vg) * 64);
-        const char *mb = reinterpret_cast<const char *>(Q.Mc + (I.b * P.Gc + I.cg) * 64);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int f0 = 16 * s + 8 * h;
-            D.a[s] = ld_bf16x8(ma + 2 * f0);
-            D.c[s] = ld_bf16x8(mb + 2 * f0);
-            if (Q.x_in) D.x[s] = ld_bf16x8(reinterpret_cast<const char *>(Q.x_in + I.rr * 64 + f0));
-        }
-        D.l = Q.x_in ? 0.0f : P.llr[I.b * P.N + I.mv];
-        return D;
-    };
-    Idx Icur = load_idx(tw.first), Inext = load_idx(tw.first + st < t1 ? tw.first + st : tw.first);
-    In Dcur = load_in(Icur);
-    for (int64_t t = tw.first; t < t1; t += st) {
-        const In Dnext = load_in(Inext);
-        const Idx Inext2 = load_idx(t + 2 * st < t1 ? t + 2 * st : t);
-        const Idx I = Icur;
-        const In D = Dcur;
-        const int64_t row = t * 32 + j;
-        const bool ok = row < R;
-        const int64_t rr = I.rr, b = I.b, m = I.m;
-        (void)m;
-        // B fragments: k-step s < 4 -> features 16s + 8h .. +7 of c; s >= 4 -> of a (var) / b (chk)
-        const float *e = embl + I.ty * kEmbStride;
-        auto cfrag = [&](int s) {
-            const int f0 = 16 * s + 8 * h;
-            bf16x8 o;
-            if (Q.x_in) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((float)D.x[s][i] + e[f0 + i]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = (__bf16)((D.l * P.w_in[f0 + i] + P.b_in[f0 + i]) + e[f0 + i]);
-            }
-            return o;
-        };
-        const bf16x8 c0 = cfrag(0), c1 = cfrag(1), c2 = cfrag(2), c3 = cfrag(3);
-        f32x16 y0 = {}, y1 = {};
-        // the weight-fragment addresses are loop-invariant: without this the compiler hoists all
-        // 48 fragment loads (192 VGPRs) out of the tile loop and spills
-        int wbase = j * 272 + 16 * h, w2base = j * 144 + 16 * h;
-        asm volatile("" : "+v"(wbase), "+v"(w2base));
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            const char *W1 = smem + (side == 0 ? kB_OffW1v : kB_OffW1c);
-            const char *W2 = smem + (side == 0 ? kB_OffW2v : kB_OffW2c);
-            const float *b1 = bias + (side == 0 ? 0 : 128);
-            f32x16 h0 = {}, h1 = {};
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const bf16x8 bop = s == 0 ? c0 : s == 1 ? c1 : s == 2 ? c2 : s == 3 ? c3
-                                 : (side == 0 ? D.a[s - 4] : D.c[s - 4]);
-                const int kb = wbase + 32 * s;
-                h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W1 + kb), bop, h0, 0, 0, 0);
-                h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W1 + 32 * 272 + kb), bop, h1, 0, 0, 0);
-            }
-            const bf16x8 p00 = relu_pack(h0, 0, b1, 0, h), p01 = relu_pack(h0, 1, b1, 0, h);
-            const bf16x8 p10 = relu_pack(h1, 0, b1, 32, h), p11 = relu_pack(h1, 1, b1, 32, h);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rt = q >> 1, s = q & 1;
-                const bf16x8 bop = q == 0 ? p00 : q == 1 ? p01 : q == 2 ? p10 : p11;
-                const int qb = w2base + 2 * (32 * rt + 16 * s);
-                y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W2 + qb), bop, y0, 0, 0, 0);
-                y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld_bf16x8(W2 + 32 * 144 + qb), bop, y1, 0, 0, 0);
-            }
-        }
-        const float *b2v = bias + 64, *b2c = bias + 192, *wo = bias + 256;
-        float part = 0.0f;
-#pragma unroll
-        for (int ot = 0; ot < 2; ++ot) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int o0 = 32 * ot + 8 * q + 4 * h;
-                float v[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = ((ot == 0 ? y0[4 * q + i] : y1[4 * q + i]) + b2v[o0 + i]) + b2c[o0 + i];
-                if (P.residual) {
-                    const bf16x4 xr = *reinterpret_cast<const bf16x4 *>(Q.x_in + rr * 64 + o0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) v[i] += (float)xr[i];
-                }
-                if (P.last) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) part += v[i] * wo[o0 + i];
-                } else if (ok) {
-                    bf16x4 o;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) o[i] = (__bf16)v[i];
-                    *reinterpret_cast<bf16x4 *>(Q.x_out + row * 64 + o0) = o;
-                }
-            }
-        }
-        if (P.last) {
-            part += __shfl_xor(part, 32, 64);
-            if (ok && h == 0) atomicAdd(&P.var_sum[b * P.N + I.mv], part + bo);
-        }
-        Icur = Inext;
-        Inext = Inext2;
-        Dcur = Dnext;
-    }
-}
-
 // ------------------------------------------------------------------------ fused MLP, any H
 // one wave per message, lanes = output units (H <= 64 per pass); VALU fp32.
 __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H) {
@@ -644,7 +368,8 @@ struct Ws {
 Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precision, void *base) {
     Ws w{};
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
-    const int64_t es = precision == 1 ? 2 : 4;  // bytes per stored feature
+    const int64_t es = 4;  // bytes per stored feature (fp32 path)
+    (void)precision;
     const int64_t xb = layers > 1 ? al(B * p->E * H * es) : 0;
     const int64_t xb2 = layers > 2 ? xb : 0;
     const int64_t mv = al(B * (int64_t)p->Gv * H * es), mc = al(B * (int64_t)p->Gc * H * es);
@@ -697,6 +422,29 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         const int d = cptr[g + 1] - cptr[g];
         inv[n_vgroups + g] = d ? 1.0f / (float)d : 0.0f;
     }
+    // bf16 path: group tiles of 8 groups of one degree (gnn.hpp), var side then check side
+    std::vector<int32_t> gt_meta, gt_grp, gt_mem;
+    auto add_tiles = [&](const std::vector<int32_t> &ptr, const std::vector<int32_t> &mem, int ngroups, int gbase) {
+        std::vector<int32_t> order;
+        for (int g = 0; g < ngroups; ++g)
+            if (ptr[g + 1] > ptr[g]) order.push_back(g);  // a group with no messages is never read
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int a, int b) { return ptr[a + 1] - ptr[a] < ptr[b + 1] - ptr[b]; });
+        for (size_t i = 0; i < order.size();) {
+            const int d = ptr[order[i] + 1] - ptr[order[i]];
+            size_t n = 0;
+            while (n < 8 && i + n < order.size() && ptr[order[i + n] + 1] - ptr[order[i + n]] == d) ++n;
+            gt_meta.push_back(d);
+            gt_meta.push_back((int32_t)gt_mem.size());
+            for (int k = 0; k < d; ++k)
+                for (size_t q = 0; q < 8; ++q)
+                    gt_mem.push_back(q < n ? mem[ptr[order[i + q]] + k] : mem[ptr[order[i]] + k]);
+            for (size_t q = 0; q < 8; ++q) gt_grp.push_back(q < n ? gbase + order[i + q] : -1);
+            i += n;
+        }
+    };
+    add_tiles(vptr, vmem, n_vgroups, 0);
+    add_tiles(cptr, cmem, n_cgroups, n_vgroups);
     std::vector<int32_t> blob;
     blob.insert(blob.end(), h_vgroup, h_vgroup + E);
     blob.insert(blob.end(), h_cgroup, h_cgroup + E);
@@ -704,19 +452,26 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     blob.insert(blob.end(), vmem.begin(), vmem.end());
     blob.insert(blob.end(), cptr.begin(), cptr.end());
     blob.insert(blob.end(), cmem.begin(), cmem.end());
+    const size_t gt_words = gt_meta.size() + gt_grp.size() + gt_mem.size();
     auto *p = new ldpc_gnn_plan();
+    p->n_gtiles = (int)(gt_meta.size() / 2);
     p->E = E;
     p->Gv = n_vgroups;
     p->Gc = n_cgroups;
     hipError_t e1 = hipGetDevice(&p->device);
     hipError_t e2 = hipMalloc(&p->d_tab, blob.size() * 4);
     hipError_t e3 = hipMalloc(&p->d_inv, inv.size() * 4);
-    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+    hipError_t e4 = hipMalloc(&p->d_gt, gt_words * 4);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan allocation failed");
     }
     if (hipMemcpy(p->d_tab, blob.data(), blob.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->d_inv, inv.data(), inv.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(p->d_inv, inv.data(), inv.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_gt, gt_meta.data(), gt_meta.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_gt + gt_meta.size(), gt_grp.data(), gt_grp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_gt + gt_meta.size() + gt_grp.size(), gt_mem.data(), gt_mem.size() * 4,
+                  hipMemcpyHostToDevice) != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan upload failed");
     }
@@ -728,6 +483,9 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     p->cg_mem = p->cg_ptr + n_cgroups + 1;
     p->inv_v = p->d_inv;
     p->inv_c = p->d_inv + n_vgroups;
+    p->gt_meta = reinterpret_cast<const int2 *>(p->d_gt);
+    p->gt_grp = p->d_gt + gt_meta.size();
+    p->gt_mem = p->gt_grp + gt_grp.size();
     *out = p;
     return LDPC_OK;
 }
@@ -736,6 +494,7 @@ extern "C" int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p) {
     if (!p) return LDPC_OK;
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_inv) (void)hipFree(p->d_inv);
+    if (p->d_gt) (void)hipFree(p->d_gt);
     delete p;
     return LDPC_OK;
 }
@@ -748,6 +507,7 @@ extern "C" int64_t ldpc_gnn_weights_size(int hidden, int types, int layers) {
 extern "C" int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers,
                                            int precision) {
     if (!p || hidden <= 0 || N <= 0 || B < 0 || layers <= 0) return fail(LDPC_EINVAL, "bad arguments");
+    if (precision == 1) return gnn_bf16_workspace(p, N, B, layers);
     return carve(p, hidden, N, B, layers, precision, nullptr).bytes;
 }
 
@@ -761,11 +521,14 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
     if (precision == 1 && hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "bf16 path needs hidden_dim 64");
     if (B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (precision == 1)
+        return gnn_bf16_forward(p, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs, d_work,
+                                work_bytes, s);
     const int H = hidden;
     Ws w = carve(p, H, N, B, layers, precision, d_work);
     if (!d_work || work_bytes < w.bytes)
         return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
-    hipStream_t s = static_cast<hipStream_t>(stream);
     if (!g_num_cus) {
         int dev = 0;
         LDPC_HIP(hipGetDevice(&dev));
@@ -814,26 +577,6 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
         L.x_out = (l % 2 == 0) ? w.xa : w.xb;
         L.var_sum = w.var_sum;
         const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
-        if (precision == 1) {
-            GnnLayerBf16 Q{};
-            Q.P = L;
-            Q.x_in = reinterpret_cast<const __bf16 *>(x_in);
-            Q.x_out = reinterpret_cast<__bf16 *>(L.x_out);
-            Q.Mv = reinterpret_cast<__bf16 *>(w.Mv);
-            Q.Mc = reinterpret_cast<__bf16 *>(w.Mc);
-            hipLaunchKernelGGL(gnn_group_mean_bf16_kernel, dim3((unsigned)((waves + 31) / 32)), dim3(256), 0, s, Q);
-            LDPC_CHECK_LAUNCH("gnn_group_mean_bf16_kernel");
-            const size_t lds = (size_t)kB_OffEmb + (size_t)types * kEmbStride * 4;
-            if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
-            LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp_bf16_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            const int64_t tiles = (B * p->E + 31) / 32;
-            const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)g_num_cus * 2);
-            hipLaunchKernelGGL(gnn_mlp_bf16_kernel, dim3(grid), dim3(256), lds, s, Q);
-            LDPC_CHECK_LAUNCH("gnn_mlp_bf16_kernel");
-            x_in = L.x_out;
-            continue;
-        }
         if (H == 64)
             hipLaunchKernelGGL(gnn_group_mean_h64_kernel, dim3((unsigned)((waves + 15) / 16)), dim3(256), 0, s, L);
         else

@@ -1,0 +1,57 @@
+// gnn.hpp -- message-GNN plan shared by the fp32 path (gnn.hip) and the bf16 path (gnn_bf16.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+struct ldpc_gnn_plan {
+    int device = 0;
+    int64_t E = 0;
+    int Gv = 0, Gc = 0;
+    int32_t *d_tab = nullptr;  // vgroup[E] cgroup[E] vg_ptr[Gv+1] vg_mem[E] cg_ptr[Gc+1] cg_mem[E]
+    float *d_inv = nullptr;    // 1/|group|: inv_v[Gv] inv_c[Gc]
+    const int32_t *vgroup, *cgroup, *vg_ptr, *vg_mem, *cg_ptr, *cg_mem;
+    const float *inv_v, *inv_c;
+    // bf16 path: "group tiles" of 8 groups of one degree each (var groups first, then check
+    // groups, each side sorted by degree), so one wave sums 8 groups with no divergence.
+    //   gt_meta[t] = {degree, offset into gt_mem}, gt_grp[8 t + q] = group id (check groups
+    //   offset by Gv; -1 = padding), gt_mem[off + 8 i + q] = i-th member message of group q.
+    int n_gtiles = 0;
+    int32_t *d_gt = nullptr;
+    const int2 *gt_meta = nullptr;
+    const int32_t *gt_grp = nullptr, *gt_mem = nullptr;
+};
+
+namespace ldpc {
+
+// bf16 forward (precision 1, H = 64); same arguments as ldpc_gnn_forward.
+// The workspace is sized for the largest type count the LDS image admits (kBf16MaxTypes).
+constexpr int kBf16MaxTypes = 200;
+int64_t gnn_bf16_workspace(const ldpc_gnn_plan *p, int N, int64_t B, int layers);
+int gnn_bf16_forward(const ldpc_gnn_plan *p, int types, int layers, const float *d_weights,
+                     const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                     int64_t B, float *d_probs, void *d_work, int64_t work_bytes, hipStream_t s);
+
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): blocks that share an
+// XCD (equal blockIdx % 8 under round-robin dispatch) get one contiguous range of work, so a
+// frame's features and group means are pulled into one XCD's L2 instead of all eight.
+// Placement only changes speed, never results.
+__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nblk) {
+    const int64_t x = bid % 8, q = nblk / 8, r = nblk % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// Tile order for the persistent MLP kernels: the tiles are split into 8 contiguous ranges, one
+// per XCD group (blockIdx % 8), and the waves of that group's blocks walk their range
+// interleaved, so at any moment one XCD works on a few consecutive frames and their group-mean
+// rows stay in its L2.  Returns this wave's first tile and stride; tiles stop at t_end.
+struct TileWalk { int64_t first, stride, end; };
+__device__ __forceinline__ TileWalk xcd_tiles(int64_t ntiles, int waves_per_block, int wave) {
+    const int64_t nb = gridDim.x, x = blockIdx.x % 8, i = blockIdx.x / 8;
+    const int64_t q = nb / 8, r = nb % 8;
+    const int64_t nbx = q + (x < r ? 1 : 0);              // blocks in this XCD group
+    const int64_t before = x * q + min<int64_t>(x, r);     // blocks in earlier groups
+    const int64_t t0 = ntiles * before / nb, t1 = ntiles * (before + nbx) / nb;
+    return {t0 + i * waves_per_block + wave, nbx * waves_per_block, t1};
+}
+
+}  // namespace ldpc

@@ -1,0 +1,553 @@
+// gnn_bf16.hip -- message-GNN forward, bf16 features on v_mfma_f32_32x32x16_bf16 (precision 1).
+//
+// Same layer as gnn.hip (message_gnn_decoder.py:51-129, :190-317), re-associated so that the
+// per-message work is MFMA + a few VALU ops:
+//
+//   MLP_s([c; g]) with c = x + emb[type] and g the group mean of c (s = var side / check side)
+//     W1_s [c; g] + b1_s = W1_s,left x  +  (W1_s,left emb[type] + b1_s)  +  W1_s,right g
+//   The bracket depends only on (layer, type, side): a "type constant" K[t][s], computed once
+//   per forward by gnn_bf16_kconst_kernel and used as the GEMM1 accumulator's initial value.
+//   Layer 0 has x = w_in llr + b_in, so W1_s,left x = llr * (W1_s,left w_in) + W1_s,left b_in:
+//   two more constant vectors (U, V) and GEMM1 over x disappears.
+//   The group means keep the emb part: g = mean(x) + mean(emb[type]) where the second term is
+//   a per-(layer, group) constant (gnn_bf16_memb_kernel).
+//
+// Feature storage order.  A 64-feature row is stored permuted: stored position p = 16 s + 8 h + i
+// holds logical unit pi(p) = 32 (s>>1) + 16 (s&1) + 8 (i>>2) + 4 h + (i&3).  Then the 16-byte
+// chunk s that lane (j, h) loads as the k-step-s B operand of GEMM1 holds exactly the units that
+// the same lane owns in its 32x32 accumulator (row tile s>>1, registers 8 (s&1) .. +7).  So the
+// residual add needs no reload and no shuffle, and the output row is written as four 16-B
+// chunks straight from the accumulators.  W1's columns are permuted to match; Mv/Mc rows use
+// the same order; the logical order never appears in memory.
+//
+// Kernels per layer:
+//   gnn_bf16_gm_kernel   group means (bf16 rows).  One wave sums 8 groups of one degree (a
+//                        "group tile", see gnn.hpp), 8 lanes x 16 B per 128-B row.
+//   gnn_bf16_mlp_kernel  persistent, weights (bf16) + type constants in LDS; one wave per
+//                        32-message tile: GEMM1 (K = 64 x-part + 64 group-part) -> ReLU -> GEMM2
+//                        for both sides into one accumulator, + b2v + b2c + residual, bf16 out.
+//                        Last layer: output projection + per-variable sum instead.
+#include <cstdint>
+#include <string>
+
+#include "common.hpp"
+#include "gnn.hpp"
+
+namespace ldpc {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int H = 64;
+
+__host__ __device__ constexpr int pi_unit(int p) {
+    return 32 * (p >> 5) + 16 * ((p >> 4) & 1) + 8 * ((p >> 2) & 1) + 4 * ((p >> 3) & 1) + (p & 3);
+}
+// accumulator order: index a = 32 rt + 16 h + r (row tile rt, lane half h, register r) -> unit
+__host__ __device__ constexpr int acc_unit(int a) {
+    return 32 * (a >> 5) + (a & 3) + 8 * ((a >> 2) & 3) + 4 * ((a >> 4) & 1);
+}
+
+struct LayerW {
+    const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
+};
+__host__ __device__ inline int64_t layer_floats(int T) { return (int64_t)T * H + 2 * (2 * H * H + H + H * H + H) + H + 1; }
+__host__ __device__ inline LayerW layer_w(const float *blob, int T, int l) {
+    LayerW w;
+    w.emb = blob + 2 * H + (int64_t)l * layer_floats(T);
+    w.w1v = w.emb + (int64_t)T * H;
+    w.b1v = w.w1v + 2 * H * H;
+    w.w2v = w.b1v + H;
+    w.b2v = w.w2v + H * H;
+    w.w1c = w.b2v + H;
+    w.b1c = w.w1c + 2 * H * H;
+    w.w2c = w.b1c + H;
+    w.b2c = w.w2c + H * H;
+    w.wo = w.b2c + H;
+    w.bo = w.wo + H;
+    return w;
+}
+
+// derived constants per layer (floats): K[T + 2][2 sides][64 acc order] (rows T, T+1 = U, V of
+// layer 0), then b2v + b2c [64 acc], wo [64 acc]
+__host__ __device__ inline int64_t kd_floats(int T) { return (int64_t)(T + 2) * 128 + 128; }
+
+__global__ __launch_bounds__(128) void gnn_bf16_kconst_kernel(const float *blob, int T, float *kd) {
+    const int l = blockIdx.x, t = blockIdx.y, side = threadIdx.x >> 6, a = threadIdx.x & 63;
+    const int u = acc_unit(a);
+    const LayerW w = layer_w(blob, T, l);
+    const float *W1 = (side ? w.w1c : w.w1v) + u * 2 * H;  // row u, left half = columns 0..63
+    const float *v = t < T ? w.emb + t * H : t == T ? blob : blob + H;  // emb[t] | w_in | b_in
+    float s = t < T ? (side ? w.b1c : w.b1v)[u] : 0.0f;
+    for (int k = 0; k < H; ++k) s = fmaf(W1[k], v[k], s);
+    float *out = kd + (int64_t)l * kd_floats(T);
+    out[(int64_t)t * 128 + side * 64 + a] = s;
+    if (t == 0 && side == 0) {
+        out[(int64_t)(T + 2) * 128 + a] = w.b2v[u] + w.b2c[u];
+        out[(int64_t)(T + 2) * 128 + 64 + a] = w.wo[u];
+    }
+}
+
+struct GtArgs {
+    const int2 *meta;
+    const int32_t *grp, *mem;
+    int n_tiles;
+};
+
+// memb[l][g][p] = mean over group g's messages of emb_l[type][pi(p)]  (one wave per (l, tile))
+__global__ __launch_bounds__(256) void gnn_bf16_memb_kernel(const float *blob, int T, int L, const int32_t *msg_type,
+                                                            GtArgs G, int Gtot, float *memb) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= (int64_t)L * G.n_tiles) return;
+    const int l = (int)(w / G.n_tiles), t = (int)(w - (int64_t)l * G.n_tiles);
+    const int lane = threadIdx.x & 63, q = lane >> 3, p0 = 8 * (lane & 7);
+    const int g = G.grp[8 * t + q];
+    if (g < 0) return;
+    const int2 md = G.meta[t];
+    const float *emb = layer_w(blob, T, l).emb;
+    float acc[8] = {};
+    for (int i = 0; i < md.x; ++i) {
+        const float *e = emb + msg_type[G.mem[md.y + 8 * i + q]] * H;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += e[pi_unit(p0 + k)];
+    }
+    float *o = memb + ((int64_t)l * Gtot + g) * H + p0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = acc[k] / (float)md.x;
+}
+
+// ------------------------------------------------------------------------ group means
+struct GmArgs {
+    const __bf16 *x_in;  // (B, E, 64) stored order; null at layer 0 (x = w_in llr + b_in)
+    const float *llr;
+    const int32_t *msg_var;
+    const float *w_in, *b_in;
+    const float *memb;   // this layer (Gv + Gc, 64) fp32
+    GtArgs G;
+    __bf16 *Mv, *Mc;
+    int Gv, Gc, E, N;
+    int64_t B;
+};
+
+__global__ __launch_bounds__(256) void gnn_bf16_gm_kernel(GmArgs A) {
+    const uint32_t w = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    if (w >= (uint32_t)(A.B * A.G.n_tiles)) return;
+    const uint32_t b = w / (uint32_t)A.G.n_tiles, t = w - b * (uint32_t)A.G.n_tiles;
+    const int lane = threadIdx.x & 63, q = lane >> 3, p0 = 8 * (lane & 7);
+    const int2 md = A.G.meta[t];
+    const int g = A.G.grp[8 * t + q];
+    const int32_t *mem = A.G.mem + md.y + q;
+    float acc[8] = {};
+    if (A.x_in) {
+        const __bf16 *xb = A.x_in + (int64_t)b * A.E * H + p0;
+        int i = 0;
+        for (; i + 4 <= md.x; i += 4) {
+            const int m0 = mem[8 * i], m1 = mem[8 * i + 8], m2 = mem[8 * i + 16], m3 = mem[8 * i + 24];
+            const bf16x8 v0 = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)m0 * H);
+            const bf16x8 v1 = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)m1 * H);
+            const bf16x8 v2 = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)m2 * H);
+            const bf16x8 v3 = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)m3 * H);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += ((float)v0[k] + (float)v1[k]) + ((float)v2[k] + (float)v3[k]);
+        }
+        for (; i < md.x; ++i) {
+            const bf16x8 v = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)mem[8 * i] * H);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += (float)v[k];
+        }
+    } else {
+        float ls = 0.0f;
+        for (int i = 0; i < md.x; ++i) ls += A.llr[(int64_t)b * A.N + A.msg_var[mem[8 * i]]];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int u = pi_unit(p0 + k);
+            acc[k] = fmaf(A.w_in[u], ls, (float)md.x * A.b_in[u]);
+        }
+    }
+    if (g < 0) return;
+    const float inv = 1.0f / (float)md.x;
+    const float4 e0 = *reinterpret_cast<const float4 *>(A.memb + (int64_t)g * H + p0);
+    const float4 e1 = *reinterpret_cast<const float4 *>(A.memb + (int64_t)g * H + p0 + 4);
+    const float e[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (__bf16)fmaf(acc[k], inv, e[k]);
+    __bf16 *dst = g < A.Gv ? A.Mv + ((int64_t)b * A.Gv + g) * H : A.Mc + ((int64_t)b * A.Gc + (g - A.Gv)) * H;
+    *reinterpret_cast<bf16x8 *>(dst + p0) = o;
+}
+
+// ------------------------------------------------------------------------ fused MLP
+// LDS image (bytes): W1v, W1c bf16 [64 u][136] (128 stored columns + 8 pad: conflict-free
+// ds_read_b128), W2v, W2c bf16 [64 o][72] (columns in GEMM1-accumulator order), then fp32:
+// K [T + 2][132] (two sides x 64 + 4 pad, so that lanes reading different types' rows spread
+// over the banks), b2 [64], wo [64].
+constexpr int kW1B = 64 * 136 * 2, kW2B = 64 * 72 * 2;
+constexpr int kOffW1v = 0, kOffW1c = kW1B, kOffW2v = 2 * kW1B, kOffW2c = 2 * kW1B + kW2B;
+constexpr int kOffK = 2 * kW1B + 2 * kW2B;
+constexpr int kKStride = 132;
+inline size_t mlp_lds_bytes(int T) { return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 128) * 4; }
+
+struct MlpArgs {
+    const __bf16 *x_in;  // null at layer 0
+    __bf16 *x_out;       // null at the last layer
+    const __bf16 *Mv, *Mc;
+    const int32_t *vgroup, *cgroup, *msg_type, *msg_var;
+    const float *llr;
+    const float *w1v, *w1c, *w2v, *w2c;  // this layer, nn.Linear layout, fp32
+    const float *kd;                     // this layer's derived constants
+    const float *bo;                     // output_projection bias (device)
+    int T, Gv, Gc, E, N, tpf;            // tpf = 32-message tiles per frame
+    int64_t B;
+    float *var_sum;                      // last layer: (B, N) sums of projected messages
+};
+
+__device__ __forceinline__ bf16x8 ld8(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
+__device__ __forceinline__ f32x16 ld16(const float *p) {
+    f32x16 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 f = reinterpret_cast<const float4 *>(p)[q];
+        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+    }
+    return v;
+}
+__device__ __forceinline__ bf16x8 relu8(const f32x16 &a, int half) {
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (__bf16)fmaxf(a[8 * half + i], 0.0f);
+    return o;
+}
+__device__ __forceinline__ bf16x8 pack8(const f32x16 &a, int half) {
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (__bf16)a[8 * half + i];
+    return o;
+}
+
+// Per-tile inputs of one lane (message j of the tile, lane half h).
+struct TileIn {
+    bf16x8 xf[4], af[4], cf[4];
+    float l;
+    int ty, var;
+    int64_t row;
+    bool ok;
+};
+
+// MODE bit 0: layer 0 (x from the LLRs, no GEMM1 over x, no residual); bit 1: last layer
+// (output projection + per-variable sum instead of writing x)
+template <int NT, int WPS, bool PF, int MODE>
+__global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 64 * 128; i += NT) {
+        const int u = i >> 7, p = i & 127;
+        const int k = p < 64 ? pi_unit(p) : 64 + pi_unit(p - 64);
+        reinterpret_cast<__bf16 *>(smem + kOffW1v)[u * 136 + p] = (__bf16)A.w1v[u * 128 + k];
+        reinterpret_cast<__bf16 *>(smem + kOffW1c)[u * 136 + p] = (__bf16)A.w1c[u * 128 + k];
+    }
+    for (int i = tid; i < 64 * 64; i += NT) {
+        const int o = i >> 6, q = i & 63;
+        const int u = pi_unit(q);  // GEMM2's k index = GEMM1 accumulator registers (see header)
+        reinterpret_cast<__bf16 *>(smem + kOffW2v)[o * 72 + q] = (__bf16)A.w2v[o * 64 + u];
+        reinterpret_cast<__bf16 *>(smem + kOffW2c)[o * 72 + q] = (__bf16)A.w2c[o * 64 + u];
+    }
+    float *Ks = reinterpret_cast<float *>(smem + kOffK);
+    const int nk = (A.T + 2) * 128;
+    for (int i = tid; i < nk; i += NT) Ks[(i >> 7) * kKStride + (i & 127)] = A.kd[i];
+    float *tail = Ks + (A.T + 2) * kKStride;  // b2 [64], wo [64]
+    if (tid < 128) tail[tid] = A.kd[nk + tid];
+    __syncthreads();
+
+    const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
+    constexpr bool layer0 = (MODE & 1) != 0, last = (MODE & 2) != 0;
+    const int64_t ntiles = A.B * A.tpf;
+    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
+    // frame / in-frame tile counters, advanced without divisions
+    const int64_t sb = tw.stride / A.tpf, sk = tw.stride - sb * A.tpf;
+    int64_t fb = tw.first / A.tpf, fk = tw.first - fb * A.tpf;
+
+    auto load = [&](int64_t t, int64_t b, int64_t k) {
+        TileIn I;
+        const int m0 = (int)k * 32 + j;
+        I.ok = m0 < A.E && t < tw.end;
+        const int m = m0 < A.E ? m0 : A.E - 1;
+        const int64_t bb = t < tw.end ? b : fb;
+        I.ty = A.msg_type[m];
+        I.var = A.msg_var[m];
+        const int vg = A.vgroup[m], cg = A.cgroup[m];
+        I.row = bb * A.E + m;
+        const char *ma = reinterpret_cast<const char *>(A.Mv + (bb * A.Gv + vg) * H) + 16 * h;
+        const char *mc = reinterpret_cast<const char *>(A.Mc + (bb * A.Gc + cg) * H) + 16 * h;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            I.af[s] = ld8(ma + 32 * s);
+            I.cf[s] = ld8(mc + 32 * s);
+        }
+        if constexpr (!layer0) {
+            const char *xr = reinterpret_cast<const char *>(A.x_in + I.row * H) + 16 * h;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) I.xf[s] = ld8(xr + 32 * s);
+            I.l = 0.0f;
+        } else {
+            I.l = A.llr[bb * A.N + I.var];
+        }
+        return I;
+    };
+
+    auto compute = [&](const TileIn &I, int64_t b) {
+        const float *Kt = Ks + I.ty * kKStride;
+        f32x16 y0 = ld16(tail + 16 * h), y1 = ld16(tail + 32 + 16 * h);  // b2v + b2c
+        int wbase = j * 272 + 16 * h, w2base = j * 144 + 16 * h;
+        asm volatile("" : "+v"(wbase), "+v"(w2base));
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const char *W1 = smem + (side == 0 ? kOffW1v : kOffW1c);
+            const char *W2 = smem + (side == 0 ? kOffW2v : kOffW2c);
+            f32x16 h0 = ld16(Kt + side * 64 + 16 * h), h1 = ld16(Kt + side * 64 + 32 + 16 * h);
+            if constexpr (layer0) {  // + llr * (W1 w_in) + W1 b_in
+                const float *U = Ks + A.T * kKStride + side * 64 + 16 * h, *V = U + kKStride;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    h0[r] += fmaf(I.l, U[r], V[r]);
+                    h1[r] += fmaf(I.l, U[32 + r], V[32 + r]);
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + wbase + 32 * s), I.xf[s], h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * s), I.xf[s], h1, 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const bf16x8 g = side == 0 ? I.af[s] : I.cf[s];
+                h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + wbase + 32 * (4 + s)), g, h0, 0, 0, 0);
+                h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * (4 + s)), g, h1, 0, 0, 0);
+            }
+            const bf16x8 p00 = relu8(h0, 0), p01 = relu8(h0, 1), p10 = relu8(h1, 0), p11 = relu8(h1, 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bf16x8 bop = q == 0 ? p00 : q == 1 ? p01 : q == 2 ? p10 : p11;
+                const int qb = w2base + 32 * q;
+                y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W2 + qb), bop, y0, 0, 0, 0);
+                y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W2 + 32 * 144 + qb), bop, y1, 0, 0, 0);
+            }
+        }
+        if constexpr (!layer0) {  // residual (message_gnn_decoder.py:261): chunk s <-> y_{s>>1}[8 (s&1) ..]
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                y0[i] += (float)I.xf[0][i];
+                y0[8 + i] += (float)I.xf[1][i];
+                y1[i] += (float)I.xf[2][i];
+                y1[8 + i] += (float)I.xf[3][i];
+            }
+        }
+        if constexpr (last) {
+            const float *wo = tail + 64;
+            float part = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                part = fmaf(y0[r], wo[16 * h + r], part);
+                part = fmaf(y1[r], wo[32 + 16 * h + r], part);
+            }
+            part += __shfl_xor(part, 32, 64);
+            if (I.ok && h == 0) atomicAdd(&A.var_sum[b * A.N + I.var], part + A.bo[0]);
+        } else if (I.ok) {
+            char *xo = reinterpret_cast<char *>(A.x_out + I.row * H) + 16 * h;
+            *reinterpret_cast<bf16x8 *>(xo) = pack8(y0, 0);
+            *reinterpret_cast<bf16x8 *>(xo + 32) = pack8(y0, 1);
+            *reinterpret_cast<bf16x8 *>(xo + 64) = pack8(y1, 0);
+            *reinterpret_cast<bf16x8 *>(xo + 96) = pack8(y1, 1);
+        }
+    };
+
+    if (tw.first >= tw.end) return;
+    if constexpr (PF) {
+        TileIn cur = load(tw.first, fb, fk);
+        int64_t b = fb, k = fk;
+        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+            int64_t nb = b + sb, nk2 = k + sk;
+            if (nk2 >= A.tpf) { nk2 -= A.tpf; ++nb; }
+            const TileIn nxt = load(t + tw.stride, nb, nk2);
+            compute(cur, b);
+            cur = nxt;
+            b = nb;
+            k = nk2;
+        }
+    } else {
+        int64_t b = fb, k = fk;
+        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+            const TileIn cur = load(t, b, k);
+            compute(cur, b);
+            b += sb;
+            k += sk;
+            if (k >= A.tpf) { k -= A.tpf; ++b; }
+        }
+    }
+}
+
+__global__ void bf16_output_kernel(const float *__restrict__ var_sum, const float *__restrict__ llr, int64_t n,
+                                   float *__restrict__ probs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) probs[i] = 1.0f / (1.0f + expf(-(var_sum[i] + llr[i])));  // :298-307
+}
+
+struct Bf16Ws {
+    float *kd, *memb, *var_sum;
+    __bf16 *xa, *xb, *Mv, *Mc;
+    int64_t bytes;
+};
+
+Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *base) {
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4);
+    const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
+    const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * N * 4);
+    char *c = static_cast<char *>(base);
+    Bf16Ws w;
+    w.kd = reinterpret_cast<float *>(c);
+    w.memb = reinterpret_cast<float *>(c + kd);
+    w.xa = reinterpret_cast<__bf16 *>(c + kd + memb);
+    w.xb = reinterpret_cast<__bf16 *>(c + kd + memb + xa);
+    w.Mv = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb);
+    w.Mc = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb + mv);
+    w.var_sum = reinterpret_cast<float *>(c + kd + memb + xa + xb + mv + mc);
+    w.bytes = kd + memb + xa + xb + mv + mc + vs;
+    return w;
+}
+
+int g_cus = 0;
+
+template <int NT, int WPS, bool PF, int MODE>
+int launch_mlp_t(int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
+    const void *fn = reinterpret_cast<const void *>(gnn_bf16_mlp_kernel<NT, WPS, PF, MODE>);
+    LDPC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int per_cu = 4 * WPS / (NT / 64);  // workgroups per CU at WPS waves per SIMD
+    const unsigned grid = (unsigned)std::min<int64_t>((tiles + NT / 64 - 1) / (NT / 64), (int64_t)g_cus * per_cu);
+    hipLaunchKernelGGL((gnn_bf16_mlp_kernel<NT, WPS, PF, MODE>), dim3(grid), dim3(NT), lds, s, m);
+    return LDPC_OK;
+}
+
+template <int NT, int WPS, bool PF>
+int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
+    switch (mode) {
+        case 0: return launch_mlp_t<NT, WPS, PF, 0>(tiles, lds, s, m);
+        case 1: return launch_mlp_t<NT, WPS, PF, 1>(tiles, lds, s, m);
+        case 2: return launch_mlp_t<NT, WPS, PF, 2>(tiles, lds, s, m);
+        default: return launch_mlp_t<NT, WPS, PF, 3>(tiles, lds, s, m);
+    }
+}
+
+// LDPC_GNN_BF16_MLP selects the MLP kernel's occupancy / pipelining (speed only):
+//   0 = 768 threads, 3 waves/SIMD, no register prefetch (default)
+//   1 = 256 threads, 2 waves/SIMD, next tile prefetched into registers
+//   2 = 512 threads, 4 waves/SIMD, no prefetch
+int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
+    switch (variant) {
+        case 1: return launch_mlp_v<256, 2, true>(mode, tiles, lds, s, m);
+        case 2: return launch_mlp_v<512, 4, false>(mode, tiles, lds, s, m);
+        default: return launch_mlp_v<768, 3, false>(mode, tiles, lds, s, m);
+    }
+}
+int mlp_variant() {
+    static int v = [] {
+        const char *e = std::getenv("LDPC_GNN_BF16_MLP");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+}  // namespace
+
+int64_t gnn_bf16_workspace(const ldpc_gnn_plan *p, int N, int64_t B, int layers) {
+    return carve_bf16(p, N, B, kBf16MaxTypes, layers, nullptr).bytes;
+}
+
+int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weights, const int32_t *d_msg_type,
+                     const int32_t *d_msg_var, const float *d_llr, int N, int64_t B, float *d_probs, void *d_work,
+                     int64_t work_bytes, hipStream_t s) {
+    if (!p->n_gtiles) return fail(LDPC_EUNSUPPORTED, "plan has no group tiles");
+    Bf16Ws w = carve_bf16(p, N, B, T, L, d_work);
+    if (!d_work || work_bytes < w.bytes)
+        return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
+    const int64_t tpf = (p->E + 31) / 32;
+    if (B * tpf >= (1LL << 31) || B * p->n_gtiles >= (1LL << 31) || p->E >= (1LL << 31))
+        return fail(LDPC_EUNSUPPORTED, "batch too large for one launch (chunk it)");
+    const size_t lds = mlp_lds_bytes(T);
+    if (T > kBf16MaxTypes || lds > 160 * 1024)
+        return fail(LDPC_EUNSUPPORTED, "too many message types for the bf16 LDS image");
+    if (!g_cus) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const GtArgs G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles};
+    const int Gtot = p->Gv + p->Gc;
+    hipLaunchKernelGGL(gnn_bf16_kconst_kernel, dim3(L, T + 2), dim3(128), 0, s, d_weights, T, w.kd);
+    LDPC_CHECK_LAUNCH("gnn_bf16_kconst_kernel");
+    hipLaunchKernelGGL(gnn_bf16_memb_kernel, dim3((unsigned)(((int64_t)L * p->n_gtiles + 3) / 4)), dim3(256), 0, s,
+                       d_weights, T, L, d_msg_type, G, Gtot, w.memb);
+    LDPC_CHECK_LAUNCH("gnn_bf16_memb_kernel");
+    LDPC_HIP(hipMemsetAsync(w.var_sum, 0, (size_t)B * N * 4, s));
+
+    const __bf16 *x_in = nullptr;
+    for (int l = 0; l < L; ++l) {
+        const LayerW lw = layer_w(d_weights, T, l);
+        GmArgs gm{};
+        gm.x_in = x_in;
+        gm.llr = d_llr;
+        gm.msg_var = d_msg_var;
+        gm.w_in = d_weights;
+        gm.b_in = d_weights + H;
+        gm.memb = w.memb + (int64_t)l * Gtot * H;
+        gm.G = G;
+        gm.Mv = w.Mv;
+        gm.Mc = w.Mc;
+        gm.Gv = p->Gv;
+        gm.Gc = p->Gc;
+        gm.E = (int)p->E;
+        gm.N = N;
+        gm.B = B;
+        const int64_t gwaves = B * p->n_gtiles;
+        hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, s, gm);
+        LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
+
+        MlpArgs m{};
+        m.x_in = x_in;
+        m.x_out = l == L - 1 ? nullptr : (l % 2 == 0 ? w.xa : w.xb);
+        m.Mv = w.Mv;
+        m.Mc = w.Mc;
+        m.vgroup = p->vgroup;
+        m.cgroup = p->cgroup;
+        m.msg_type = d_msg_type;
+        m.msg_var = d_msg_var;
+        m.llr = d_llr;
+        m.w1v = lw.w1v;
+        m.w1c = lw.w1c;
+        m.w2v = lw.w2v;
+        m.w2c = lw.w2c;
+        m.kd = w.kd + (int64_t)l * kd_floats(T);
+        m.bo = lw.bo;
+        m.T = T;
+        m.Gv = p->Gv;
+        m.Gc = p->Gc;
+        m.E = (int)p->E;
+        m.N = N;
+        m.tpf = (int)tpf;
+        m.B = B;
+        m.var_sum = w.var_sum;
+        const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0);
+        const int rc = launch_mlp(mlp_variant(), mode, B * tpf, lds, s, m);
+        if (rc != LDPC_OK) return rc;
+        LDPC_CHECK_LAUNCH("gnn_bf16_mlp_kernel");
+        x_in = m.x_out;
+    }
+    const int64_t n = B * N;
+    hipLaunchKernelGGL(bf16_output_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.var_sum, d_llr, n,
+                       d_probs);
+    LDPC_CHECK_LAUNCH("bf16_output_kernel");
+    return LDPC_OK;
+}
+
+}  // namespace ldpc

@@ -143,6 +143,7 @@ class MessageGNNDecoder(nn.Module):
                                          for _ in range(num_iterations)])
         self.output_layer = nn.Linear(hidden_dim, 1)  # unused by forward (:188), kept for state_dicts
         self.precision = "fp32"  # or "bf16": bf16 MLP operands, fp32 accumulate
+        self.default_chunk = 0   # frames per native launch (0 = the whole batch, within budget)
         self._plans = {}
         self._blob_key = None
         self._blob = None
@@ -184,9 +185,12 @@ class MessageGNNDecoder(nn.Module):
         probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
         if B == 0:
             return probs
-        per_frame = N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, self.hidden_dim, Nv, 1, L, prec))
+        ws1 = N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, self.hidden_dim, Nv, 1, L, prec))
+        per_frame = N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, self.hidden_dim, Nv, 2, L, prec)) - ws1
         budget = int(os.environ.get("LDPC_GNN_WORKSPACE_BYTES", 48 << 30))
-        chunk = chunk or max(1, min(B, budget // max(per_frame, 1)))
+        # frames per launch: bounded by the workspace budget and by LDPC_GNN_CHUNK (speed only)
+        chunk = chunk or int(os.environ.get("LDPC_GNN_CHUNK", 0)) or self.default_chunk
+        chunk = max(1, min(B, chunk or B, max(1, (budget - ws1) // max(per_frame, 1))))
         wsb = N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, self.hidden_dim, Nv, chunk, L, prec))
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         for s in range(0, B, chunk):
