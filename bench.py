@@ -15,6 +15,7 @@ Workloads (BASELINE.json configs):
   gnn-z4      cfg2: BG2 Z=4, MessageGNN 5 layers, H=64, T=4, B=4096, fp32
   gnn-z32     cfg4 per GPU: BG2 Z=32, MessageGNN 10 layers, H=64, T=32, B=32768/GPU, fp32
   gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate)
+  gnn-z32-bf16-i10  cfg4 shape (10 layers) on the bf16 path: the north-star "10 iterations" GNN line
 """
 import argparse
 import json
@@ -42,6 +43,7 @@ WORKLOADS = {
     "gnn-z32": ("gnn", 32, 10, 32768, 2.0),
     "gnn-z32-bf16": ("gnn-bf16", 32, 15, 32768, 2.0),
     "gnn-z4-bf16": ("gnn-bf16", 4, 5, 4096, 2.0),
+    "gnn-z32-bf16-i10": ("gnn-bf16", 32, 10, 32768, 2.0),
 }
 
 
@@ -100,36 +102,61 @@ def barrier(world):
 
 
 def cpu_baseline(workload, z, iters, target_s):
-    """The oracle (oracle/ldpc_oracle.c, single thread, the reference's literal loop order) on a
-    bounded sample of the same workload, timed on this host's cores."""
+    """The CPU restatement of the same workload (oracle/: ldpc_oracle.c single-threaded for the
+    flooding decoders, the reference's literal loop order; oracle.gnn_forward in torch fp32 on
+    torch's CPU threads for the GNN) on a bounded sample of ~target_s seconds, on this host."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     kind, _, _, _, snr = WORKLOADS[workload]
-    H = oracle.expand(oracle.load_base(os.path.join(ROOT, "codes", f"NR_2_0_{z}.txt")), z)
+    base = oracle.load_base(os.path.join(ROOT, "codes", f"NR_2_0_{z}.txt"))
+    H = oracle.expand(base, z)
     g = oracle.Graph(H)
     rng = np.random.default_rng(0)
     s = 10 ** (snr / 10)
+    cpu = platform.processor() or platform.machine()
 
     def sample(b):
         noise = rng.normal(0.0, np.sqrt(1 / (2 * s)), size=(b, g.N))
         return (2 * s * (1 / np.sqrt(2) + noise)).astype(np.float32)
 
     if kind.startswith("gnn"):
-        return None
+        from ldpc_neural_decoder.models import create_message_gnn_decoder
+        torch.manual_seed(7)
+        dec, conv = create_message_gnn_decoder(torch.from_numpy(H), num_iterations=iters,
+                                               hidden_dim=64, base_graph=torch.from_numpy(base), Z=z)
+        sd = {k: v.detach() for k, v in dec.state_dict().items()}
+        types = conv.get_message_types(torch.from_numpy(base), z)
+        ev, ec = conv.edge_var, conv.edge_chk
+
+        def run(b):
+            with torch.no_grad():
+                oracle.gnn_forward(sd, torch.from_numpy(sample(b)), ev, ev, ec, g.N, g.M, types)
+        run(1)  # warm-up (thread pool, allocator)
+        b = 2
+        t0 = time.perf_counter()
+        run(b)
+        dt = max(time.perf_counter() - t0, 1e-6)
+        b = int(min(4096, max(2, b * target_s / dt)))
+        t0 = time.perf_counter()
+        run(b)
+        dt = time.perf_counter() - t0
+        return {"value": b / dt, "unit": "codewords/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"{b} frames, BG2 Z={z}, MessageGNN {iters} layers H=64 fp32, {snr} dB, "
+                          f"oracle.gnn_forward (torch CPU, segment means) on {cpu} with "
+                          f"{torch.get_num_threads()} threads, {dt:.1f} s"}
     algo = "minsum" if kind == "minsum" else "bp"
-    b = 4
+    b = 16
     t0 = time.perf_counter()
     oracle.flood_decode(g, sample(b), algo, iters, 0.75, 0)
     dt = max(time.perf_counter() - t0, 1e-6)
-    b = int(min(4096, max(8, b * target_s / dt)))
+    b = int(min(1 << 16, max(16, b * target_s / dt)))
     x = sample(b)
     t0 = time.perf_counter()
     oracle.flood_decode(g, x, algo, iters, 0.75, 0)
     dt = time.perf_counter() - t0
     return {"value": b / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
             "sample": f"{b} frames, BG2 Z={z}, {algo} {iters} it, {snr} dB, oracle/ldpc_oracle.c "
-                      f"single-threaded on {platform.processor() or platform.machine()} "
-                      f"(os.cpu_count()={os.cpu_count()}), {dt:.1f} s"}
+                      f"single-threaded on {cpu} (os.cpu_count()={os.cpu_count()}), {dt:.1f} s"}
 
 
 def main():
@@ -178,6 +205,7 @@ def main():
         io = conv.message_to_var_index().to(dev).to(torch.int32)
         probs = torch.empty((B, n), dtype=torch.float32, device=dev)
         vg, cg = conv.var_groups, conv.check_groups
+        g_m, g_n = H.shape
 
         def step(count):
             p = gdec.native_forward(llr, io, types, vg, cg)
@@ -187,9 +215,14 @@ def main():
 
         dtype = "bf16" if kind == "gnn-bf16" else "f32"
         E = len(conv.messages)
-        per_launch_alg = 12 * 64 * 64 * E * B * iters  # useful MLP FLOPs per forward
-        bound, unit = "mfma", "TFLOP/s"
-        peak = BF16_MFMA_PEAK_TFS if kind == "gnn-bf16" else FP32_MFMA_PEAK_TFS
+        if kind == "gnn-bf16":
+            # HBM-bound; per frame-layer 3 passes over the bf16 features
+            # (group-mean read, MLP read + write) + the fp32-sized group-mean rows written + read
+            per_launch_alg = iters * (3 * E * 64 * 2 + 2 * (g_n + g_m) * 64 * 4) * B
+            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+        else:
+            per_launch_alg = 12 * 64 * 64 * E * B * iters  # useful MLP FLOPs per forward
+            bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         dominant = "gnn forward (all layers)"
 
     for _ in range(a.warmup):

@@ -1,0 +1,16 @@
+# Bench lines for every workload (+ kernel-trace stats for the GNN ones) into gpurun_out/bench_all.
+set -o pipefail
+R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/bench_all; mkdir -p $OUT
+cd $R
+run() {  # name, args...
+  local n=$1; shift
+  timeout -k 10 400 python3 bench.py "$@" > $OUT/$n.json 2> $OUT/$n.err || { rc=$?; echo "bench $n rc=$rc"; tail -5 $OUT/$n.err; exit $rc; }
+  python3 -c "import json; d=json.load(open('$OUT/$n.json')); r=d['roofline']; c=d['cpu_baseline'] or {}; print('$n', round(d['value']), d['unit'], 'frac', round(r['frac'],3), 'kern_ms', round(r['kernel_ms'],2), 'cpu', c.get('value'))"
+}
+run minsum-z32 --steps 20 --warmup 3
+run bp-z4 --workload bp-z4 --batch 65536 --steps 10 --warmup 3 --cpu-baseline-seconds 5
+run gnn-z4 --workload gnn-z4 --steps 10 --warmup 3 --cpu-baseline-seconds 10
+run gnn-z4-bf16 --workload gnn-z4-bf16 --steps 10 --warmup 3 --cpu-baseline-seconds 0
+run gnn-z32 --workload gnn-z32 --steps 3 --warmup 1 --cpu-baseline-seconds 10
+run gnn-z32-bf16 --workload gnn-z32-bf16 --steps 3 --warmup 1 --cpu-baseline-seconds 0
+run gnn-z32-bf16-i10 --workload gnn-z32-bf16-i10 --steps 3 --warmup 1 --cpu-baseline-seconds 10
