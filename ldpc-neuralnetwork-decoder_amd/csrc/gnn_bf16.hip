@@ -89,6 +89,12 @@ __global__ __launch_bounds__(128) void gnn_bf16_kconst_kernel(const float *blob,
     }
 }
 
+__global__ void gnn_bf16_info_kernel(int E, const int32_t *vgroup, const int32_t *cgroup, const int32_t *msg_type,
+                                     const int32_t *msg_var, int4 *info) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < E) info[m] = make_int4(vgroup[m], cgroup[m], msg_type[m], msg_var[m]);
+}
+
 struct GtArgs {
     const int2 *meta;
     const int32_t *grp, *mem;
@@ -192,7 +198,7 @@ struct MlpArgs {
     const __bf16 *x_in;  // null at layer 0
     __bf16 *x_out;       // null at the last layer
     const __bf16 *Mv, *Mc;
-    const int32_t *vgroup, *cgroup, *msg_type, *msg_var;
+    const int4 *info;                    // per message {var group, check group, type, variable}
     const float *llr;
     const float *w1v, *w1c, *w2v, *w2c;  // this layer, nn.Linear layout, fp32
     const float *kd;                     // this layer's derived constants
@@ -230,7 +236,7 @@ struct TileIn {
     bf16x8 xf[4], af[4], cf[4];
     float l;
     int ty, var;
-    int64_t row;
+    int64_t row, b;
     bool ok;
 };
 
@@ -267,23 +273,23 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     const int64_t sb = tw.stride / A.tpf, sk = tw.stride - sb * A.tpf;
     int64_t fb = tw.first / A.tpf, fk = tw.first - fb * A.tpf;
 
-    auto load = [&](int64_t t, int64_t b, int64_t k) {
+    // per-message static info {var group, check group, type, variable} of this lane's message
+    auto load_info = [&](int64_t k) {
+        const int m0 = (int)k * 32 + j;
+        return A.info[m0 < A.E ? m0 : A.E - 1];
+    };
+    auto load = [&](const int4 &inf, int64_t t, int64_t b, int64_t k) {
         TileIn I;
         const int m0 = (int)k * 32 + j;
         I.ok = m0 < A.E && t < tw.end;
         const int m = m0 < A.E ? m0 : A.E - 1;
         const int64_t bb = t < tw.end ? b : fb;
-        I.ty = A.msg_type[m];
-        I.var = A.msg_var[m];
-        const int vg = A.vgroup[m], cg = A.cgroup[m];
+        I.ty = inf.z;
+        I.var = inf.w;
         I.row = bb * A.E + m;
-        const char *ma = reinterpret_cast<const char *>(A.Mv + (bb * A.Gv + vg) * H) + 16 * h;
-        const char *mc = reinterpret_cast<const char *>(A.Mc + (bb * A.Gc + cg) * H) + 16 * h;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            I.af[s] = ld8(ma + 32 * s);
-            I.cf[s] = ld8(mc + 32 * s);
-        }
+        I.b = bb;
+        const char *ma = reinterpret_cast<const char *>(A.Mv + (bb * A.Gv + inf.x) * H) + 16 * h;
+        const char *mc = reinterpret_cast<const char *>(A.Mc + (bb * A.Gc + inf.y) * H) + 16 * h;
         if constexpr (!layer0) {
             const char *xr = reinterpret_cast<const char *>(A.x_in + I.row * H) + 16 * h;
 #pragma unroll
@@ -292,10 +298,14 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         } else {
             I.l = A.llr[bb * A.N + I.var];
         }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) I.cf[s] = ld8(mc + 32 * s);
         return I;
     };
 
-    auto compute = [&](const TileIn &I, int64_t b) {
+    auto compute = [&](const TileIn &I) {
         const float *Kt = Ks + I.ty * kKStride;
         f32x16 y0 = ld16(tail + 16 * h), y1 = ld16(tail + 32 + 16 * h);  // b2v + b2c
         int wbase = j * 272 + 16 * h, w2base = j * 144 + 16 * h;
@@ -352,7 +362,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                 part = fmaf(y1[r], wo[32 + 16 * h + r], part);
             }
             part += __shfl_xor(part, 32, 64);
-            if (I.ok && h == 0) atomicAdd(&A.var_sum[b * A.N + I.var], part + A.bo[0]);
+            if (I.ok && h == 0) atomicAdd(&A.var_sum[I.b * A.N + I.var], part + A.bo[0]);
         } else if (I.ok) {
             char *xo = reinterpret_cast<char *>(A.x_out + I.row * H) + 16 * h;
             *reinterpret_cast<bf16x8 *>(xo) = pack8(y0, 0);
@@ -364,25 +374,29 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
 
     if (tw.first >= tw.end) return;
     if constexpr (PF) {
-        TileIn cur = load(tw.first, fb, fk);
+        TileIn cur = load(load_info(fk), tw.first, fb, fk);
         int64_t b = fb, k = fk;
         for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
             int64_t nb = b + sb, nk2 = k + sk;
             if (nk2 >= A.tpf) { nk2 -= A.tpf; ++nb; }
-            const TileIn nxt = load(t + tw.stride, nb, nk2);
-            compute(cur, b);
+            const TileIn nxt = load(load_info(nk2), t + tw.stride, nb, nk2);
+            compute(cur);
             cur = nxt;
             b = nb;
             k = nk2;
         }
     } else {
+        // the next tile's message info is fetched one tile ahead, so each tile's row loads
+        // start at once instead of behind a dependent index load
         int64_t b = fb, k = fk;
+        int4 inf = load_info(k);
         for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-            const TileIn cur = load(t, b, k);
-            compute(cur, b);
+            const TileIn cur = load(inf, t, b, k);
             b += sb;
             k += sk;
             if (k >= A.tpf) { k -= A.tpf; ++b; }
+            inf = load_info(k < A.tpf ? k : 0);
+            compute(cur);
         }
     }
 }
@@ -395,6 +409,7 @@ __global__ void bf16_output_kernel(const float *__restrict__ var_sum, const floa
 
 struct Bf16Ws {
     float *kd, *memb, *var_sum;
+    int4 *info;
     __bf16 *xa, *xb, *Mv, *Mc;
     int64_t bytes;
 };
@@ -404,8 +419,10 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4);
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
     const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * N * 4);
+    const int64_t inf = al(p->E * 16);
     char *c = static_cast<char *>(base);
     Bf16Ws w;
+    w.info = reinterpret_cast<int4 *>(c + kd + memb + xa + xb + mv + mc + vs);
     w.kd = reinterpret_cast<float *>(c);
     w.memb = reinterpret_cast<float *>(c + kd);
     w.xa = reinterpret_cast<__bf16 *>(c + kd + memb);
@@ -413,7 +430,7 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     w.Mv = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb);
     w.Mc = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb + mv);
     w.var_sum = reinterpret_cast<float *>(c + kd + memb + xa + xb + mv + mc);
-    w.bytes = kd + memb + xa + xb + mv + mc + vs;
+    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf;
     return w;
 }
 
@@ -440,20 +457,21 @@ int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpAr
 }
 
 // LDPC_GNN_BF16_MLP selects the MLP kernel's occupancy / pipelining (speed only):
-//   0 = 768 threads, 3 waves/SIMD, no register prefetch (default)
-//   1 = 256 threads, 2 waves/SIMD, next tile prefetched into registers
-//   2 = 512 threads, 4 waves/SIMD, no prefetch
+//   1 = 256 threads, 2 waves/SIMD, next tile prefetched into registers (default)
+//   0 = 768 threads, 3 waves/SIMD, no register prefetch
+//   2 = 512 threads, 4 waves/SIMD, no prefetch (spills at 128 VGPRs)
 int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (variant) {
-        case 1: return launch_mlp_v<256, 2, true>(mode, tiles, lds, s, m);
+        case 0: return launch_mlp_v<768, 3, false>(mode, tiles, lds, s, m);
         case 2: return launch_mlp_v<512, 4, false>(mode, tiles, lds, s, m);
-        default: return launch_mlp_v<768, 3, false>(mode, tiles, lds, s, m);
+        default: return launch_mlp_v<256, 2, true>(mode, tiles, lds, s, m);
     }
 }
+
 int mlp_variant() {
     static int v = [] {
         const char *e = std::getenv("LDPC_GNN_BF16_MLP");
-        return e ? std::atoi(e) : 0;
+        return e ? std::atoi(e) : 1;
     }();
     return v;
 }
@@ -484,6 +502,9 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     }
     const GtArgs G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles};
     const int Gtot = p->Gv + p->Gc;
+    hipLaunchKernelGGL(gnn_bf16_info_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, (int)p->E,
+                       p->vgroup, p->cgroup, d_msg_type, d_msg_var, w.info);
+    LDPC_CHECK_LAUNCH("gnn_bf16_info_kernel");
     hipLaunchKernelGGL(gnn_bf16_kconst_kernel, dim3(L, T + 2), dim3(128), 0, s, d_weights, T, w.kd);
     LDPC_CHECK_LAUNCH("gnn_bf16_kconst_kernel");
     hipLaunchKernelGGL(gnn_bf16_memb_kernel, dim3((unsigned)(((int64_t)L * p->n_gtiles + 3) / 4)), dim3(256), 0, s,
@@ -518,10 +539,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.x_out = l == L - 1 ? nullptr : (l % 2 == 0 ? w.xa : w.xb);
         m.Mv = w.Mv;
         m.Mc = w.Mc;
-        m.vgroup = p->vgroup;
-        m.cgroup = p->cgroup;
-        m.msg_type = d_msg_type;
-        m.msg_var = d_msg_var;
+        m.info = w.info;
         m.llr = d_llr;
         m.w1v = lw.w1v;
         m.w1c = lw.w1c;
