@@ -147,6 +147,26 @@ int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                      const float *d_llr, int N, int64_t B, int precision, float *d_probs,
                      void *d_work, int64_t work_bytes, void *stream);
 
+/* ---- training (fp32, hidden_dim <= 64) -------------------------------------------------------
+ * Replaces torch autograd through MessageGNNDecoder.forward + F.binary_cross_entropy
+ * (message_gnn_decoder.py:190-317, :314), as driven by trainer.py:70-102 (zero_grad, forward,
+ * loss.backward(), SGD step).
+ * ldpc_gnn_forward_train: the fp32 forward (same arguments as ldpc_gnn_forward, precision 0) that
+ *   also writes every layer's output features to d_saved (L, B, E, H) float32.
+ * ldpc_gnn_backward: given d_grad_probs = dLoss/dprobs (B, N), writes dLoss/dweights into
+ *   d_grad_weights, laid out exactly like the weight blob (zeroed first).  The output_projection of
+ *   every layer but the last gets zeros (the reference's forward never uses it: its grad is None).
+ * Both take a workspace of ldpc_gnn_train_workspace_size(...) bytes. */
+int64_t ldpc_gnn_train_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers);
+int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                           const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                           const float *d_llr, int N, int64_t B, float *d_probs, float *d_saved,
+                           void *d_work, int64_t work_bytes, void *stream);
+int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                      const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                      int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
+                      float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

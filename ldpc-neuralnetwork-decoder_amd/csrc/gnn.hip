@@ -65,7 +65,7 @@ struct GnnLayer {
     // group means
     float *Mv, *Mc;  // (B, Gv, H), (B, Gc, H)
     // outputs
-    float *x_out;    // (B, E, H), unused on the last layer
+    float *x_out;    // (B, E, H); null on the last layer unless training saves its features
     float *var_sum;  // (B, N), last layer only
     int residual, last;
 };
@@ -290,9 +290,8 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
                 if (P.last) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) part += vv[i] * wo[o0 + i];
-                } else if (ok) {
-                    *reinterpret_cast<float4 *>(P.x_out + row * H + o0) = v;
                 }
+                if (ok && P.x_out) *reinterpret_cast<float4 *>(P.x_out + row * H + o0) = v;
             }
         }
         if (P.last) {
@@ -340,7 +339,7 @@ __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H)
             float v = y[i];
             if (P.residual) v += P.x_in[row * H + o];
             if (P.last) part += v * P.wo[o];
-            else P.x_out[row * H + o] = v;
+            if (P.x_out) P.x_out[row * H + o] = v;
         }
         if (P.last) {
             for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
@@ -511,22 +510,11 @@ extern "C" int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, i
     return carve(p, hidden, N, B, layers, precision, nullptr).bytes;
 }
 
-extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
-                                const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
-                                int64_t B, int precision, float *d_probs, void *d_work, int64_t work_bytes,
-                                void *stream) {
-    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
-    if (hidden <= 0 || types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
-    if (precision != 0 && precision != 1) return fail(LDPC_EINVAL, "precision must be 0 (fp32) or 1 (bf16)");
-    if (precision == 1 && hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "bf16 path needs hidden_dim 64");
-    if (B == 0) return LDPC_OK;
-    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (precision == 1)
-        return gnn_bf16_forward(p, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs, d_work,
-                                work_bytes, s);
+int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                           const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
+                           float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s) {
     const int H = hidden;
-    Ws w = carve(p, H, N, B, layers, precision, d_work);
+    Ws w = carve(p, H, N, B, layers, 0, d_work);
     if (!d_work || work_bytes < w.bytes)
         return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
     if (!g_num_cus) {
@@ -574,7 +562,7 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
         L.x_in = x_in;
         L.residual = l > 0;
         L.last = l == layers - 1;
-        L.x_out = (l % 2 == 0) ? w.xa : w.xb;
+        L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H : L.last ? nullptr : (l % 2 == 0) ? w.xa : w.xb;
         L.var_sum = w.var_sum;
         const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
         if (H == 64)
@@ -604,4 +592,22 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
                        d_probs);
     LDPC_CHECK_LAUNCH("gnn_output_kernel");
     return LDPC_OK;
+}
+
+extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                                const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                                int64_t B, int precision, float *d_probs, void *d_work, int64_t work_bytes,
+                                void *stream) {
+    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    if (hidden <= 0 || types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
+    if (precision != 0 && precision != 1) return fail(LDPC_EINVAL, "precision must be 0 (fp32) or 1 (bf16)");
+    if (precision == 1 && hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "bf16 path needs hidden_dim 64");
+    if (B == 0) return LDPC_OK;
+    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (precision == 1)
+        return gnn_bf16_forward(p, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs, d_work,
+                                work_bytes, s);
+    return gnn_fp32_forward(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
+                            nullptr, d_work, work_bytes, s);
 }

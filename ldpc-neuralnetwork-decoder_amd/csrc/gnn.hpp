@@ -23,6 +23,12 @@ struct ldpc_gnn_plan {
 
 namespace ldpc {
 
+// fp32 forward (precision 0).  d_saved (L, B, E, H) or null: when set, layer l writes its output
+// features to d_saved[l] (the last layer included) for the backward pass (gnn_train.hip).
+int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                     const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
+                     float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s);
+
 // bf16 forward (precision 1, H = 64); same arguments as ldpc_gnn_forward.
 // The workspace is sized for the largest type count the LDS image admits (kBf16MaxTypes).
 constexpr int kBf16MaxTypes = 200;

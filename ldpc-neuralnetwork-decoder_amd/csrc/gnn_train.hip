@@ -1,0 +1,566 @@
+// gnn_train.hip -- backward pass of the message-GNN decoder (fp32), for training on the device.
+//
+// The reference trains with torch autograd through MessageGNNDecoder.forward + the BCE of
+// message_gnn_decoder.py:314 (loss.backward(), then SGD: trainer.py:70-102).  This file is that
+// backward, written out by hand.  The forward (gnn.hip, fp32) saves every layer's output features
+// x_{l+1}; the backward walks the layers in reverse and recomputes what it needs.
+//
+// Forward of layer l (message_gnn_decoder.py:51-129, :261), per message m of frame b:
+//   c = x_l + emb[t]          a = mean_{var group of m} c       q = mean_{check group of m} c
+//   u_v = W1v [c; a] + b1v    h_v = relu(u_v)    (same with W1c, [c; q] -> u_c, h_c)
+//   x_{l+1} = W2v h_v + b2v + W2c h_c + b2c (+ x_l if l > 0)
+// Head (:270-307): out_m = wo . x_L + bo,  z_v = llr_v + sum_{m -> v} out_m,  p = sigmoid(z).
+//
+// Backward, given G = dLoss/dp (from torch's BCE):
+//   dz = G p (1 - p);  dout_m = dz[var(m)];  dX_L = dout (x) wo;  dwo = sum dout x_L;  dbo = sum dout
+//   per layer, with dX = dLoss/dx_{l+1}:
+//     dW2s += dX (x) h_s, db2s += dX;  dh_s = (W2s^T dX) * [u_s > 0]
+//     dW1s += dh_s (x) [c; g_s], db1s += dh_s;  dz_s = W1s^T dh_s   (s = v, c;  g_v = a, g_c = q)
+//     dc = dz_v[:H] + dz_c[:H] + mean_{var group}(dz_v[H:]) + mean_{check group}(dz_c[H:])
+//          (the group-mean operator is symmetric, so its transpose is itself)
+//     demb[t] += dc;  dx_l = dc (+ dX if l > 0);   layer 0: dw_in += dc llr, db_in += dc
+//
+// Kernels (lanes = hidden units, H <= 64; VALU fp32 -- a training batch is small next to the
+// decode batches, and every product is an exact fp32 fma chain):
+//   train_group_mean_kernel  group means of c (or of any (B, E, H) array), one wave per group
+//   train_mlp_bwd_kernel     recompute u, h; dh, dz; writes c, h_v, h_c, dh_v, dh_c, dz parts
+//   train_combine_kernel     dc and dx_l
+//   train_outer_kernel       weight gradients sum_r A_r (x) Z_r (+ bias sums), split over rows
+//   train_vec_kernel         emb / input-embedding / output-projection gradients
+#include <cstdint>
+#include <string>
+
+#include "common.hpp"
+#include "gnn.hpp"
+
+namespace ldpc {
+namespace {
+
+constexpr int kMaxH = 64;
+
+struct TW {  // one layer's weights in the blob (see ldpc_amd.h)
+    const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
+};
+__host__ __device__ inline int64_t tl_floats(int H, int T) {
+    return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1;
+}
+template <typename P>
+__host__ __device__ inline void t_layer(P blob, int H, int T, int l, P *out) {  // 11 section pointers
+    P e = blob + 2 * H + (int64_t)l * tl_floats(H, T);
+    out[0] = e;                           // emb
+    out[1] = out[0] + (int64_t)T * H;     // w1v
+    out[2] = out[1] + 2LL * H * H;        // b1v
+    out[3] = out[2] + H;                  // w2v
+    out[4] = out[3] + (int64_t)H * H;     // b2v
+    out[5] = out[4] + H;                  // w1c
+    out[6] = out[5] + 2LL * H * H;        // b1c
+    out[7] = out[6] + H;                  // w2c
+    out[8] = out[7] + (int64_t)H * H;     // b2c
+    out[9] = out[8] + H;                  // wo
+    out[10] = out[9] + H;                 // bo
+}
+
+// ------------------------------------------------------------------------ head
+__global__ void train_head_kernel(const float *__restrict__ p, const float *__restrict__ g, int64_t n,
+                                  float *__restrict__ dz) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dz[i] = g[i] * (p[i] * (1.0f - p[i]));  // d sigmoid
+}
+
+// dX_L[r][u] = dz[b][var(m)] * wo[u]
+__global__ void train_dx_last_kernel(const float *__restrict__ dz, const int32_t *__restrict__ msg_var,
+                                     const float *__restrict__ wo, int H, int64_t E, int N, int64_t n,
+                                     float *__restrict__ dX) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = i / H;
+    const int u = (int)(i - r * H);
+    const int64_t b = r / E, m = r - b * E;
+    dX[i] = dz[b * N + msg_var[m]] * wo[u];
+}
+
+// ------------------------------------------------------------------------ group means
+// src_mode 0: src is the (B, E, H) array itself; 1: c = src + emb[type]; 2: c = w_in llr + b_in + emb
+struct GmT {
+    const float *src, *emb, *llr, *w_in, *b_in;
+    const int32_t *msg_type, *msg_var, *ptr, *mem;
+    const float *inv;
+    float *dst;  // (B, G, H)
+    int src_mode, G, H, N;
+    int64_t E, B;
+};
+
+__device__ __forceinline__ float c_value(const GmT &A, int64_t b, int64_t m, int u) {
+    float v;
+    if (A.src_mode == 2) v = A.w_in[u] * A.llr[b * A.N + A.msg_var[m]] + A.b_in[u];
+    else v = A.src[(b * A.E + m) * A.H + u];
+    if (A.src_mode != 0) v += A.emb[A.msg_type[m] * A.H + u];
+    return v;
+}
+
+__global__ __launch_bounds__(256) void train_group_mean_kernel(GmT A) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int u = threadIdx.x & 63;
+    if (w >= A.B * A.G || u >= A.H) return;
+    const int64_t b = w / A.G;
+    const int g = (int)(w - b * A.G);
+    float s = 0.0f;
+    for (int q = A.ptr[g]; q < A.ptr[g + 1]; ++q) s += c_value(A, b, A.mem[q], u);
+    A.dst[w * A.H + u] = s * A.inv[g];
+}
+
+// ------------------------------------------------------------------------ MLP backward
+constexpr int kNM = 4;  // rows per wave and step (share every weight read from LDS)
+
+struct MlpT {
+    const float *x, *llr, *w_in, *b_in;  // x = x_l (null at layer 0)
+    const float *Mv, *Mc, *dX;
+    const int32_t *msg_type, *msg_var, *vgroup, *cgroup;
+    const float *emb, *w1v, *b1v, *w2v, *w1c, *b1c, *w2c;
+    float *cbuf, *hv, *hc, *dhv, *dhc, *dco, *da, *db;
+    int H, N, Gv, Gc;
+    int64_t E, R;  // R = B E rows
+};
+
+// LDS (floats): W1v, W1c [H][2H + 1]; W2v, W2c [H][H + 1]; b1v, b1c [H];
+// per wave: z [kNM][3H] (c | a | q), dX [kNM][H], dh [kNM][2][H]
+inline size_t mlp_bwd_lds(int H) {
+    return ((size_t)2 * H * (2 * H + 1) + 2 * H * (H + 1) + 2 * H + 4 * (size_t)kNM * (3 * H + H + 2 * H)) * 4;
+}
+
+__global__ __launch_bounds__(256) void train_mlp_bwd_kernel(MlpT A) {
+    extern __shared__ float sm[];
+    const int H = A.H, H2 = 2 * H, S1 = H2 + 1, S2 = H + 1;
+    float *W1v = sm, *W1c = W1v + H * S1, *W2v = W1c + H * S1, *W2c = W2v + H * S2;
+    float *b1v = W2c + H * S2, *b1c = b1v + H;
+    const int wave = threadIdx.x >> 6, u = threadIdx.x & 63;
+    float *z = b1c + H + wave * kNM * 6 * H, *dXs = z + kNM * 3 * H, *dh = dXs + kNM * H;
+    for (int i = threadIdx.x; i < H * H2; i += 256) {
+        const int o = i / H2, k = i - o * H2;
+        W1v[o * S1 + k] = A.w1v[i];
+        W1c[o * S1 + k] = A.w1c[i];
+    }
+    for (int i = threadIdx.x; i < H * H; i += 256) {
+        const int o = i / H, k = i - o * H;
+        W2v[o * S2 + k] = A.w2v[i];
+        W2c[o * S2 + k] = A.w2c[i];
+    }
+    if (threadIdx.x < H) {
+        b1v[threadIdx.x] = A.b1v[threadIdx.x];
+        b1c[threadIdx.x] = A.b1c[threadIdx.x];
+    }
+    __syncthreads();
+    const bool lane_on = u < H;
+    const int64_t step = (int64_t)gridDim.x * 4 * kNM;
+    for (int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kNM; r0 - wave * kNM < A.R; r0 += step) {
+        // stage c | a | q and dX of this wave's kNM rows
+        float uv[kNM], uc[kNM];
+#pragma unroll
+        for (int i = 0; i < kNM; ++i) {
+            const int64_t r = r0 + i;
+            if (lane_on && r < A.R) {
+                const int64_t b = r / A.E, m = r - b * A.E;
+                const float c = (A.x ? A.x[r * H + u] : A.w_in[u] * A.llr[b * A.N + A.msg_var[m]] + A.b_in[u]) +
+                                A.emb[A.msg_type[m] * H + u];
+                z[i * 3 * H + u] = c;
+                z[i * 3 * H + H + u] = A.Mv[(b * A.Gv + A.vgroup[m]) * H + u];
+                z[i * 3 * H + H2 + u] = A.Mc[(b * A.Gc + A.cgroup[m]) * H + u];
+                dXs[i * H + u] = A.dX[r * H + u];
+                A.cbuf[r * H + u] = c;
+            } else if (lane_on) {
+                z[i * 3 * H + u] = z[i * 3 * H + H + u] = z[i * 3 * H + H2 + u] = 0.0f;
+                dXs[i * H + u] = 0.0f;
+            }
+        }
+        __syncthreads();
+        if (lane_on) {
+            // u_s = W1s [c; g_s] + b1s   (row u of W1, lanes on rows: stride 2H + 1, conflict-free)
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) { uv[i] = b1v[u]; uc[i] = b1c[u]; }
+            for (int k = 0; k < H; ++k) {  // c part, shared by both sides
+                const float wv = W1v[u * S1 + k], wc = W1c[u * S1 + k];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    const float c = z[i * 3 * H + k];
+                    uv[i] = fmaf(wv, c, uv[i]);
+                    uc[i] = fmaf(wc, c, uc[i]);
+                }
+            }
+            for (int k = 0; k < H; ++k) {
+                const float wv = W1v[u * S1 + H + k], wc = W1c[u * S1 + H + k];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    uv[i] = fmaf(wv, z[i * 3 * H + H + k], uv[i]);
+                    uc[i] = fmaf(wc, z[i * 3 * H + H2 + k], uc[i]);
+                }
+            }
+            // dh_s = (W2s^T dX) * [u_s > 0]   (column u of W2: lanes on columns)
+            float gv[kNM], gc[kNM];
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) gv[i] = gc[i] = 0.0f;
+            for (int o = 0; o < H; ++o) {
+                const float wv = W2v[o * S2 + u], wc = W2c[o * S2 + u];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    const float d = dXs[i * H + o];
+                    gv[i] = fmaf(wv, d, gv[i]);
+                    gc[i] = fmaf(wc, d, gc[i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) {
+                const int64_t r = r0 + i;
+                const float dv = uv[i] > 0.0f ? gv[i] : 0.0f, dc = uc[i] > 0.0f ? gc[i] : 0.0f;
+                dh[(i * 2) * H + u] = dv;
+                dh[(i * 2 + 1) * H + u] = dc;
+                if (r < A.R) {
+                    A.hv[r * H + u] = fmaxf(uv[i], 0.0f);
+                    A.hc[r * H + u] = fmaxf(uc[i], 0.0f);
+                    A.dhv[r * H + u] = dv;
+                    A.dhc[r * H + u] = dc;
+                }
+            }
+        }
+        __syncthreads();
+        if (lane_on) {
+            // dz_s[k] = sum_u W1s[u][k] dh_s[u] for k = u (c part) and k = H + u (group part)
+            float zc0[kNM], zv1[kNM], zc1[kNM];
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) zc0[i] = zv1[i] = zc1[i] = 0.0f;
+            float zv0[kNM];
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) zv0[i] = 0.0f;
+            for (int q = 0; q < H; ++q) {
+                const float wv0 = W1v[q * S1 + u], wv1 = W1v[q * S1 + H + u];
+                const float wc0 = W1c[q * S1 + u], wc1 = W1c[q * S1 + H + u];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    const float dv = dh[(i * 2) * H + q], dc = dh[(i * 2 + 1) * H + q];
+                    zv0[i] = fmaf(wv0, dv, zv0[i]);
+                    zv1[i] = fmaf(wv1, dv, zv1[i]);
+                    zc0[i] = fmaf(wc0, dc, zc0[i]);
+                    zc1[i] = fmaf(wc1, dc, zc1[i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) {
+                const int64_t r = r0 + i;
+                if (r < A.R) {
+                    A.dco[r * H + u] = zv0[i] + zc0[i];
+                    A.da[r * H + u] = zv1[i];
+                    A.db[r * H + u] = zc1[i];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// dc = dco + mean_var(da) + mean_chk(db) -> dco (kept for demb); dx_l = dc (+ dX)
+__global__ void train_combine_kernel(float *__restrict__ dco, const float *__restrict__ Mda,
+                                     const float *__restrict__ Mdb, const float *__restrict__ dX,
+                                     const int32_t *__restrict__ vgroup, const int32_t *__restrict__ cgroup, int H,
+                                     int Gv, int Gc, int64_t E, int64_t n, int residual, float *__restrict__ dx_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = i / H;
+    const int u = (int)(i - r * H);
+    const int64_t b = r / E, m = r - b * E;
+    const float dc = (dco[i] + Mda[(b * Gv + vgroup[m]) * H + u]) + Mdb[(b * Gc + cgroup[m]) * H + u];
+    dco[i] = dc;
+    dx_out[i] = residual ? dc + dX[i] : dc;
+}
+
+// ------------------------------------------------------------------------ weight gradients
+// out[i][j] += sum_r A[r][i] Z_r[j] (i < H, j < J), bias[i] += sum_r A[r][i];
+// Z_r = zsrc[r] (J = H), or [zsrc[r]; G[b][grp(m)]] (J = 2H, the concatenated MLP input)
+struct OuterT {
+    const float *A, *zsrc, *G;
+    const int32_t *grp;
+    float *out, *bias;
+    int H, J, Gn;
+    int64_t E, R;
+};
+constexpr int kRB = 16;  // rows staged per step
+
+__global__ __launch_bounds__(256) void train_outer_kernel(OuterT P) {
+    __shared__ float As[kRB][kMaxH];
+    __shared__ float Zs[kRB][2 * kMaxH];
+    const int t = threadIdx.x, i = t >> 2, jq = t & 3;
+    const int H = P.H, J = P.J, JW = J / 4;
+    float acc[32], bacc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) acc[k] = 0.0f;
+    const int64_t per = (P.R + gridDim.x - 1) / gridDim.x;
+    const int64_t r_begin = (int64_t)blockIdx.x * per, r_end = r_begin + per < P.R ? r_begin + per : P.R;
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += kRB) {
+        for (int e = t; e < kRB * H; e += 256) {
+            const int rr = e / H, k = e - rr * H;
+            const int64_t r = r0 + rr;
+            As[rr][k] = r < r_end ? P.A[r * H + k] : 0.0f;
+        }
+        for (int e = t; e < kRB * J; e += 256) {
+            const int rr = e / J, k = e - rr * J;
+            const int64_t r = r0 + rr;
+            float v = 0.0f;
+            if (r < r_end) {
+                if (k < H) {
+                    v = P.zsrc[r * H + k];
+                } else {
+                    const int64_t b = r / P.E, m = r - b * P.E;
+                    v = P.G[(b * P.Gn + P.grp[m]) * H + (k - H)];
+                }
+            }
+            Zs[rr][k] = v;
+        }
+        __syncthreads();
+        if (i < H) {
+            for (int rr = 0; rr < kRB; ++rr) {
+                const float a = As[rr][i];
+                bacc += a;
+#pragma unroll
+                for (int k = 0; k < 32; ++k)
+                    if (k < JW) acc[k] = fmaf(a, Zs[rr][jq * JW + k], acc[k]);
+            }
+        }
+        __syncthreads();
+    }
+    if (i < H) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k)
+            if (k < JW) atomicAdd(&P.out[i * J + jq * JW + k], acc[k]);
+        if (jq == 0 && P.bias) atomicAdd(&P.bias[i], bacc);
+    }
+}
+
+// per-row vector gradients, lanes = units:
+//   mode 0 (emb):  demb[type(m)][u] += src[r][u]
+//   mode 1 (input embedding, layer 0): dw_in[u] += src[r][u] llr[b][var(m)], db_in[u] += src[r][u]
+//   mode 2 (head): dwo[u] += dz[b][var(m)] src[r][u], dbo += dz[b][var(m)]
+struct VecT {
+    const float *src, *llr, *dz;
+    const int32_t *msg_type, *msg_var;
+    float *g0, *g1;  // mode 0: demb; 1: dw_in, db_in; 2: dwo, dbo
+    int H, T, N, mode;
+    int64_t E, R;
+};
+
+__global__ __launch_bounds__(256) void train_vec_kernel(VecT P) {
+    extern __shared__ float acc[];  // mode 0: [T][H]; else [4 waves][2][H]
+    const int wave = threadIdx.x >> 6, u = threadIdx.x & 63, H = P.H;
+    const int nacc = P.mode == 0 ? P.T * H : 4 * 2 * H;
+    for (int e = threadIdx.x; e < nacc; e += 256) acc[e] = 0.0f;
+    __syncthreads();
+    float s0 = 0.0f, s1 = 0.0f;
+    if (u < H) {
+        for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < P.R; r += (int64_t)gridDim.x * 4) {
+            const int64_t b = r / P.E, m = r - b * P.E;
+            const float v = P.src[r * H + u];
+            if (P.mode == 0) {
+                atomicAdd(&acc[P.msg_type[m] * H + u], v);
+            } else if (P.mode == 1) {
+                s0 = fmaf(v, P.llr[b * P.N + P.msg_var[m]], s0);
+                s1 += v;
+            } else {
+                const float d = P.dz[b * P.N + P.msg_var[m]];
+                s0 = fmaf(d, v, s0);
+                s1 += d;
+            }
+        }
+        if (P.mode != 0) {
+            acc[(wave * 2) * H + u] = s0;
+            acc[(wave * 2 + 1) * H + u] = s1;
+        }
+    }
+    __syncthreads();
+    if (P.mode == 0) {
+        for (int e = threadIdx.x; e < nacc; e += 256) atomicAdd(&P.g0[e], acc[e]);
+    } else if (threadIdx.x < H) {
+        const int k = threadIdx.x;
+        const float t0 = ((acc[k] + acc[2 * H + k]) + acc[4 * H + k]) + acc[6 * H + k];
+        const float t1 = ((acc[H + k] + acc[3 * H + k]) + acc[5 * H + k]) + acc[7 * H + k];
+        atomicAdd(&P.g0[k], t0);
+        if (P.mode == 1) atomicAdd(&P.g1[k], t1);
+        else if (k == 0) {  // dbo: every lane summed the same dz; take lane 0's
+            atomicAdd(&P.g1[0], t1);
+        }
+    }
+}
+
+struct TrainWs {
+    float *Mv, *Mc, *dz, *dX, *dXp, *cbuf, *hv, *hc, *dhv, *dhc, *dco, *da, *db, *Mda, *Mdb;
+    int64_t bytes;
+};
+
+TrainWs carve_train(const ldpc_gnn_plan *p, int H, int N, int64_t B, void *base) {
+    auto al = [](int64_t x) { return (x + 63) / 64 * 64; };  // floats (256-B alignment)
+    const int64_t reh = al(B * p->E * H), mv = al(B * p->Gv * H), mc = al(B * p->Gc * H), nz = al(B * N);
+    float *c = static_cast<float *>(base);
+    TrainWs w;
+    int64_t o = 0;
+    auto take = [&](int64_t n) { float *q = c + o; o += n; return q; };
+    w.Mv = take(mv);
+    w.Mc = take(mc);
+    w.Mda = take(mv);
+    w.Mdb = take(mc);
+    w.dz = take(nz);
+    w.dX = take(reh);
+    w.dXp = take(reh);
+    w.cbuf = take(reh);
+    w.hv = take(reh);
+    w.hc = take(reh);
+    w.dhv = take(reh);
+    w.dhc = take(reh);
+    w.dco = take(reh);
+    w.da = take(reh);
+    w.db = take(reh);
+    w.bytes = o * 4;
+    return w;
+}
+
+int g_cus_t = 0;
+
+}  // namespace
+}  // namespace ldpc
+
+using namespace ldpc;
+
+extern "C" int64_t ldpc_gnn_train_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers) {
+    if (!p || hidden <= 0 || hidden > kMaxH || N <= 0 || B < 0 || layers <= 0)
+        return fail(LDPC_EINVAL, "bad arguments (training needs hidden_dim <= 64)");
+    const int64_t fwd = ldpc_gnn_workspace_size(p, hidden, N, B, layers, 0);
+    const int64_t bwd = carve_train(p, hidden, N, B, nullptr).bytes;
+    return fwd > bwd ? fwd : bwd;
+}
+
+extern "C" int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                                      const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                                      const float *d_llr, int N, int64_t B, float *d_probs, float *d_saved,
+                                      void *d_work, int64_t work_bytes, void *stream) {
+    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    if (hidden <= 0 || hidden > kMaxH || types <= 0 || layers <= 0 || N <= 0 || B < 0)
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 64)");
+    if (B == 0) return LDPC_OK;
+    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_saved)
+        return fail(LDPC_EINVAL, "NULL tensor");
+    return gnn_fp32_forward(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs, d_saved,
+                            d_work, work_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                                 const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                                 int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
+                                 float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream) {
+    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    const int H = hidden, T = types, L = layers;
+    if (H <= 0 || H > kMaxH || T <= 0 || L <= 0 || N <= 0 || B < 0)
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 64)");
+    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_grad_probs || !d_saved || !d_grad_weights)
+        return fail(LDPC_EINVAL, "NULL tensor");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t wfloats = 2LL * H + (int64_t)L * tl_floats(H, T);
+    LDPC_HIP(hipMemsetAsync(d_grad_weights, 0, (size_t)wfloats * 4, s));
+    if (B == 0) return LDPC_OK;
+    TrainWs w = carve_train(p, H, N, B, d_work);
+    if (!d_work || work_bytes < w.bytes)
+        return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
+    if (!g_cus_t) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_cus_t, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int64_t E = p->E, R = B * E, n = R * H;
+    const size_t lds_mlp = mlp_bwd_lds(H);
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_mlp));
+    auto blocks = [](int64_t work, int per) { return dim3((unsigned)((work + per - 1) / per)); };
+    const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * 4);
+
+    // head: dz, dX_L, dwo, dbo
+    const float *WL[11];
+    t_layer(d_weights, H, T, L - 1, WL);
+    float *GL[11];
+    t_layer(d_grad_weights, H, T, L - 1, GL);
+    hipLaunchKernelGGL(train_head_kernel, blocks(B * N, 256), dim3(256), 0, s, d_probs, d_grad_probs, B * N, w.dz);
+    LDPC_CHECK_LAUNCH("train_head_kernel");
+    hipLaunchKernelGGL(train_dx_last_kernel, blocks(n, 256), dim3(256), 0, s, w.dz, d_msg_var, WL[9], H, E, N, n,
+                       w.dX);
+    LDPC_CHECK_LAUNCH("train_dx_last_kernel");
+    {
+        VecT v{};
+        v.src = d_saved + (int64_t)(L - 1) * n;
+        v.dz = w.dz;
+        v.msg_type = d_msg_type;
+        v.msg_var = d_msg_var;
+        v.g0 = GL[9];
+        v.g1 = GL[10];
+        v.H = H; v.T = T; v.N = N; v.mode = 2; v.E = E; v.R = R;
+        hipLaunchKernelGGL(train_vec_kernel, dim3(red_grid), dim3(256), (size_t)8 * H * 4, s, v);
+        LDPC_CHECK_LAUNCH("train_vec_kernel");
+    }
+    for (int l = L - 1; l >= 0; --l) {
+        const float *W[11];
+        t_layer(d_weights, H, T, l, W);
+        float *Gw[11];
+        t_layer(d_grad_weights, H, T, l, Gw);
+        const float *x = l > 0 ? d_saved + (int64_t)(l - 1) * n : nullptr;
+        // group means of c (forward recompute)
+        GmT g{};
+        g.src = x; g.emb = W[0]; g.llr = d_llr; g.w_in = d_weights; g.b_in = d_weights + H;
+        g.msg_type = d_msg_type; g.msg_var = d_msg_var;
+        g.src_mode = x ? 1 : 2; g.H = H; g.N = N; g.E = E; g.B = B;
+        g.ptr = p->vg_ptr; g.mem = p->vg_mem; g.inv = p->inv_v; g.G = p->Gv; g.dst = w.Mv;
+        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gv, 4), dim3(256), 0, s, g);
+        g.ptr = p->cg_ptr; g.mem = p->cg_mem; g.inv = p->inv_c; g.G = p->Gc; g.dst = w.Mc;
+        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gc, 4), dim3(256), 0, s, g);
+        LDPC_CHECK_LAUNCH("train_group_mean_kernel");
+        // MLP backward
+        MlpT m{};
+        m.x = x; m.llr = d_llr; m.w_in = d_weights; m.b_in = d_weights + H;
+        m.Mv = w.Mv; m.Mc = w.Mc; m.dX = w.dX;
+        m.msg_type = d_msg_type; m.msg_var = d_msg_var; m.vgroup = p->vgroup; m.cgroup = p->cgroup;
+        m.emb = W[0]; m.w1v = W[1]; m.b1v = W[2]; m.w2v = W[3]; m.w1c = W[5]; m.b1c = W[6]; m.w2c = W[7];
+        m.cbuf = w.cbuf; m.hv = w.hv; m.hc = w.hc; m.dhv = w.dhv; m.dhc = w.dhc;
+        m.dco = w.dco; m.da = w.da; m.db = w.db;
+        m.H = H; m.N = N; m.Gv = p->Gv; m.Gc = p->Gc; m.E = E; m.R = R;
+        const unsigned mgrid = (unsigned)std::min<int64_t>((R + 4 * kNM - 1) / (4 * kNM), (int64_t)g_cus_t * 2);
+        hipLaunchKernelGGL(train_mlp_bwd_kernel, dim3(mgrid), dim3(256), lds_mlp, s, m);
+        LDPC_CHECK_LAUNCH("train_mlp_bwd_kernel");
+        // group means of the aggregated-input gradients (the mean operator is symmetric)
+        GmT d{};
+        d.src_mode = 0; d.H = H; d.N = N; d.E = E; d.B = B;
+        d.src = w.da; d.ptr = p->vg_ptr; d.mem = p->vg_mem; d.inv = p->inv_v; d.G = p->Gv; d.dst = w.Mda;
+        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gv, 4), dim3(256), 0, s, d);
+        d.src = w.db; d.ptr = p->cg_ptr; d.mem = p->cg_mem; d.inv = p->inv_c; d.G = p->Gc; d.dst = w.Mdb;
+        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gc, 4), dim3(256), 0, s, d);
+        LDPC_CHECK_LAUNCH("train_group_mean_kernel");
+        hipLaunchKernelGGL(train_combine_kernel, blocks(n, 256), dim3(256), 0, s, w.dco, w.Mda, w.Mdb, w.dX,
+                           p->vgroup, p->cgroup, H, p->Gv, p->Gc, E, n, l > 0 ? 1 : 0, w.dXp);
+        LDPC_CHECK_LAUNCH("train_combine_kernel");
+        // weight gradients
+        OuterT o{};
+        o.H = H; o.E = E; o.R = R;
+        o.A = w.dX; o.zsrc = w.hv; o.J = H; o.out = Gw[3]; o.bias = Gw[4];
+        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
+        o.zsrc = w.hc; o.out = Gw[7]; o.bias = Gw[8];
+        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
+        o.A = w.dhv; o.zsrc = w.cbuf; o.J = 2 * H; o.G = w.Mv; o.grp = p->vgroup; o.Gn = p->Gv;
+        o.out = Gw[1]; o.bias = Gw[2];
+        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
+        o.A = w.dhc; o.G = w.Mc; o.grp = p->cgroup; o.Gn = p->Gc; o.out = Gw[5]; o.bias = Gw[6];
+        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
+        LDPC_CHECK_LAUNCH("train_outer_kernel");
+        VecT v{};
+        v.src = w.dco; v.llr = d_llr; v.msg_type = d_msg_type; v.msg_var = d_msg_var;
+        v.H = H; v.T = T; v.N = N; v.E = E; v.R = R;
+        v.mode = 0; v.g0 = Gw[0];
+        hipLaunchKernelGGL(train_vec_kernel, dim3(red_grid), dim3(256), (size_t)std::max(T * H, 8 * H) * 4, s, v);
+        if (l == 0) {
+            v.mode = 1; v.g0 = d_grad_weights; v.g1 = d_grad_weights + H;
+            hipLaunchKernelGGL(train_vec_kernel, dim3(red_grid), dim3(256), (size_t)8 * H * 4, s, v);
+        }
+        LDPC_CHECK_LAUNCH("train_vec_kernel");
+        std::swap(w.dX, w.dXp);
+    }
+    return LDPC_OK;
+}

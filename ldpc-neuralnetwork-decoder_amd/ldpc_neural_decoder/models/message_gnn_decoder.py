@@ -149,6 +149,16 @@ class MessageGNNDecoder(nn.Module):
         self._blob = None
 
     # -------------------------------------------------------------- native plumbing
+    def _blob_params(self):
+        """The parameters in weight-blob order (include/ldpc_amd.h); output_layer is unused."""
+        ps = [self.input_embedding.weight, self.input_embedding.bias]
+        for layer in self.gnn_layers:
+            v, c = layer.var_to_check_update, layer.check_to_var_update
+            ps += [layer.message_type_embeddings, v[0].weight, v[0].bias, v[2].weight, v[2].bias,
+                   c[0].weight, c[0].bias, c[2].weight, c[2].bias, layer.output_projection.weight,
+                   layer.output_projection.bias]
+        return ps
+
     def _weights_blob(self, device):
         params = [self.input_embedding.weight, self.input_embedding.bias]
         params += [p for layer in self.gnn_layers for p in layer.parameters()]
@@ -214,8 +224,14 @@ class MessageGNNDecoder(nn.Module):
         io_map = _io_mapping(message_to_var_mapping, E, llr.shape[1], dev)
         T = self.gnn_layers[0].message_type_embeddings.shape[0]
         types = _types_for(message_types, E, T, dev)
-        with torch.no_grad():
-            probs = self.native_forward(llr, io_map, types, vg, cg)
+        params = self._blob_params()
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            # training: fp32 forward that saves every layer's features + the HIP backward
+            plan = self._plan(vg[0], vg[1], cg[0], cg[1], dev)
+            probs = _NativeGnnTrain.apply(self, llr, io_map, types, plan, *params)
+        else:
+            with torch.no_grad():
+                probs = self.native_forward(llr, io_map, types, vg, cg)
         if home != dev:
             probs = probs.to(home)
         if ground_truth is not None:
@@ -229,6 +245,59 @@ class MessageGNNDecoder(nn.Module):
         soft_bits = self.forward(input_llr, message_to_var_mapping, message_types,
                                  var_to_check_adjacency, check_to_var_adjacency)
         return (soft_bits > 0.5).float()
+
+
+class _NativeGnnTrain(torch.autograd.Function):
+    """Autograd node of the native fp32 forward (message_gnn_decoder.py:190-307): forward saves
+    each layer's features, backward is ldpc_gnn_backward (csrc/gnn_train.hip).  Replaces torch's
+    autograd graph through the reference's forward for loss.backward() (trainer.py:93-99)."""
+
+    @staticmethod
+    def forward(ctx, dec, llr, io_map, types, plan, *params):
+        dev = llr.device
+        H, L = dec.hidden_dim, len(dec.gnn_layers)
+        T = dec.gnn_layers[0].message_type_embeddings.shape[0]
+        if H > 64:
+            raise NotImplementedError("the native backward supports hidden_dim <= 64")
+        B, Nv = llr.shape
+        E = dec.num_messages
+        blob = torch.cat([p.detach().reshape(-1).to(dev, torch.float32) for p in params]).contiguous()
+        probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
+        saved = torch.empty((L, B, E, H), dtype=torch.float32, device=dev)
+        if B:
+            wsb = N.check(N.lib().ldpc_gnn_train_workspace_size(plan.handle, H, Nv, B, L))
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            N.check(N.lib().ldpc_gnn_forward_train(
+                plan.handle, H, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr), Nv, B,
+                N.ptr(probs), N.ptr(saved), N.ptr(ws), wsb, N.stream_ptr(dev)))
+        ctx.save_for_backward(llr, io_map, types, blob, probs, saved)
+        ctx.meta = (plan, H, T, L, [p.shape for p in params])
+        return probs
+
+    @staticmethod
+    def backward(ctx, grad_probs):
+        llr, io_map, types, blob, probs, saved = ctx.saved_tensors
+        plan, H, T, L, shapes = ctx.meta
+        dev = llr.device
+        B, Nv = llr.shape
+        grad = torch.empty_like(blob)
+        wsb = N.check(N.lib().ldpc_gnn_train_workspace_size(plan.handle, H, Nv, B, L))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        g = grad_probs.to(dev, torch.float32).contiguous()
+        N.check(N.lib().ldpc_gnn_backward(
+            plan.handle, H, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr), Nv, B,
+            N.ptr(probs), N.ptr(g), N.ptr(saved), N.ptr(grad), N.ptr(ws), wsb, N.stream_ptr(dev)))
+        grads, off = [], 0
+        for s in shapes:
+            n = int(torch.Size(s).numel())
+            grads.append(grad[off:off + n].view(s))
+            off += n
+        # only the last layer's output_projection takes part in the forward (:270): the others
+        # get no gradient, exactly like the reference's autograd graph
+        for layer in range(L - 1):
+            grads[2 + layer * 11 + 9] = None
+            grads[2 + layer * 11 + 10] = None
+        return (None, None, None, None, None, *grads)
 
 
 class TannerToMessageGraph:

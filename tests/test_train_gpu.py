@@ -1,0 +1,117 @@
+"""Native GNN backward (csrc/gnn_train.hip) vs torch autograd through the CPU oracle (GPU).
+
+The reference trains with torch autograd (trainer.py:93-99: loss.backward() through
+MessageGNNDecoder.forward + BCE, message_gnn_decoder.py:314).  The oracle's gnn_forward is the
+same math in torch fp32 ops, so autograd on it gives the reference gradients.
+
+Tolerance (floating point, stated): per parameter tensor, max |g - g_ref| <= 1e-3 * max|g_ref|
++ 1e-6.  Both sides are fp32; they differ only in summation order (segment sums vs index_add,
+per-row fma chains vs MKL GEMMs), which leaves ~1e-6 relative error per layer."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import code_path
+
+from ldpc_neural_decoder.models import create_message_gnn_decoder
+from ldpc_neural_decoder.utils import expand_base_matrix, load_base_matrix
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-3
+
+
+def _setup(z, layers, hidden, B, seed=0, scale=0.5):
+    torch.manual_seed(seed)
+    base = load_base_matrix(code_path(z))
+    H = expand_base_matrix(base, z)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=layers, hidden_dim=hidden, base_graph=base, Z=z)
+    with torch.no_grad():
+        for p in dec.parameters():
+            p.mul_(scale)
+    types = conv.get_message_types(base, z)
+    llr = torch.randn(B, H.shape[1]) * 2 + 1.0
+    gt = (torch.rand(B, H.shape[1]) < 0.3).float()
+    return base, H, dec, conv, types, llr, gt
+
+
+def _oracle_grads(oracle_mod, dec, conv, H, types, llr, gt):
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in dec.state_dict().items()}
+    ev, ec = conv.edge_var, conv.edge_chk
+    probs, loss = oracle_mod.gnn_forward(sd, llr, ev, ev, ec, H.shape[1], H.shape[0], types, ground_truth=gt)
+    loss.backward()
+    return probs.detach(), loss.detach(), {k: v.grad for k, v in sd.items()}
+
+
+def _check(dec, ref_grads):
+    seen = 0
+    for name, p in dec.named_parameters():
+        g_ref = ref_grads[name]
+        if g_ref is None:
+            assert p.grad is None, f"{name}: reference has no gradient, native has one"
+            continue
+        assert p.grad is not None, f"{name}: missing gradient"
+        g = p.grad.detach().cpu()
+        err = float((g - g_ref).abs().max())
+        bound = RTOL * float(g_ref.abs().max()) + 1e-6
+        assert err <= bound, f"{name}: max err {err:.3e} > {bound:.3e}"
+        seen += 1
+    return seen
+
+
+@pytest.mark.parametrize("z,layers,hidden,B", [(4, 3, 64, 8), (4, 2, 32, 5), (32, 2, 64, 2)])
+def test_backward_matches_autograd(cuda, oracle_mod, z, layers, hidden, B):
+    base, H, dec, conv, types, llr, gt = _setup(z, layers, hidden, B)
+    ref_p, ref_loss, ref_g = _oracle_grads(oracle_mod, dec, conv, H, types, llr, gt)
+    dec = dec.to(cuda)
+    probs, loss = dec(llr.to(cuda), conv.message_to_var_index(), types, conv.var_to_check_adjacency,
+                      conv.check_to_var_adjacency, ground_truth=gt.to(cuda))
+    assert probs.requires_grad and loss.requires_grad
+    np.testing.assert_allclose(probs.detach().cpu().numpy(), ref_p.numpy(), atol=2e-5)
+    assert abs(loss.item() - ref_loss.item()) < 1e-5
+    loss.backward()
+    n = _check(dec, ref_g)
+    assert n == 2 + 9 * layers + 2  # every used parameter compared
+    # unused: output_projection of the non-last layers, output_layer
+    assert dec.gnn_layers[0].output_projection.weight.grad is None
+    assert dec.output_layer.weight.grad is None
+
+
+def test_sgd_steps_track_reference(cuda, oracle_mod):
+    """Three SGD steps with the trainer's optimizer settings (trainer.py:70: momentum 0.9,
+    weight decay 1e-4) on the native path and on the oracle give the same parameters."""
+    base, H, dec, conv, types, llr, gt = _setup(4, 2, 32, 6, seed=1)
+    ref = {k: v.detach().clone().requires_grad_(True) for k, v in dec.state_dict().items()}
+    used = [k for k in ref if not k.startswith("output_layer") and
+            not (k.startswith("gnn_layers.0.output_projection"))]
+    opt_ref = torch.optim.SGD([ref[k] for k in used], lr=0.05, momentum=0.9, weight_decay=1e-4)
+    dec = dec.to(cuda)
+    opt = torch.optim.SGD(dec.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    ev, ec = conv.edge_var, conv.edge_chk
+    for step in range(3):
+        opt_ref.zero_grad()
+        _, loss_r = oracle_mod.gnn_forward(ref, llr, ev, ev, ec, H.shape[1], H.shape[0], types, ground_truth=gt)
+        loss_r.backward()
+        opt_ref.step()
+        opt.zero_grad()
+        _, loss = dec(llr.to(cuda), conv.message_to_var_index(), types, conv.var_to_check_adjacency,
+                      conv.check_to_var_adjacency, ground_truth=gt.to(cuda))
+        loss.backward()
+        opt.step()
+        assert abs(loss.item() - loss_r.item()) < 1e-4 * max(1.0, abs(loss_r.item()))
+    sd = dec.state_dict()
+    for k in used:
+        np.testing.assert_allclose(sd[k].cpu().numpy(), ref[k].detach().numpy(), rtol=1e-3, atol=1e-5)
+
+
+def test_no_grad_path_unchanged(cuda):
+    """Inference (no grad) keeps the fast path: same probs, no graph."""
+    base, H, dec, conv, types, llr, gt = _setup(4, 2, 64, 4)
+    dec = dec.to(cuda)
+    args = (llr.to(cuda), conv.message_to_var_index(), types, conv.var_to_check_adjacency,
+            conv.check_to_var_adjacency)
+    with torch.no_grad():
+        p0 = dec(*args)
+    p1 = dec(*args)
+    assert not p0.requires_grad and p1.requires_grad
+    np.testing.assert_allclose(p0.cpu().numpy(), p1.detach().cpu().numpy(), atol=1e-6)
