@@ -16,6 +16,8 @@ Workloads (BASELINE.json configs):
   gnn-z32     cfg4 per GPU: BG2 Z=32, MessageGNN 10 layers, H=64, T=32, B=32768/GPU, fp32
   gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate)
   gnn-z32-bf16-i10  cfg4 shape (10 layers) on the bf16 path: the north-star "10 iterations" GNN line
+  gnn-train-z32 / gnn-train-z4  one training step (fp32 forward saving features, BCE, HIP backward,
+                SGD with the trainer's momentum 0.9 / weight decay 1e-4), frames/s
 """
 import argparse
 import json
@@ -44,6 +46,8 @@ WORKLOADS = {
     "gnn-z32-bf16": ("gnn-bf16", 32, 15, 32768, 2.0),
     "gnn-z4-bf16": ("gnn-bf16", 4, 5, 4096, 2.0),
     "gnn-z32-bf16-i10": ("gnn-bf16", 32, 10, 32768, 2.0),
+    "gnn-train-z32": ("gnn-train", 32, 10, 256, 2.0),
+    "gnn-train-z4": ("gnn-train", 4, 5, 4096, 2.0),
 }
 
 
@@ -128,9 +132,19 @@ def cpu_baseline(workload, z, iters, target_s):
         types = conv.get_message_types(torch.from_numpy(base), z)
         ev, ec = conv.edge_var, conv.edge_chk
 
+        train = kind == "gnn-train"
+        if train:
+            sd = {k: v.requires_grad_(True) for k, v in sd.items()}
+
         def run(b):
+            x = torch.from_numpy(sample(b))
+            if train:
+                _, loss = oracle.gnn_forward(sd, x, ev, ev, ec, g.N, g.M, types,
+                                             ground_truth=torch.zeros(b, g.N))
+                loss.backward()
+                return
             with torch.no_grad():
-                oracle.gnn_forward(sd, torch.from_numpy(sample(b)), ev, ev, ec, g.N, g.M, types)
+                oracle.gnn_forward(sd, x, ev, ev, ec, g.N, g.M, types)
         run(1)  # warm-up (thread pool, allocator)
         b = 2
         t0 = time.perf_counter()
@@ -142,6 +156,7 @@ def cpu_baseline(workload, z, iters, target_s):
         dt = time.perf_counter() - t0
         return {"value": b / dt, "unit": "codewords/s", "cores": torch.get_num_threads(), "kind": "port",
                 "sample": f"{b} frames, BG2 Z={z}, MessageGNN {iters} layers H=64 fp32, {snr} dB, "
+                          f"{'forward + BCE + autograd backward' if train else 'forward'}, "
                           f"oracle.gnn_forward (torch CPU, segment means) on {cpu} with "
                           f"{torch.get_num_threads()} threads, {dt:.1f} s"}
     algo = "minsum" if kind == "minsum" else "bp"
@@ -207,11 +222,25 @@ def main():
         vg, cg = conv.var_groups, conv.check_groups
         g_m, g_n = H.shape
 
-        def step(count):
-            p = gdec.native_forward(llr, io, types, vg, cg)
-            if count:
-                from ldpc_neural_decoder.utils import count_errors
-                count_errors((p > 0.5).to(torch.uint8), counters=counters)
+        if kind == "gnn-train":
+            opt = torch.optim.SGD(gdec.parameters(), lr=1e-3, momentum=0.9, weight_decay=1e-4)
+            gt = torch.zeros((B, n), dtype=torch.float32, device=dev)
+            Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
+
+            def step(count):  # trainer.py:90-102: zero_grad, forward + BCE, backward, SGD step
+                opt.zero_grad()
+                p, loss = gdec(llr, io, types, Av, Ac, ground_truth=gt)
+                loss.backward()
+                opt.step()
+                if count:
+                    from ldpc_neural_decoder.utils import count_errors
+                    count_errors((p.detach() > 0.5).to(torch.uint8), counters=counters)
+        else:
+            def step(count):
+                p = gdec.native_forward(llr, io, types, vg, cg)
+                if count:
+                    from ldpc_neural_decoder.utils import count_errors
+                    count_errors((p > 0.5).to(torch.uint8), counters=counters)
 
         dtype = "bf16" if kind == "gnn-bf16" else "f32"
         E = len(conv.messages)
@@ -220,10 +249,15 @@ def main():
             # (group-mean read, MLP read + write) + the fp32-sized group-mean rows written + read
             per_launch_alg = iters * (3 * E * 64 * 2 + 2 * (g_n + g_m) * 64 * 4) * B
             bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+        elif kind == "gnn-train":
+            # forward 12 H^2 E + backward 24 H^2 E (recomputed GEMM1, W2^T, W1^T, 4 weight-grad
+            # outer products) per frame-layer, fp32 (VALU fp32 peak = fp32 MFMA peak)
+            per_launch_alg = 36 * 64 * 64 * E * B * iters
+            bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         else:
             per_launch_alg = 12 * 64 * 64 * E * B * iters  # useful MLP FLOPs per forward
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
-        dominant = "gnn forward (all layers)"
+        dominant = "gnn training step" if kind == "gnn-train" else "gnn forward (all layers)"
 
     for _ in range(a.warmup):
         step(False)
@@ -266,7 +300,8 @@ def main():
         if world == 1 and a.cpu_baseline_seconds > 0:
             cpu = cpu_baseline(a.workload, z, iters, a.cpu_baseline_seconds)
         out = {
-            "metric": "codewords/s at fixed SNR (BG2, %d iters)" % iters,
+            "metric": ("training codewords/s (BG2, %d layers, fwd+bwd+SGD)" % iters if kind == "gnn-train"
+                       else "codewords/s at fixed SNR (BG2, %d iters)" % iters),
             "value": value,
             "unit": "codewords/s",
             "coded_bits_per_s": value * n,
