@@ -333,6 +333,83 @@ __global__ __launch_bounds__(256) void train_outer_kernel(OuterT P) {
     }
 }
 
+// Same reduction on fp32 MFMA: dW (i < H, j < J) = A^T Z with the rows as the K dimension.
+// v_mfma_f32_32x32x2_f32 takes K = 2 rows per instruction; its A fragment (lane l: row i = l & 31
+// of the 32 x 2 block, k = l >> 5) is A[r0 + k][32 it + i] and its B fragment is
+// Z[r0 + k][32 jt + (l & 31)] -- both straight from global memory, two 128-B row segments per
+// load, no LDS.  Every wave owns a contiguous range of rows and keeps the whole (up to) 64 x 128
+// tile in 8 accumulators; at the end it adds them into the gradient with float atomics (a 32 x 32
+// accumulator register is two 128-B row segments: the full-rate atomic shape).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int NIT, int NJT>
+__global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
+    const int lane = threadIdx.x & 63, col = lane & 31, k = lane >> 5;
+    const int H = P.H, J = P.J;
+    const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t per = ((P.R + nw - 1) / nw + 1) & ~1LL;  // even: whole k-steps
+    const int64_t r_begin = w * per, r_end = r_begin + per < P.R ? r_begin + per : P.R;
+    f32x16 acc[NIT][NJT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it)
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt) acc[it][jt] = f32x16{};
+    float bsum[NIT] = {};
+    auto zval = [&](int64_t r, int j) -> float {
+        if (j >= J) return 0.0f;
+        if (j < H) return P.zsrc[r * H + j];
+        const int64_t b = r / P.E, m = r - b * P.E;
+        return P.G[(b * P.Gn + P.grp[m]) * H + (j - H)];
+    };
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += 2) {
+        const int64_t r = r0 + k;
+        const bool ok = r < r_end;
+        float a[NIT], z[NJT];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int i = 32 * it + col;
+            a[it] = ok && i < H ? P.A[r * H + i] : 0.0f;
+        }
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt) z[jt] = ok ? zval(r, 32 * jt + col) : 0.0f;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            bsum[it] += a[it];
+#pragma unroll
+            for (int jt = 0; jt < NJT; ++jt)
+                acc[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[it], z[jt], acc[it][jt], 0, 0, 0);
+        }
+    }
+    if (r_begin >= r_end) return;
+    // D[i][j]: register q of lane l holds i = 8 (q >> 2) + 4 k + (q & 3), j = col
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt) {
+            const int j = 32 * jt + col;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int i = 32 * it + 8 * (q >> 2) + 4 * k + (q & 3);
+                if (i < H && j < J) atomicAdd(&P.out[i * J + j], acc[it][jt][q]);
+            }
+        }
+        float s = bsum[it] + __shfl_xor(bsum[it], 32, 64);
+        const int i = 32 * it + col;
+        if (P.bias && k == 0 && i < H) atomicAdd(&P.bias[i], s);
+    }
+}
+
+int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
+    const int nit = (o.H + 31) / 32, njt = (o.J + 31) / 32;
+    if (nit == 2 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4>), dim3(grid), dim3(256), 0, s, o);
+    else if (nit == 2 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2>), dim3(grid), dim3(256), 0, s, o);
+    else if (nit == 1 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<1, 2>), dim3(grid), dim3(256), 0, s, o);
+    else if (nit == 1 && njt == 1) hipLaunchKernelGGL((train_outer_mfma_kernel<1, 1>), dim3(grid), dim3(256), 0, s, o);
+    else hipLaunchKernelGGL(train_outer_kernel, dim3(grid), dim3(256), 0, s, o);
+    LDPC_CHECK_LAUNCH("train_outer_kernel");
+    return LDPC_OK;
+}
+
 // per-row vector gradients, lanes = units:
 //   mode 0 (emb):  demb[type(m)][u] += src[r][u]
 //   mode 1 (input embedding, layer 0): dw_in[u] += src[r][u] llr[b][var(m)], db_in[u] += src[r][u]
@@ -541,15 +618,14 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         OuterT o{};
         o.H = H; o.E = E; o.R = R;
         o.A = w.dX; o.zsrc = w.hv; o.J = H; o.out = Gw[3]; o.bias = Gw[4];
-        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
+        if (int rc = launch_outer(o, red_grid, s)) return rc;
         o.zsrc = w.hc; o.out = Gw[7]; o.bias = Gw[8];
-        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
+        if (int rc = launch_outer(o, red_grid, s)) return rc;
         o.A = w.dhv; o.zsrc = w.cbuf; o.J = 2 * H; o.G = w.Mv; o.grp = p->vgroup; o.Gn = p->Gv;
         o.out = Gw[1]; o.bias = Gw[2];
-        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
+        if (int rc = launch_outer(o, red_grid, s)) return rc;
         o.A = w.dhc; o.G = w.Mc; o.grp = p->cgroup; o.Gn = p->Gc; o.out = Gw[5]; o.bias = Gw[6];
-        hipLaunchKernelGGL(train_outer_kernel, dim3(red_grid), dim3(256), 0, s, o);
-        LDPC_CHECK_LAUNCH("train_outer_kernel");
+        if (int rc = launch_outer(o, red_grid, s)) return rc;
         VecT v{};
         v.src = w.dco; v.llr = d_llr; v.msg_type = d_msg_type; v.msg_var = d_msg_var;
         v.H = H; v.T = T; v.N = N; v.E = E; v.R = R;
