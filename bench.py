@@ -14,7 +14,8 @@ Workloads (BASELINE.json configs):
   bp-z4       cfg1 sizes on the GPU: BG2 Z=4, BP, 5 iterations, B=64 (x --batch)
   gnn-z4      cfg2: BG2 Z=4, MessageGNN 5 layers, H=64, T=4, B=4096, fp32
   gnn-z32     cfg4 per GPU: BG2 Z=32, MessageGNN 10 layers, H=64, T=32, B=32768/GPU, fp32
-  gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate)
+  gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate),
+              per-frame early-termination syndrome check after every layer (avg_layers reported)
   gnn-z32-bf16-i10  cfg4 shape (10 layers) on the bf16 path: the north-star "10 iterations" GNN line
   gnn-train-z32 / gnn-train-z4  one training step (fp32 forward saving features, BCE, HIP backward,
                 SGD with the trainer's momentum 0.9 / weight decay 1e-4), frames/s
@@ -216,6 +217,8 @@ def main():
         gdec = gdec.to(dev)
         if kind == "gnn-bf16":
             gdec.precision = "bf16"
+            # cfg5 = 15 iterations + per-frame early-termination syndrome check
+            gdec.early_termination = a.workload == "gnn-z32-bf16"
         types = conv.get_message_types(base, z).to(dev).to(torch.int32)
         io = conv.message_to_var_index().to(dev).to(torch.int32)
         probs = torch.empty((B, n), dtype=torch.float32, device=dev)
@@ -282,6 +285,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed, kern_ms = t.tolist()
+    avg_layers = None
+    if kind.startswith("gnn") and kind != "gnn-train" and getattr(gdec, "last_iterations", None) is not None:
+        avg_layers = float(gdec.last_iterations.double().mean())  # this rank's last step
     be, fe, fr, _ = tot.tolist()
 
     if rank == 0:
@@ -325,6 +331,7 @@ def main():
                          "kernel_ms": kern_ms,
                          "algorithmic_per_launch": per_launch_alg},
             "roofline_notes": roofline_notes(kind, B, n, kern_ms, traffic),
+            "avg_layers": avg_layers,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

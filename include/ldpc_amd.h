@@ -136,6 +136,8 @@ int ldpc_count_errors(const void *d_bits, int bits_dtype, const uint8_t *d_ref, 
  * d_probs (B, N) float32 = sigmoid(llr + sum of each variable's projected messages).
  * d_work: at least ldpc_gnn_workspace_size(plan, H, N, B, precision) bytes. */
 typedef struct ldpc_gnn_plan ldpc_gnn_plan;
+/* ldpc_gnn_forward_ex flags */
+#define LDPC_GNN_EARLY_STOP 1 /* cfg5 per-frame early termination (bf16 path; see below) */
 int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_vgroup, int n_cgroups,
                          const int32_t *h_cgroup, ldpc_gnn_plan **out);
 int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p);
@@ -146,6 +148,17 @@ int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                      const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
                      const float *d_llr, int N, int64_t B, int precision, float *d_probs,
                      void *d_work, int64_t work_bytes, void *stream);
+
+/* ldpc_gnn_forward_ex: ldpc_gnn_forward plus flags and a per-frame layer count d_iters (B,) int32
+ * (optional).  LDPC_GNN_EARLY_STOP (precision 1 only; a feature with no reference counterpart,
+ * BASELINE cfg5): after every layer but the last, each frame still decoding takes the hard
+ * decision [llr + sum of the LAST layer's output_projection over its messages > 0] on its current
+ * features; a frame whose decision satisfies every parity check stops there, gets its probs from
+ * that decision's soft values and d_iters = layers used; the others run on. */
+int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                        const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                        const float *d_llr, int N, int64_t B, int precision, int flags, float *d_probs,
+                        int32_t *d_iters, void *d_work, int64_t work_bytes, void *stream);
 
 /* ---- training (fp32, hidden_dim <= 64) -------------------------------------------------------
  * Replaces torch autograd through MessageGNNDecoder.forward + F.binary_cross_entropy

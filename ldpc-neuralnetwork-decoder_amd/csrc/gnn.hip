@@ -20,7 +20,7 @@
 //                           data movement; bias, ReLU, the v+c sum, the residual and (last
 //                           layer) the output projection + per-variable scatter are fused.
 //   gnn_mlp_generic_kernel  any H (VALU); used for H != 64 (e.g. the small-H test fixtures).
-//   gnn_output_kernel       probs = sigmoid(var_sum + llr).
+//   gnn_output_kernel       probs = sigmoid(sum of each variable's messages + llr), ascending order.
 // precision 1 (bf16 features, bf16 MFMA) lives in gnn_bf16.hip.
 #include <algorithm>
 #include <cmath>
@@ -66,7 +66,7 @@ struct GnnLayer {
     float *Mv, *Mc;  // (B, Gv, H), (B, Gc, H)
     // outputs
     float *x_out;    // (B, E, H); null on the last layer unless training saves its features
-    float *var_sum;  // (B, N), last layer only
+    float *msg_out;  // (B, E) projected message LLRs, last layer only
     int residual, last;
 };
 
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
         }
         if (P.last) {
             part += __shfl_xor(part, 32, 64);
-            if (ok && half == 0) atomicAdd(&P.var_sum[b * P.N + P.msg_var[m]], part + bo);
+            if (ok && half == 0) P.msg_out[b * P.E + m] = part + bo;
         }
     }
 }
@@ -343,24 +343,74 @@ __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H)
         }
         if (P.last) {
             for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
-            if (lane == 0) atomicAdd(&P.var_sum[b * P.N + P.msg_var[m]], part + P.bo[0]);
+            if (lane == 0) P.msg_out[b * P.E + m] = part + P.bo[0];
         }
     }
 }
 
-__global__ void gnn_output_kernel(const float *__restrict__ var_sum, const float *__restrict__ llr,
-                                  int64_t n, float *__restrict__ probs) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const float z = var_sum[i] + llr[i];  // (sum of messages) + input_llr (:298)
-        probs[i] = 1.0f / (1.0f + expf(-z));  // torch.sigmoid (:307)
+// per-call CSR of msg_var: ints = ptr[N + 1] | cursor[N + 1] | mem[E]
+__global__ void csr_count_kernel(const int32_t *__restrict__ msg_var, int64_t E, int32_t *__restrict__ cnt) {
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < E) atomicAdd(&cnt[msg_var[m] + 1], 1);
+}
+__global__ __launch_bounds__(1024) void csr_scan_kernel(int32_t *__restrict__ ptr, int32_t *__restrict__ cur, int N) {
+    __shared__ int32_t part[1024];
+    const int t = threadIdx.x, per = (N + 1 + 1023) / 1024, lo = t * per, hi = min(lo + per, N + 1);
+    int32_t s = 0;
+    for (int i = lo; i < hi; ++i) s += ptr[i];
+    part[t] = s;
+    __syncthreads();
+    if (t == 0)
+        for (int i = 1; i < 1024; ++i) part[i] += part[i - 1];
+    __syncthreads();
+    s = t ? part[t - 1] : 0;
+    for (int i = lo; i < hi; ++i) {
+        s += ptr[i];
+        ptr[i] = s;  // inclusive over the shifted counts = exclusive start of variable i
+        cur[i] = s;
     }
+}
+__global__ void csr_fill_kernel(const int32_t *__restrict__ msg_var, int64_t E, int32_t *__restrict__ cur,
+                                int32_t *__restrict__ mem) {
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < E) mem[atomicAdd(&cur[msg_var[m]], 1)] = (int32_t)m;
+}
+__global__ void csr_sort_kernel(const int32_t *__restrict__ ptr, int N, int32_t *__restrict__ mem) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;  // ascending message order per variable
+    if (v >= N) return;
+    for (int i = ptr[v] + 1; i < ptr[v + 1]; ++i) {
+        const int32_t x = mem[i];
+        int j = i - 1;
+        for (; j >= ptr[v] && mem[j] > x; --j) mem[j + 1] = mem[j];
+        mem[j + 1] = x;
+    }
+}
+__global__ void gnn_output_csr_kernel(const float *__restrict__ msg_out, const int32_t *__restrict__ ints,
+                                      const float *__restrict__ llr, int64_t E, int N, int64_t n,
+                                      const uint8_t *__restrict__ active, float *__restrict__ probs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t b = i / N;
+    const int v = (int)(i - b * N);
+    if (active && !active[b]) return;
+    const int32_t *ptr = ints, *mem = ints + 2 * N + 2;
+    const float *mo = msg_out + b * E;
+    float s = 0.0f;  // var_llrs[var] += decoded_llrs[b, msg] in ascending msg (:277-296)
+    for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[mem[q]];
+    probs[i] = 1.0f / (1.0f + expf(-(s + llr[i])));  // sigmoid(var_llrs + input_llr) (:298-307)
+}
+
+
+__global__ void gnn_fill_kernel(int32_t *p, int64_t n, int32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
 }
 
 int64_t layer_floats(int H, int T) { return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1; }
 
 struct Ws {
-    float *xa, *xb, *Mv, *Mc, *var_sum;
+    float *xa, *xb, *Mv, *Mc, *msg_out;
+    int32_t *csr;
     int64_t bytes;
 };
 
@@ -372,14 +422,15 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     const int64_t xb = layers > 1 ? al(B * p->E * H * es) : 0;
     const int64_t xb2 = layers > 2 ? xb : 0;
     const int64_t mv = al(B * (int64_t)p->Gv * H * es), mc = al(B * (int64_t)p->Gc * H * es);
-    const int64_t vs = al(B * (int64_t)N * 4);
+    const int64_t vs = al(B * p->E * 4), cs = al(gnn_csr_ints(p->E, N) * 4);
     char *c = static_cast<char *>(base);
     w.xa = reinterpret_cast<float *>(c);
     w.xb = reinterpret_cast<float *>(c + xb);
     w.Mv = reinterpret_cast<float *>(c + xb + xb2);
     w.Mc = reinterpret_cast<float *>(c + xb + xb2 + mv);
-    w.var_sum = reinterpret_cast<float *>(c + xb + xb2 + mv + mc);
-    w.bytes = xb + xb2 + mv + mc + vs;
+    w.msg_out = reinterpret_cast<float *>(c + xb + xb2 + mv + mc);
+    w.csr = reinterpret_cast<int32_t *>(c + xb + xb2 + mv + mc + vs);
+    w.bytes = xb + xb2 + mv + mc + vs + cs;
     return w;
 }
 
@@ -389,6 +440,27 @@ int g_num_cus = 0;
 }  // namespace ldpc
 
 using namespace ldpc;
+
+int ldpc::gnn_build_var_csr(const int32_t *d_msg_var, int64_t E, int N, int32_t *d_ints, hipStream_t s) {
+    int32_t *ptr = d_ints, *cur = d_ints + N + 1, *mem = d_ints + 2 * N + 2;
+    LDPC_HIP(hipMemsetAsync(ptr, 0, (size_t)(N + 1) * 4, s));
+    const unsigned ge = (unsigned)((E + 255) / 256);
+    hipLaunchKernelGGL(csr_count_kernel, dim3(ge), dim3(256), 0, s, d_msg_var, E, ptr);
+    hipLaunchKernelGGL(csr_scan_kernel, dim3(1), dim3(1024), 0, s, ptr, cur, N);
+    hipLaunchKernelGGL(csr_fill_kernel, dim3(ge), dim3(256), 0, s, d_msg_var, E, cur, mem);
+    hipLaunchKernelGGL(csr_sort_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, ptr, N, mem);
+    LDPC_CHECK_LAUNCH("gnn csr kernels");
+    return LDPC_OK;
+}
+
+int ldpc::gnn_output(const float *d_msg_out, const int32_t *d_ints, const float *d_llr, int64_t E, int N, int64_t B,
+                     const uint8_t *d_active, float *d_probs, hipStream_t s) {
+    const int64_t n = B * N;
+    hipLaunchKernelGGL(gnn_output_csr_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_msg_out, d_ints,
+                       d_llr, E, N, n, d_active, d_probs);
+    LDPC_CHECK_LAUNCH("gnn_output_csr_kernel");
+    return LDPC_OK;
+}
 
 extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_vgroup, int n_cgroups,
                                     const int32_t *h_cgroup, ldpc_gnn_plan **out) {
@@ -522,7 +594,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         LDPC_HIP(hipGetDevice(&dev));
         LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    LDPC_HIP(hipMemsetAsync(w.var_sum, 0, (size_t)B * N * 4, s));
+    if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
     GnnLayer L{};
     L.llr = d_llr;
     L.msg_var = d_msg_var;
@@ -563,7 +635,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.residual = l > 0;
         L.last = l == layers - 1;
         L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H : L.last ? nullptr : (l % 2 == 0) ? w.xa : w.xb;
-        L.var_sum = w.var_sum;
+        L.msg_out = w.msg_out;
         const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
         if (H == 64)
             hipLaunchKernelGGL(gnn_group_mean_h64_kernel, dim3((unsigned)((waves + 15) / 16)), dim3(256), 0, s, L);
@@ -588,26 +660,40 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         x_in = L.x_out;
     }
     const int64_t n = B * N;
-    hipLaunchKernelGGL(gnn_output_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.var_sum, d_llr, n,
-                       d_probs);
-    LDPC_CHECK_LAUNCH("gnn_output_kernel");
+    (void)n;
+    if (int rc = gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, nullptr, d_probs, s)) return rc;
     return LDPC_OK;
+}
+
+extern "C" int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                                   const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                                   int64_t B, int precision, int flags, float *d_probs, int32_t *d_iters,
+                                   void *d_work, int64_t work_bytes, void *stream) {
+    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    if (hidden <= 0 || types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
+    if (precision != 0 && precision != 1) return fail(LDPC_EINVAL, "precision must be 0 (fp32) or 1 (bf16)");
+    if (precision == 1 && hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "bf16 path needs hidden_dim 64");
+    if (flags & ~LDPC_GNN_EARLY_STOP) return fail(LDPC_EINVAL, "unknown flags");
+    if ((flags & LDPC_GNN_EARLY_STOP) && precision != 1)
+        return fail(LDPC_EUNSUPPORTED, "early termination is implemented on the bf16 path (precision 1)");
+    if (B == 0) return LDPC_OK;
+    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (precision == 1)
+        return gnn_bf16_forward(p, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, flags, d_probs,
+                                d_iters, d_work, work_bytes, s);
+    if (d_iters) {  // no early termination: every frame runs every layer
+        hipLaunchKernelGGL(gnn_fill_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, d_iters, B, layers);
+        LDPC_CHECK_LAUNCH("gnn_fill_kernel");
+    }
+    return gnn_fp32_forward(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
+                            nullptr, d_work, work_bytes, s);
 }
 
 extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
                                 const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
                                 int64_t B, int precision, float *d_probs, void *d_work, int64_t work_bytes,
                                 void *stream) {
-    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
-    if (hidden <= 0 || types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
-    if (precision != 0 && precision != 1) return fail(LDPC_EINVAL, "precision must be 0 (fp32) or 1 (bf16)");
-    if (precision == 1 && hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "bf16 path needs hidden_dim 64");
-    if (B == 0) return LDPC_OK;
-    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (precision == 1)
-        return gnn_bf16_forward(p, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs, d_work,
-                                work_bytes, s);
-    return gnn_fp32_forward(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
-                            nullptr, d_work, work_bytes, s);
+    return ldpc_gnn_forward_ex(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, precision, 0,
+                               d_probs, nullptr, d_work, work_bytes, stream);
 }

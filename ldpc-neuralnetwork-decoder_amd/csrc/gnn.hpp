@@ -23,6 +23,18 @@ struct ldpc_gnn_plan {
 
 namespace ldpc {
 
+// Deterministic output stage (message_gnn_decoder.py:277-307).  The last layer writes each
+// message's projected LLR into msg_out (B, E); every variable then sums its messages in ascending
+// message order, as the reference's loop does, from a per-call CSR of msg_var (gnn.hip).
+// Workspace: gnn_csr_ints(E, N) int32 words.
+inline int64_t gnn_csr_ints(int64_t E, int N) { return 2LL * N + 2 + E; }
+int gnn_build_var_csr(const int32_t *d_msg_var, int64_t E, int N, int32_t *d_ints, hipStream_t s);
+// probs[b][v] = sigmoid(sum_{m -> v} msg_out[b][m] + llr[b][v]) for frames with active[b] (null = all)
+int gnn_output(const float *d_msg_out, const int32_t *d_ints, const float *d_llr, int64_t E, int N, int64_t B,
+               const uint8_t *d_active, float *d_probs, hipStream_t s);
+__device__ __forceinline__ const int32_t *csr_ptr(const int32_t *ints) { return ints; }
+__device__ __forceinline__ const int32_t *csr_mem(const int32_t *ints, int N) { return ints + 2 * N + 2; }
+
 // fp32 forward (precision 0).  d_saved (L, B, E, H) or null: when set, layer l writes its output
 // features to d_saved[l] (the last layer included) for the backward pass (gnn_train.hip).
 int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
@@ -35,7 +47,8 @@ constexpr int kBf16MaxTypes = 200;
 int64_t gnn_bf16_workspace(const ldpc_gnn_plan *p, int N, int64_t B, int layers);
 int gnn_bf16_forward(const ldpc_gnn_plan *p, int types, int layers, const float *d_weights,
                      const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
-                     int64_t B, float *d_probs, void *d_work, int64_t work_bytes, hipStream_t s);
+                     int64_t B, int flags, float *d_probs, int32_t *d_iters, void *d_work, int64_t work_bytes,
+                     hipStream_t s);
 
 // XCD-aware block order (cdna_hip_programming.md T1, bijective form): blocks that share an
 // XCD (equal blockIdx % 8 under round-robin dispatch) get one contiguous range of work, so a

@@ -27,6 +27,10 @@
 //                        32-message tile: GEMM1 (K = 64 x-part + 64 group-part) -> ReLU -> GEMM2
 //                        for both sides into one accumulator, + b2v + b2c + residual, bf16 out.
 //                        Last layer: output projection + per-variable sum instead.
+//   gnn_bf16_syndrome_kernel  (early termination, cfg5) per frame, after every layer but the
+//                        last: hard decision through the last layer's output projection on the
+//                        current features, parity checks; a satisfied frame writes its probs
+//                        and every later kernel skips it.
 #include <cstdint>
 #include <string>
 
@@ -132,6 +136,7 @@ struct GmArgs {
     const float *memb;   // this layer (Gv + Gc, 64) fp32
     GtArgs G;
     __bf16 *Mv, *Mc;
+    const uint8_t *active;  // early termination: frames still decoding (null = all)
     int Gv, Gc, E, N;
     int64_t B;
 };
@@ -140,6 +145,7 @@ __global__ __launch_bounds__(256) void gnn_bf16_gm_kernel(GmArgs A) {
     const uint32_t w = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
     if (w >= (uint32_t)(A.B * A.G.n_tiles)) return;
     const uint32_t b = w / (uint32_t)A.G.n_tiles, t = w - b * (uint32_t)A.G.n_tiles;
+    if (A.active && !A.active[b]) return;
     const int lane = threadIdx.x & 63, q = lane >> 3, p0 = 8 * (lane & 7);
     const int2 md = A.G.meta[t];
     const int g = A.G.grp[8 * t + q];
@@ -192,7 +198,7 @@ constexpr int kW1B = 64 * 136 * 2, kW2B = 64 * 72 * 2;
 constexpr int kOffW1v = 0, kOffW1c = kW1B, kOffW2v = 2 * kW1B, kOffW2c = 2 * kW1B + kW2B;
 constexpr int kOffK = 2 * kW1B + 2 * kW2B;
 constexpr int kKStride = 132;
-inline size_t mlp_lds_bytes(int T) { return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 128) * 4; }
+inline size_t mlp_lds_bytes(int T) { return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 192) * 4; }
 
 struct MlpArgs {
     const __bf16 *x_in;  // null at layer 0
@@ -205,7 +211,9 @@ struct MlpArgs {
     const float *bo;                     // output_projection bias (device)
     int T, Gv, Gc, E, N, tpf;            // tpf = 32-message tiles per frame
     int64_t B;
-    float *var_sum;                      // last layer: (B, N) sums of projected messages
+    float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
+    const uint8_t *active;               // early termination: frames still decoding (null = all)
+    const float *kd_last, *bo_last;      // early termination: the last layer's output projection
 };
 
 __device__ __forceinline__ bf16x8 ld8(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
@@ -237,7 +245,7 @@ struct TileIn {
     float l;
     int ty, var;
     int64_t row, b;
-    bool ok;
+    bool ok, on;  // on: the frame is still decoding (early termination)
 };
 
 // MODE bit 0: layer 0 (x from the LLRs, no GEMM1 over x, no residual); bit 1: last layer
@@ -263,6 +271,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     for (int i = tid; i < nk; i += NT) Ks[(i >> 7) * kKStride + (i & 127)] = A.kd[i];
     float *tail = Ks + (A.T + 2) * kKStride;  // b2 [64], wo [64]
     if (tid < 128) tail[tid] = A.kd[nk + tid];
+    if (A.kd_last && tid < 64) tail[128 + tid] = A.kd_last[nk + 64 + tid];  // wo of the last layer
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
@@ -288,6 +297,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         I.var = inf.w;
         I.row = bb * A.E + m;
         I.b = bb;
+        I.on = !A.active || A.active[bb];
+        if (!I.on) return I;  // a terminated frame: nothing to load (uniform over the tile)
         const char *ma = reinterpret_cast<const char *>(A.Mv + (bb * A.Gv + inf.x) * H) + 16 * h;
         const char *mc = reinterpret_cast<const char *>(A.Mc + (bb * A.Gc + inf.y) * H) + 16 * h;
         if constexpr (!layer0) {
@@ -306,6 +317,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     };
 
     auto compute = [&](const TileIn &I) {
+        if (!I.on) return;
         const float *Kt = Ks + I.ty * kKStride;
         f32x16 y0 = ld16(tail + 16 * h), y1 = ld16(tail + 32 + 16 * h);  // b2v + b2c
         int wbase = j * 272 + 16 * h, w2base = j * 144 + 16 * h;
@@ -362,8 +374,20 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                 part = fmaf(y1[r], wo[32 + 16 * h + r], part);
             }
             part += __shfl_xor(part, 32, 64);
-            if (I.ok && h == 0) atomicAdd(&A.var_sum[I.b * A.N + I.var], part + A.bo[0]);
-        } else if (I.ok) {
+            if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo[0];
+        } else {
+            if (A.kd_last) {  // early termination: project with the last layer's output head
+                const float *wo = tail + 128;
+                float part = 0.0f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    part = fmaf(y0[r], wo[16 * h + r], part);
+                    part = fmaf(y1[r], wo[32 + 16 * h + r], part);
+                }
+                part += __shfl_xor(part, 32, 64);
+                if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo_last[0];
+            }
+            if (!I.ok) return;
             char *xo = reinterpret_cast<char *>(A.x_out + I.row * H) + 16 * h;
             *reinterpret_cast<bf16x8 *>(xo) = pack8(y0, 0);
             *reinterpret_cast<bf16x8 *>(xo + 32) = pack8(y0, 1);
@@ -401,15 +425,63 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     }
 }
 
-__global__ void bf16_output_kernel(const float *__restrict__ var_sum, const float *__restrict__ llr, int64_t n,
-                                   float *__restrict__ probs) {
+// Early termination (cfg5; no reference counterpart).  One workgroup per frame still decoding,
+// after layer `layer` < L - 1: bit_v = [llr_v + sum_{m -> v} (wo_L . x_m + bo_L) > 0] (the
+// decoder's P(bit = 1) > 0.5, message_gnn_decoder.py:298-307, with the last layer's head as the
+// output stage, :270); if every check group has even parity the frame is done: its probs are
+// written now, its layer count recorded, and every later kernel skips it.
+__global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__restrict__ msg_out,
+                                                                const int32_t *__restrict__ csr, int64_t E,
+                                                                const float *__restrict__ llr, int N,
+                                                                const int32_t *__restrict__ cg_ptr,
+                                                                const int32_t *__restrict__ cg_mem, int Gc,
+                                                                const int32_t *__restrict__ msg_var, int layer,
+                                                                uint8_t *__restrict__ active,
+                                                                int32_t *__restrict__ iters, float *__restrict__ probs) {
+    extern __shared__ uint32_t bits[];
+    __shared__ int odd;
+    const int64_t b = blockIdx.x;
+    if (!active[b]) return;
+    const float *mo = msg_out + b * E, *lr = llr + b * N;
+    const int32_t *vptr = csr_ptr(csr), *vmem = csr_mem(csr, N);
+    auto z = [&](int v) {  // the output stage's own sum order (gnn_output)
+        float s = 0.0f;
+        for (int q = vptr[v]; q < vptr[v + 1]; ++q) s += mo[vmem[q]];
+        return s + lr[v];
+    };
+    for (int i = threadIdx.x; i < (N + 31) / 32; i += blockDim.x) bits[i] = 0u;
+    if (threadIdx.x == 0) odd = 0;
+    __syncthreads();
+    for (int v = threadIdx.x; v < N; v += blockDim.x)
+        if (z(v) > 0.0f) atomicOr(&bits[v >> 5], 1u << (v & 31));
+    __syncthreads();
+    for (int g = threadIdx.x; g < Gc; g += blockDim.x) {
+        uint32_t p = 0;
+        for (int q = cg_ptr[g]; q < cg_ptr[g + 1]; ++q) {
+            const int v = msg_var[cg_mem[q]];
+            p ^= bits[v >> 5] >> (v & 31);
+        }
+        if (p & 1u) odd = 1;
+    }
+    __syncthreads();
+    if (odd) return;
+    if (threadIdx.x == 0) {
+        active[b] = 0;
+        if (iters) iters[b] = layer + 1;
+    }
+    for (int v = threadIdx.x; v < N; v += blockDim.x) probs[b * N + v] = 1.0f / (1.0f + expf(-z(v)));
+}
+
+__global__ void fill_i32_kernel(int32_t *p, int64_t n, int32_t v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) probs[i] = 1.0f / (1.0f + expf(-(var_sum[i] + llr[i])));  // :298-307
+    if (i < n) p[i] = v;
 }
 
 struct Bf16Ws {
-    float *kd, *memb, *var_sum;
+    float *kd, *memb, *msg_out;
+    int32_t *csr;
     int4 *info;
+    uint8_t *active;
     __bf16 *xa, *xb, *Mv, *Mc;
     int64_t bytes;
 };
@@ -418,19 +490,21 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4);
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
-    const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * N * 4);
-    const int64_t inf = al(p->E * 16);
+    const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * p->E * 4);
+    const int64_t inf = al(p->E * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
     char *c = static_cast<char *>(base);
     Bf16Ws w;
     w.info = reinterpret_cast<int4 *>(c + kd + memb + xa + xb + mv + mc + vs);
+    w.active = reinterpret_cast<uint8_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf);
+    w.csr = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act);
     w.kd = reinterpret_cast<float *>(c);
     w.memb = reinterpret_cast<float *>(c + kd);
     w.xa = reinterpret_cast<__bf16 *>(c + kd + memb);
     w.xb = reinterpret_cast<__bf16 *>(c + kd + memb + xa);
     w.Mv = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb);
     w.Mc = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb + mv);
-    w.var_sum = reinterpret_cast<float *>(c + kd + memb + xa + xb + mv + mc);
-    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf;
+    w.msg_out = reinterpret_cast<float *>(c + kd + memb + xa + xb + mv + mc);
+    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf + act + cs;
     return w;
 }
 
@@ -483,8 +557,9 @@ int64_t gnn_bf16_workspace(const ldpc_gnn_plan *p, int N, int64_t B, int layers)
 }
 
 int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weights, const int32_t *d_msg_type,
-                     const int32_t *d_msg_var, const float *d_llr, int N, int64_t B, float *d_probs, void *d_work,
-                     int64_t work_bytes, hipStream_t s) {
+                     const int32_t *d_msg_var, const float *d_llr, int N, int64_t B, int flags, float *d_probs,
+                     int32_t *d_iters, void *d_work, int64_t work_bytes, hipStream_t s) {
+    const bool et = (flags & LDPC_GNN_EARLY_STOP) && L > 1;
     if (!p->n_gtiles) return fail(LDPC_EUNSUPPORTED, "plan has no group tiles");
     Bf16Ws w = carve_bf16(p, N, B, T, L, d_work);
     if (!d_work || work_bytes < w.bytes)
@@ -510,7 +585,15 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     hipLaunchKernelGGL(gnn_bf16_memb_kernel, dim3((unsigned)(((int64_t)L * p->n_gtiles + 3) / 4)), dim3(256), 0, s,
                        d_weights, T, L, d_msg_type, G, Gtot, w.memb);
     LDPC_CHECK_LAUNCH("gnn_bf16_memb_kernel");
-    LDPC_HIP(hipMemsetAsync(w.var_sum, 0, (size_t)B * N * 4, s));
+    if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
+    if (d_iters) {
+        hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, d_iters, B, L);
+        LDPC_CHECK_LAUNCH("fill_i32_kernel");
+    }
+    if (et) LDPC_HIP(hipMemsetAsync(w.active, 1, (size_t)B, s));
+    const uint8_t *active = et ? w.active : nullptr;
+    const float *kd_last = w.kd + (int64_t)(L - 1) * kd_floats(T);
+    const float *bo_last = layer_w(d_weights, T, L - 1).bo;
 
     const __bf16 *x_in = nullptr;
     for (int l = 0; l < L; ++l) {
@@ -530,6 +613,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.E = (int)p->E;
         gm.N = N;
         gm.B = B;
+        gm.active = active;
         const int64_t gwaves = B * p->n_gtiles;
         hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, s, gm);
         LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
@@ -554,18 +638,23 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.N = N;
         m.tpf = (int)tpf;
         m.B = B;
-        m.var_sum = w.var_sum;
+        m.msg_out = w.msg_out;
+        m.active = active;
+        m.kd_last = et && l < L - 1 ? kd_last : nullptr;
+        m.bo_last = bo_last;
         const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0);
         const int rc = launch_mlp(mlp_variant(), mode, B * tpf, lds, s, m);
         if (rc != LDPC_OK) return rc;
         LDPC_CHECK_LAUNCH("gnn_bf16_mlp_kernel");
+        if (m.kd_last) {
+            hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)B), dim3(256), (size_t)(N + 31) / 32 * 4, s,
+                               w.msg_out, w.csr, p->E, d_llr, N, p->cg_ptr, p->cg_mem, p->Gc, d_msg_var, l, w.active, d_iters,
+                               d_probs);
+            LDPC_CHECK_LAUNCH("gnn_bf16_syndrome_kernel");
+        }
         x_in = m.x_out;
     }
-    const int64_t n = B * N;
-    hipLaunchKernelGGL(bf16_output_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w.var_sum, d_llr, n,
-                       d_probs);
-    LDPC_CHECK_LAUNCH("bf16_output_kernel");
-    return LDPC_OK;
+    return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s);
 }
 
 }  // namespace ldpc

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("LDPC_AMD_LIB", os.path.join(_HERE, "_lib", "libldpc_a
 LDPC_ALGO_MINSUM, LDPC_ALGO_BP = 0, 1
 LDPC_ES_OFF, LDPC_ES_BATCH, LDPC_ES_FRAME = 0, 1, 2
 LDPC_OUT_U8, LDPC_OUT_F32 = 0, 1
+LDPC_GNN_EARLY_STOP = 1
 
 _P = ctypes.c_void_p
 _I32, _I64, _U64, _F32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
@@ -42,6 +43,8 @@ SIGNATURES = {
     "ldpc_gnn_workspace_size": (_I64, [_P, ctypes.c_int, ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int]),
     "ldpc_gnn_forward": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                         ctypes.c_int, _I64, ctypes.c_int, _P, _P, _I64, _P]),
+    "ldpc_gnn_forward_ex": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
+                                           ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int, _P, _P, _P, _I64, _P]),
     "ldpc_gnn_train_workspace_size": (_I64, [_P, ctypes.c_int, ctypes.c_int, _I64, ctypes.c_int]),
     "ldpc_gnn_forward_train": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                               ctypes.c_int, _I64, _P, _P, _P, _I64, _P]),

@@ -144,6 +144,11 @@ class MessageGNNDecoder(nn.Module):
         self.output_layer = nn.Linear(hidden_dim, 1)  # unused by forward (:188), kept for state_dicts
         self.precision = "fp32"  # or "bf16": bf16 MLP operands, fp32 accumulate
         self.default_chunk = 0   # frames per native launch (0 = the whole batch, within budget)
+        # cfg5 per-frame early termination (bf16 path; no reference counterpart): a frame stops
+        # after the first layer whose hard decision (through the last layer's output projection)
+        # satisfies every parity check.  last_iterations holds the layers each frame used.
+        self.early_termination = False
+        self.last_iterations = None
         self._plans = {}
         self._blob_key = None
         self._blob = None
@@ -192,7 +197,12 @@ class MessageGNNDecoder(nn.Module):
         plan = self._plan(vgroups[0], vgroups[1], cgroups[0], cgroups[1], dev)
         blob = self._weights_blob(dev)
         prec = 1 if self.precision == "bf16" else 0
+        flags = N.LDPC_GNN_EARLY_STOP if self.early_termination else 0
+        if flags and prec != 1:
+            raise NotImplementedError("early termination is implemented on the bf16 path (precision='bf16')")
         probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
+        iters = torch.empty(B, dtype=torch.int32, device=dev)
+        self.last_iterations = iters
         if B == 0:
             return probs
         ws1 = N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, self.hidden_dim, Nv, 1, L, prec))
@@ -205,10 +215,10 @@ class MessageGNNDecoder(nn.Module):
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         for s in range(0, B, chunk):
             n = min(chunk, B - s)
-            N.check(N.lib().ldpc_gnn_forward(
+            N.check(N.lib().ldpc_gnn_forward_ex(
                 plan.handle, self.hidden_dim, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map),
-                N.ptr(llr[s:s + n]), Nv, n, prec, N.ptr(probs[s:s + n]), N.ptr(ws), wsb,
-                N.stream_ptr(dev)))
+                N.ptr(llr[s:s + n]), Nv, n, prec, flags, N.ptr(probs[s:s + n]), N.ptr(iters[s:s + n]),
+                N.ptr(ws), wsb, N.stream_ptr(dev)))
         return probs
 
     # -------------------------------------------------------------- reference API
@@ -225,8 +235,9 @@ class MessageGNNDecoder(nn.Module):
         T = self.gnn_layers[0].message_type_embeddings.shape[0]
         types = _types_for(message_types, E, T, dev)
         params = self._blob_params()
-        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        if self.precision == "fp32" and torch.is_grad_enabled() and any(p.requires_grad for p in params):
             # training: fp32 forward that saves every layer's features + the HIP backward
+            # (precision="bf16" is an inference setting: it always takes the no-grad path)
             plan = self._plan(vg[0], vg[1], cg[0], cg[1], dev)
             probs = _NativeGnnTrain.apply(self, llr, io_map, types, plan, *params)
         else:

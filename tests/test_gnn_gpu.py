@@ -37,9 +37,9 @@ def test_forward_matches_reference(cuda, z):
     mv = conv.message_to_var_index()
     Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
     p = dec(llr, mv, types, Av, Ac)
-    np.testing.assert_allclose(p.cpu().numpy(), f["probs"], atol=TOL)
+    np.testing.assert_allclose(p.detach().cpu().numpy(), f["probs"], atol=TOL)
     p = dec(llr, mv, None, Av, Ac)
-    np.testing.assert_allclose(p.cpu().numpy(), f["probs_no_types"], atol=TOL)
+    np.testing.assert_allclose(p.detach().cpu().numpy(), f["probs_no_types"], atol=TOL)
     p, loss = dec(llr, mv, types, Av, Ac, ground_truth=torch.from_numpy(f["ground_truth"]).to(cuda))
     assert abs(loss.item() - float(f["loss"])) < 1e-4
     bits = dec.decode(llr, mv, types, Av, Ac)
@@ -56,7 +56,7 @@ def test_2d_mapping_quirk(cuda):
     llr = torch.from_numpy(f["llr"]).to(cuda)
     p = dec(llr, conv.message_to_var_mapping.long(), conv.get_message_types(base, 4),
             conv.var_to_check_adjacency, conv.check_to_var_adjacency)
-    np.testing.assert_allclose(p.cpu().numpy(), f["probs_2d_quirk"], atol=TOL)
+    np.testing.assert_allclose(p.detach().cpu().numpy(), f["probs_2d_quirk"], atol=TOL)
     with pytest.raises(IndexError):  # the float one-hot fails in the reference too
         dec(llr, conv.message_to_var_mapping, None, conv.var_to_check_adjacency,
             conv.check_to_var_adjacency)
@@ -69,7 +69,7 @@ def test_untagged_adjacency_on_device(cuda):
     llr = torch.from_numpy(f["llr"]).to(cuda)
     p = dec(llr, conv.message_to_var_index(), conv.get_message_types(base, 4),
             conv.var_to_check_adjacency.to(cuda), conv.check_to_var_adjacency.to(cuda))
-    np.testing.assert_allclose(p.cpu().numpy(), f["probs"], atol=TOL)
+    np.testing.assert_allclose(p.detach().cpu().numpy(), f["probs"], atol=TOL)
 
 
 @pytest.mark.parametrize("B,chunk", [(3, None), (70, 16)])
@@ -91,7 +91,7 @@ def test_z32_h64_vs_oracle(cuda, oracle_mod, B, chunk):
     p = dec.native_forward(llr, io, types.to(cuda).to(torch.int32), vg, cg, chunk=chunk)
     sd = {k: v.cpu() for k, v in dec.state_dict().items()}
     ref = oracle_mod.gnn_forward(sd, llr.cpu(), ev, ev, ec, H.shape[1], H.shape[0], types)
-    np.testing.assert_allclose(p.cpu().numpy(), ref.numpy(), atol=TOL)
+    np.testing.assert_allclose(p.detach().cpu().numpy(), ref.numpy(), atol=TOL)
 
 
 def test_state_dict_keys_match_reference():
