@@ -1,0 +1,327 @@
+// layers.hip -- the index-gather neural-BP layers of models/layers.py.
+//
+// The reference's CheckLayer / VariableLayer (layers.py:5-125) expand the (B, n) input to
+// (n_out, B, n + 1), gather it through an (n_out, K) index tensor (-1 = padding -> a zero
+// column) and reduce over K.  Here one thread owns one output (b, i) and walks its K indices:
+// no expanded copies, every gathered value read once.  ResidualLayer (:128-168) and OutputLayer
+// (:171-208) are elementwise / per-frame kernels.  Each forward has a backward that reproduces
+// torch autograd through the reference's ops (gather -> scatter-add, min -> its argmin, the
+// in-place masked writes -> zero gradient).
+#include <cmath>
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace ldpc {
+namespace {
+
+__device__ __forceinline__ float torch_sign(float x) {  // torch.sign: NaN -> NaN, 0 -> 0
+    return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x * 0.0f);
+}
+
+// CheckLayer (layers.py:14-66): out[b][i] = prod_k sign(v_k + 1e-10) * min_k |v_k|' where
+// v_k = in[b][idx[i][k]] (0 for idx -1) and |v|' replaces 0 by 1e10; torch.min propagates NaN and
+// returns the first index of the minimum (kept for the backward).
+__global__ void gather_minsum_kernel(const float *__restrict__ in, int64_t B, int n_in,
+                                     const int64_t *__restrict__ idx, int n_out, int K, float *__restrict__ out,
+                                     int32_t *__restrict__ argmin) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * n_out) return;
+    const int64_t b = t / n_out;
+    const int i = (int)(t - b * n_out);
+    const float *x = in + b * n_in;
+    const int64_t *row = idx + (int64_t)i * K;
+    float sp = 1.0f, m = 0.0f;
+    int am = 0;
+    for (int k = 0; k < K; ++k) {
+        const int64_t j = row[k];
+        const float v = j < 0 ? 0.0f : x[j];
+        sp = sp * torch_sign(v + 1e-10f);
+        float a = fabsf(v);
+        if (a == 0.0f) a = 1e10f;
+        if (k == 0 || (!isnan(m) && (a < m || isnan(a)))) {
+            m = a;
+            am = k;
+        }
+    }
+    out[t] = sp * m;
+    if (argmin) argmin[t] = am;
+}
+
+// d in[b][idx[i][k*]] += g[b][i] * sign_product * sgn(v_k*)  (k* = argmin; sgn(0) = 0 covers the
+// padded and zero entries, whose |v| was overwritten in place)
+__global__ void gather_minsum_bwd_kernel(const float *__restrict__ g, const float *__restrict__ in, int64_t B,
+                                         int n_in, const int64_t *__restrict__ idx, int n_out, int K,
+                                         const int32_t *__restrict__ argmin, float *__restrict__ gin) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * n_out) return;
+    const int64_t b = t / n_out;
+    const int i = (int)(t - b * n_out);
+    const float *x = in + b * n_in;
+    const int64_t *row = idx + (int64_t)i * K;
+    float sp = 1.0f;
+    for (int k = 0; k < K; ++k) {
+        const int64_t j = row[k];
+        sp = sp * torch_sign((j < 0 ? 0.0f : x[j]) + 1e-10f);
+    }
+    const int64_t j = row[argmin[t]];
+    if (j < 0) return;
+    const float v = x[j];
+    const float s = v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f);
+    const float d = g[t] * sp * s;
+    if (d != 0.0f) atomicAdd(&gin[b * n_in + j], d);
+}
+
+// VariableLayer (layers.py:78-125): out[b][i] = llr[b][i] + sum_k msgs[b][idx[i][k]] (0 for -1)
+__global__ void gather_sum_kernel(const float *__restrict__ llr, const float *__restrict__ msgs, int64_t B, int n_in,
+                                  const int64_t *__restrict__ idx, int n_out, int K, float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * n_out) return;
+    const int64_t b = t / n_out;
+    const int i = (int)(t - b * n_out);
+    const float *x = msgs + b * n_in;
+    const int64_t *row = idx + (int64_t)i * K;
+    float s = 0.0f;
+    for (int k = 0; k < K; ++k) {
+        const int64_t j = row[k];
+        s += j < 0 ? 0.0f : x[j];
+    }
+    out[t] = llr[t] + s;
+}
+
+__global__ void gather_sum_bwd_kernel(const float *__restrict__ g, int64_t B, int n_in,
+                                      const int64_t *__restrict__ idx, int n_out, int K, float *__restrict__ gmsgs) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * n_out) return;
+    const int64_t b = t / n_out;
+    const int i = (int)(t - b * n_out);
+    const int64_t *row = idx + (int64_t)i * K;
+    const float d = g[t];
+    for (int k = 0; k < K; ++k)
+        if (row[k] >= 0) atomicAdd(&gmsgs[b * n_in + row[k]], d);
+}
+
+// ResidualLayer (layers.py:143-168): r = llr * w_ch + cm, then r = r + w_res[i] * prev_i, i < D
+struct ResArgs {
+    const float *llr, *w_ch, *cm, *w_res;
+    const float *prev[8];
+    int D, n;
+    int64_t total;
+};
+
+__global__ void residual_kernel(ResArgs A, float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= A.total) return;
+    float r = A.llr[t] * A.w_ch[t % A.n];
+    r = r + A.cm[t];
+    for (int i = 0; i < A.D; ++i) r = r + A.w_res[i] * A.prev[i][t];
+    out[t] = r;
+}
+
+// grads: g_cm = g; g_prev_i = w_res[i] g; g_w_ch[n] = sum_b g llr; g_w_res[i] = sum g prev_i
+struct ResBwd {
+    ResArgs A;
+    const float *g;
+    float *g_prev[8];
+    float *g_w_ch, *g_w_res, *g_llr;
+    int64_t B;
+};
+
+__global__ void residual_bwd_kernel(ResBwd P) {
+    const ResArgs &A = P.A;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float part[8] = {};
+    if (t < A.total) {
+        const float g = P.g[t];
+        const int n = (int)(t % A.n);
+        if (P.g_llr) P.g_llr[t] = g * A.w_ch[n];
+        if (P.g_w_ch) atomicAdd(&P.g_w_ch[n], g * A.llr[t]);
+        for (int i = 0; i < A.D; ++i) {
+            if (P.g_prev[i]) P.g_prev[i][t] = A.w_res[i] * g;
+            part[i] = g * A.prev[i][t];
+        }
+    }
+    // w_res: wave reduction, one atomic per wave and residual term
+    for (int i = 0; i < A.D; ++i) {
+        float s = part[i];
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if ((threadIdx.x & 63) == 0 && P.g_w_res) atomicAdd(&P.g_w_res[i], s);
+    }
+}
+
+// OutputLayer (layers.py:180-208): soft = sigmoid(final + llr); loss = max over n of
+// BCE(soft, gt) (torch clamps log at -100), argmax kept for the backward
+__global__ __launch_bounds__(256) void output_layer_kernel(const float *__restrict__ fin, const float *__restrict__ llr,
+                                                           const float *__restrict__ gt, int n,
+                                                           float *__restrict__ soft, float *__restrict__ maxloss,
+                                                           int32_t *__restrict__ argmax) {
+    __shared__ float sv[256];
+    __shared__ int si[256];
+    const int64_t b = blockIdx.x;
+    float best = -INFINITY;
+    int bi = 0;
+    bool have = false;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int64_t t = b * n + i;
+        const float p = 1.0f / (1.0f + expf(-(fin[t] + llr[t])));
+        soft[t] = p;
+        if (gt) {
+            const float y = gt[t];
+            // ATen binary_cross_entropy: (y - 1) max(log1p(-p), -100) - y max(log(p), -100)
+            const float l = (y - 1.0f) * fmaxf(log1pf(-p), -100.0f) - y * fmaxf(logf(p), -100.0f);
+            if (!have || l > best || (isnan(l) && !isnan(best))) {
+                best = l;
+                bi = i;
+                have = true;
+            }
+        }
+    }
+    if (!gt) return;
+    sv[threadIdx.x] = have ? best : -INFINITY;
+    si[threadIdx.x] = have ? bi : 0x7fffffff;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (threadIdx.x < off) {
+            const float a = sv[threadIdx.x], c = sv[threadIdx.x + off];
+            const int ia = si[threadIdx.x], ic = si[threadIdx.x + off];
+            // larger wins; NaN wins; ties -> smaller index (first occurrence)
+            const bool take = (isnan(c) && !isnan(a)) || (!isnan(a) && c > a) || (c == a && ic < ia) ||
+                              (isnan(c) && isnan(a) && ic < ia);
+            if (take) {
+                sv[threadIdx.x] = c;
+                si[threadIdx.x] = ic;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        maxloss[b] = sv[0];
+        argmax[b] = si[0];
+    }
+}
+
+// g_final = g_llr = (g_soft + [i == argmax] g_loss[b] (p - y) / max((1 - p) p, 1e-12)) (1 - p) p
+__global__ void output_layer_bwd_kernel(const float *__restrict__ soft, const float *__restrict__ gt,
+                                        const float *__restrict__ g_soft, const float *__restrict__ g_loss,
+                                        const int32_t *__restrict__ argmax, int64_t B, int n,
+                                        float *__restrict__ g_z) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * n) return;
+    const int64_t b = t / n;
+    const int i = (int)(t - b * n);
+    const float p = soft[t];
+    float gp = g_soft ? g_soft[t] : 0.0f;  // BCE backward: g (p - y) / max((1 - p) p, 1e-12)
+    if (g_loss && gt && argmax[b] == i) gp += g_loss[b] * (p - gt[t]) / fmaxf((1.0f - p) * p, 1e-12f);
+    g_z[t] = gp * (1.0f - p) * p;  // sigmoid backward: g (1 - y) y
+}
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace
+}  // namespace ldpc
+
+using namespace ldpc;
+
+extern "C" int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const int64_t *d_idx, int n_out, int K,
+                                  float *d_out, int32_t *d_argmin, void *stream) {
+    if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
+    if (!B || !n_out) return LDPC_OK;
+    if (!d_in || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
+    hipLaunchKernelGGL(gather_minsum_kernel, grid_for(B * n_out), dim3(256), 0, static_cast<hipStream_t>(stream), d_in,
+                       B, n_in, d_idx, n_out, K, d_out, d_argmin);
+    LDPC_CHECK_LAUNCH("gather_minsum_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_gather_minsum_backward(const float *d_grad_out, const float *d_in, int64_t B, int n_in,
+                                           const int64_t *d_idx, int n_out, int K, const int32_t *d_argmin,
+                                           float *d_grad_in, void *stream) {
+    if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (d_grad_in) LDPC_HIP(hipMemsetAsync(d_grad_in, 0, (size_t)B * n_in * 4, s));
+    if (!B || !n_out) return LDPC_OK;
+    if (!d_grad_out || !d_in || !d_idx || !d_argmin || !d_grad_in) return fail(LDPC_EINVAL, "NULL tensor");
+    hipLaunchKernelGGL(gather_minsum_bwd_kernel, grid_for(B * n_out), dim3(256), 0, s, d_grad_out, d_in, B, n_in, d_idx,
+                       n_out, K, d_argmin, d_grad_in);
+    LDPC_CHECK_LAUNCH("gather_minsum_bwd_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t B, int n_in, const int64_t *d_idx,
+                               int n_out, int K, float *d_out, void *stream) {
+    if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
+    if (!B || !n_out) return LDPC_OK;
+    if (!d_llr || !d_msgs || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
+    hipLaunchKernelGGL(gather_sum_kernel, grid_for(B * n_out), dim3(256), 0, static_cast<hipStream_t>(stream), d_llr,
+                       d_msgs, B, n_in, d_idx, n_out, K, d_out);
+    LDPC_CHECK_LAUNCH("gather_sum_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_gather_sum_backward(const float *d_grad_out, int64_t B, int n_in, const int64_t *d_idx, int n_out,
+                                        int K, float *d_grad_msgs, void *stream) {
+    if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (d_grad_msgs) LDPC_HIP(hipMemsetAsync(d_grad_msgs, 0, (size_t)B * n_in * 4, s));
+    if (!B || !n_out) return LDPC_OK;
+    if (!d_grad_out || !d_idx || !d_grad_msgs) return fail(LDPC_EINVAL, "NULL tensor");
+    hipLaunchKernelGGL(gather_sum_bwd_kernel, grid_for(B * n_out), dim3(256), 0, s, d_grad_out, B, n_in, d_idx, n_out,
+                       K, d_grad_msgs);
+    LDPC_CHECK_LAUNCH("gather_sum_bwd_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_residual(const float *d_llr, const float *d_w_ch, const float *d_cm, const float *d_w_res,
+                             const float *const *h_prev, int depth, int64_t B, int n, float *d_out, void *stream) {
+    if (B < 0 || n <= 0 || depth < 0 || depth > 8) return fail(LDPC_EINVAL, "bad residual arguments (depth <= 8)");
+    if (!B) return LDPC_OK;
+    ResArgs A{};
+    A.llr = d_llr; A.w_ch = d_w_ch; A.cm = d_cm; A.w_res = d_w_res; A.D = depth; A.n = n; A.total = B * n;
+    for (int i = 0; i < depth; ++i) A.prev[i] = h_prev[i];
+    hipLaunchKernelGGL(residual_kernel, grid_for(A.total), dim3(256), 0, static_cast<hipStream_t>(stream), A, d_out);
+    LDPC_CHECK_LAUNCH("residual_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_residual_backward(const float *d_grad, const float *d_llr, const float *d_w_ch,
+                                      const float *d_w_res, const float *const *h_prev, int depth, int64_t B, int n,
+                                      float *d_grad_llr, float *d_grad_w_ch, float *d_grad_w_res,
+                                      float *const *h_grad_prev, void *stream) {
+    if (B < 0 || n <= 0 || depth < 0 || depth > 8) return fail(LDPC_EINVAL, "bad residual arguments (depth <= 8)");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (d_grad_w_ch) LDPC_HIP(hipMemsetAsync(d_grad_w_ch, 0, (size_t)n * 4, s));
+    if (d_grad_w_res && depth) LDPC_HIP(hipMemsetAsync(d_grad_w_res, 0, (size_t)depth * 4, s));
+    if (!B) return LDPC_OK;
+    ResBwd P{};
+    P.A.llr = d_llr; P.A.w_ch = d_w_ch; P.A.w_res = d_w_res; P.A.D = depth; P.A.n = n; P.A.total = B * n;
+    for (int i = 0; i < depth; ++i) {
+        P.A.prev[i] = h_prev[i];
+        P.g_prev[i] = h_grad_prev ? h_grad_prev[i] : nullptr;
+    }
+    P.g = d_grad; P.g_w_ch = d_grad_w_ch; P.g_w_res = d_grad_w_res; P.g_llr = d_grad_llr; P.B = B;
+    hipLaunchKernelGGL(residual_bwd_kernel, grid_for(P.A.total), dim3(256), 0, s, P);
+    LDPC_CHECK_LAUNCH("residual_bwd_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_output_layer(const float *d_final, const float *d_llr, const float *d_gt, int64_t B, int n,
+                                 float *d_soft, float *d_max_loss, int32_t *d_argmax, void *stream) {
+    if (B < 0 || n <= 0) return fail(LDPC_EINVAL, "bad output-layer dimensions");
+    if (!B) return LDPC_OK;
+    if (d_gt && (!d_max_loss || !d_argmax)) return fail(LDPC_EINVAL, "loss outputs are NULL");
+    hipLaunchKernelGGL(output_layer_kernel, dim3((unsigned)B), dim3(256), 0, static_cast<hipStream_t>(stream), d_final,
+                       d_llr, d_gt, n, d_soft, d_max_loss, d_argmax);
+    LDPC_CHECK_LAUNCH("output_layer_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_output_layer_backward(const float *d_soft, const float *d_gt, const float *d_grad_soft,
+                                          const float *d_grad_loss, const int32_t *d_argmax, int64_t B, int n,
+                                          float *d_grad_z, void *stream) {
+    if (B < 0 || n <= 0) return fail(LDPC_EINVAL, "bad output-layer dimensions");
+    if (!B) return LDPC_OK;
+    hipLaunchKernelGGL(output_layer_bwd_kernel, grid_for(B * n), dim3(256), 0, static_cast<hipStream_t>(stream), d_soft,
+                       d_gt, d_grad_soft, d_grad_loss, d_argmax, B, n, d_grad_z);
+    LDPC_CHECK_LAUNCH("output_layer_bwd_kernel");
+    return LDPC_OK;
+}

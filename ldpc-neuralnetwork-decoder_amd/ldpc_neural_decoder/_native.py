@@ -45,6 +45,16 @@ SIGNATURES = {
                                         ctypes.c_int, _I64, ctypes.c_int, _P, _P, _I64, _P]),
     "ldpc_gnn_forward_ex": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                            ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int, _P, _P, _P, _I64, _P]),
+    "ldpc_gather_minsum": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P, _P]),
+    "ldpc_gather_minsum_backward": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P,
+                                                   _P, _P]),
+    "ldpc_gather_sum": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
+    "ldpc_gather_sum_backward": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
+    "ldpc_residual": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int, _I64, ctypes.c_int, _P, _P]),
+    "ldpc_residual_backward": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int, _I64, ctypes.c_int, _P, _P, _P, _P,
+                                              _P]),
+    "ldpc_output_layer": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int, _P, _P, _P, _P]),
+    "ldpc_output_layer_backward": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, ctypes.c_int, _P, _P]),
     "ldpc_gnn_train_workspace_size": (_I64, [_P, ctypes.c_int, ctypes.c_int, _I64, ctypes.c_int]),
     "ldpc_gnn_forward_train": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                               ctypes.c_int, _I64, _P, _P, _P, _I64, _P]),

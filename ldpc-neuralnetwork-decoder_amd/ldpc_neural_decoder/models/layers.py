@@ -1,0 +1,193 @@
+"""Index-gather neural-BP layers (drop-in for models/layers.py of the reference, :5-208).
+
+Same modules, signatures and parameters; the gathers and reductions run in csrc/layers.hip
+through the C ABI, with HIP backward kernels behind torch autograd Functions (the reference
+trains through these layers with autograd).  CPU inputs are moved to the HIP device and the
+outputs moved back; there is no CPU fallback.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from ldpc_neural_decoder import _native as N
+
+
+def _dev_f32(t, dev):
+    return t.to(dev, torch.float32).contiguous()
+
+
+def _check_index(idx, n_in, dev):
+    """The reference gathers from (B, n_in + 1) after mapping -1 to the zero column n_in: any
+    other index outside [0, n_in] is torch.gather's out-of-bounds RuntimeError."""
+    idx = torch.as_tensor(idx)
+    if idx.dim() != 2:
+        raise RuntimeError("index tensor must be 2-D (num_nodes, max_neighbors)")
+    if idx.dtype.is_floating_point:
+        raise RuntimeError("gather(): Expected dtype int64 for index")
+    idx = idx.to(dev, torch.int64).contiguous()
+    if idx.numel() and (int(idx.max()) > n_in or int(idx.min()) < -1):
+        raise RuntimeError(f"index out of bounds for a dimension of size {n_in + 1}")
+    return torch.where(idx == n_in, torch.full_like(idx, -1), idx)
+
+
+class _CheckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx):
+        B, n_in = x.shape
+        n_out, K = idx.shape
+        out = torch.empty((B, n_out), dtype=torch.float32, device=x.device)
+        am = torch.empty((B, n_out), dtype=torch.int32, device=x.device)
+        N.check(N.lib().ldpc_gather_minsum(N.ptr(x), B, n_in, N.ptr(idx), n_out, K, N.ptr(out), N.ptr(am),
+                                           N.stream_ptr(x.device)))
+        ctx.save_for_backward(x, idx, am)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, idx, am = ctx.saved_tensors
+        B, n_in = x.shape
+        n_out, K = idx.shape
+        gin = torch.empty_like(x)
+        N.check(N.lib().ldpc_gather_minsum_backward(N.ptr(g.contiguous()), N.ptr(x), B, n_in, N.ptr(idx), n_out, K,
+                                                    N.ptr(am), N.ptr(gin), N.stream_ptr(x.device)))
+        return gin, None
+
+
+class _VarFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, llr, msgs, idx):
+        B, n_in = msgs.shape
+        n_out, K = idx.shape
+        out = torch.empty((B, n_out), dtype=torch.float32, device=msgs.device)
+        N.check(N.lib().ldpc_gather_sum(N.ptr(llr), N.ptr(msgs), B, n_in, N.ptr(idx), n_out, K, N.ptr(out),
+                                        N.stream_ptr(msgs.device)))
+        ctx.save_for_backward(idx)
+        ctx.shape = (B, n_in)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        B, n_in = ctx.shape
+        n_out, K = idx.shape
+        g = g.contiguous()
+        gm = torch.empty((B, n_in), dtype=torch.float32, device=g.device)
+        N.check(N.lib().ldpc_gather_sum_backward(N.ptr(g), B, n_in, N.ptr(idx), n_out, K, N.ptr(gm),
+                                                 N.stream_ptr(g.device)))
+        return g, gm, None
+
+
+class _ResFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, llr, cm, w_ch, w_res, *prevs):
+        B, n = llr.shape
+        out = torch.empty_like(llr)
+        arr = (ctypes.c_void_p * max(1, len(prevs)))(*[p.data_ptr() for p in prevs])
+        N.check(N.lib().ldpc_residual(N.ptr(llr), N.ptr(w_ch), N.ptr(cm), N.ptr(w_res), arr, len(prevs), B, n,
+                                      N.ptr(out), N.stream_ptr(llr.device)))
+        ctx.save_for_backward(llr, w_ch, w_res, *prevs)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        llr, w_ch, w_res, *prevs = ctx.saved_tensors
+        B, n = llr.shape
+        g = g.contiguous()
+        g_llr = torch.empty_like(llr) if ctx.needs_input_grad[0] else None
+        g_wch = torch.empty_like(w_ch)
+        g_wres = torch.empty_like(w_res)
+        g_prev = [torch.empty_like(p) for p in prevs]
+        arr = (ctypes.c_void_p * max(1, len(prevs)))(*[p.data_ptr() for p in prevs])
+        garr = (ctypes.c_void_p * max(1, len(prevs)))(*[p.data_ptr() for p in g_prev])
+        N.check(N.lib().ldpc_residual_backward(N.ptr(g), N.ptr(llr), N.ptr(w_ch), N.ptr(w_res), arr, len(prevs), B,
+                                               n, N.ptr(g_llr), N.ptr(g_wch), N.ptr(g_wres), garr,
+                                               N.stream_ptr(g.device)))
+        return (g_llr, g, g_wch, g_wres, *g_prev)
+
+
+class _OutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, final, llr, gt):
+        B, n = final.shape
+        soft = torch.empty_like(final)
+        loss = torch.empty(B, dtype=torch.float32, device=final.device) if gt is not None else None
+        am = torch.empty(B, dtype=torch.int32, device=final.device) if gt is not None else None
+        N.check(N.lib().ldpc_output_layer(N.ptr(final), N.ptr(llr), N.ptr(gt), B, n, N.ptr(soft), N.ptr(loss),
+                                          N.ptr(am), N.stream_ptr(final.device)))
+        ctx.save_for_backward(soft, gt, am)
+        ctx.has_gt = gt is not None
+        if gt is None:
+            return soft
+        return soft, loss
+
+    @staticmethod
+    def backward(ctx, g_soft, g_loss=None):
+        soft, gt, am = ctx.saved_tensors
+        B, n = soft.shape
+        gz = torch.empty_like(soft)
+        gs = g_soft.contiguous() if g_soft is not None else None
+        gl = g_loss.contiguous() if g_loss is not None else None
+        N.check(N.lib().ldpc_output_layer_backward(N.ptr(soft), N.ptr(gt), N.ptr(gs), N.ptr(gl), N.ptr(am), B, n,
+                                                   N.ptr(gz), N.stream_ptr(soft.device)))
+        return gz, gz, None
+
+
+def _home_and_dev(t):
+    return t.device, N.device_of(t)
+
+
+class CheckLayer(nn.Module):
+    """layers.py:5-66: min-sum check update over an (num_nodes, max_neighbors) index tensor."""
+
+    def forward(self, input_tensor, check_index_tensor):
+        home, dev = _home_and_dev(input_tensor)
+        x = _dev_f32(input_tensor, dev)
+        idx = _check_index(check_index_tensor, x.shape[1], dev)
+        return _CheckFn.apply(x, idx).to(home)
+
+
+class VariableLayer(nn.Module):
+    """layers.py:69-125: input_llr + the sum of the gathered check messages."""
+
+    def forward(self, input_llr, check_messages, var_index_tensor):
+        home, dev = _home_and_dev(check_messages)
+        msgs = _dev_f32(check_messages, dev)
+        idx = _check_index(var_index_tensor, msgs.shape[1], dev)
+        llr = _dev_f32(input_llr, dev)
+        if llr.shape != (msgs.shape[0], idx.shape[0]):
+            raise RuntimeError(f"input_llr of shape {tuple(llr.shape)} does not match the summed messages "
+                               f"{(msgs.shape[0], idx.shape[0])}")
+        return _VarFn.apply(llr, msgs, idx).to(home)
+
+
+class ResidualLayer(nn.Module):
+    """layers.py:128-168: llr * w_ch + check messages + sum_i w_res[i] * prev_i (i < depth_L)."""
+
+    def __init__(self, num_nodes, depth_L=2):
+        super().__init__()
+        self.num_nodes = num_nodes
+        self.depth_L = depth_L
+        self.w_ch = nn.Parameter(torch.ones(num_nodes))
+        self.w_res = nn.Parameter(torch.ones(depth_L))
+
+    def forward(self, input_llr, check_messages, prev_var_messages):
+        home, dev = _home_and_dev(input_llr)
+        prevs = [_dev_f32(p, dev) for p in list(prev_var_messages)[:self.depth_L]]
+        if len(prevs) > 8:
+            raise NotImplementedError("depth_L > 8")
+        out = _ResFn.apply(_dev_f32(input_llr, dev), _dev_f32(check_messages, dev), self.w_ch.to(dev),
+                           self.w_res.to(dev), *prevs)
+        return out.to(home)
+
+
+class OutputLayer(nn.Module):
+    """layers.py:171-208: (sigmoid(final + input), per-frame max of the BCE or None)."""
+
+    def forward(self, final_llr, input_llr, ground_truth=None):
+        home, dev = _home_and_dev(final_llr)
+        fin, llr = _dev_f32(final_llr, dev), _dev_f32(input_llr, dev)
+        if ground_truth is None:
+            return _OutFn.apply(fin, llr, None).to(home), None
+        soft, loss = _OutFn.apply(fin, llr, _dev_f32(ground_truth, dev))
+        return soft.to(home), loss.to(home)

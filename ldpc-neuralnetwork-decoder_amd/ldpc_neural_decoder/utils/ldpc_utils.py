@@ -1,4 +1,5 @@
-"""H-matrix loader and lifting (drop-in for utils/ldpc_utils.py:97-147 of the reference).
+"""H-matrix loader, lifting and the var-major LLR mapping (drop-in for utils/ldpc_utils.py of the
+reference: :5-95 and :97-147).
 
 Setup-time helpers, not the hot path: the decoders turn H into a device-resident graph once
 (libldpc_amd's ldpc_graph_create detects the lifting back from H).
@@ -36,3 +37,38 @@ def edge_list(H):
     Ht = torch.as_tensor(H)
     nz = torch.nonzero(Ht == 1).cpu().numpy()
     return nz[:, 0].astype(np.int32), nz[:, 1].astype(np.int32)
+
+
+def get_LLR_indexes(H_to_LLR_mapping_T):
+    """utils/ldpc_utils.py:5-60: for every LLR index, the other LLR indices of its check (rows of
+    the (checks, vars) mapping) and of its variable (columns), in ascending order, -1 padded to
+    the longest list.  Vectorised: one stable sort per side instead of Python dict loops."""
+    m = np.asarray(torch.as_tensor(H_to_LLR_mapping_T).cpu(), dtype=np.int64)
+    E = int((m >= 0).sum())
+
+    def side(mat):
+        r, c = np.nonzero(mat >= 0)            # row-major: groups in order, members ascending by column
+        ids = mat[r, c]
+        groups = np.split(ids, np.cumsum(np.bincount(r, minlength=mat.shape[0]))[:-1])
+        K = max((len(gid) - 1 for gid in groups if len(gid)), default=0)
+        out = np.full((E, max(K, 0)), -1, dtype=np.int64)
+        for gid in groups:
+            for a in range(len(gid)):
+                nb = np.delete(gid, a)
+                out[gid[a], :len(nb)] = nb
+        return torch.from_numpy(out)
+
+    return side(m), side(m.T)
+
+
+def create_LLR_mapping(H_T):
+    """utils/ldpc_utils.py:62-95: LLR index i = the i-th nonzero of H_T (variables outer, checks
+    inner).  Returns (H_to_LLR_mapping_T (checks, vars) long, check_LLR_matrix, var_LLR_matrix,
+    output_index_tensor (1, E) = the variable of every LLR index)."""
+    HT = torch.as_tensor(H_T)
+    rows, cols = (HT == 1).nonzero(as_tuple=True)
+    mapping = torch.full(HT.shape, -1, dtype=torch.long, device=HT.device)
+    mapping[rows, cols] = torch.arange(rows.numel(), device=HT.device)
+    mapping_T = mapping.T
+    check_LLR, var_LLR = get_LLR_indexes(mapping_T)
+    return mapping_T, check_LLR, var_LLR, rows.unsqueeze(0)

@@ -168,6 +168,77 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
     return probs
 
 
+# --------------------------------------------------------------------------- index-gather layers
+# Restatement of models/layers.py:5-208 and utils/ldpc_utils.py:5-95 (var-major edge mapping),
+# in torch ops so that autograd gives the reference gradients (test infrastructure only).
+def llr_mapping(H):
+    """ldpc_utils.py:62-95 with H_T = H.T: LLR index i = i-th nonzero of H_T in row-major order
+    (variables outer, checks inner); neighbour lists in ascending LLR index, -1 padded."""
+    import torch
+    HT = np.asarray(H, dtype=np.float32).T
+    rows, cols = np.nonzero(HT == 1)
+    E = len(rows)
+    m = np.full(HT.shape, -1, dtype=np.int64)
+    m[rows, cols] = np.arange(E)
+    mT = m.T  # (checks, vars)
+    def neighbours(mat):
+        lists = [[] for _ in range(E)]
+        for r in range(mat.shape[0]):
+            ids = mat[r][mat[r] >= 0]
+            for a in ids:
+                lists[a] = [int(b) for b in ids if b != a]
+        K = max(len(x) for x in lists)
+        out = np.full((E, K), -1, dtype=np.int64)
+        for a, x in enumerate(lists):
+            out[a, :len(x)] = x
+        return out
+    return (torch.from_numpy(mT.copy()), torch.from_numpy(neighbours(mT)),
+            torch.from_numpy(neighbours(m)), torch.from_numpy(rows.astype(np.int64)[None, :]))
+
+
+def _gathered(x, idx):
+    import torch
+    valid = idx >= 0
+    v = x[:, idx.clamp(min=0)]                       # (B, n_out, K)
+    return torch.where(valid.unsqueeze(0), v, torch.zeros_like(v)), valid
+
+
+def check_layer(x, idx):
+    """layers.py:14-66: prod sign(v + 1e-10) * min |v| (|0| -> 1e10, padding -> 0)."""
+    import torch
+    v, _ = _gathered(x, idx)
+    sp = torch.prod(torch.sign(v + 1e-10), dim=2)
+    a = torch.abs(v)
+    a = torch.where(a == 0, torch.full_like(a, 1e10), a)
+    return sp * torch.min(a, dim=2).values
+
+
+def variable_layer(llr, msgs, idx):
+    """layers.py:78-125: llr + sum of the gathered messages (padding -> 0)."""
+    import torch
+    v, _ = _gathered(msgs, idx)
+    return llr + torch.sum(v, dim=2)
+
+
+def residual_layer(llr, cm, prevs, w_ch, w_res):
+    """layers.py:143-168."""
+    r = llr * w_ch.unsqueeze(0) + cm
+    for i, p in enumerate(prevs):
+        if i < w_res.shape[0]:
+            r = r + w_res[i] * p
+    return r
+
+
+def output_layer(final, llr, gt=None):
+    """layers.py:180-208: sigmoid(final + llr); with gt, the per-frame max of the elementwise BCE."""
+    import torch
+    import torch.nn.functional as F
+    soft = torch.sigmoid(final + llr)
+    if gt is None:
+        return soft, None
+    return soft, torch.max(F.binary_cross_entropy(soft, gt, reduction="none"), dim=1).values
+
+
 # --------------------------------------------------------------------------- Philox-4x32-10
 def philox4x32_10(ctr, key):
     """Random123 Philox-4x32-10 (Salmon et al., SC'11) on uint32 arrays.

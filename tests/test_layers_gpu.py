@@ -1,0 +1,123 @@
+"""HIP index-gather layers (csrc/layers.hip) vs the reference's golden vectors and the oracle (GPU).
+
+Tolerances (floating point, stated): CheckLayer forward bit-exact (signs and a min: no rounding);
+ResidualLayer forward bit-exact (same fp32 operation sequence); VariableLayer forward and every
+gradient within 1e-5 relative (summation order of the gathered terms / of the scatter-adds
+differs from torch's reductions); OutputLayer within 2e-6 absolute (expf/log1pf vs SLEEF)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import code_path, golden
+
+from ldpc_neural_decoder.models import CheckLayer, OutputLayer, ResidualLayer, VariableLayer
+from ldpc_neural_decoder.utils import create_LLR_mapping, expand_base_matrix, load_base_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return golden("layers_z4.npz")
+
+
+def t(a, dev, grad=False):
+    x = torch.from_numpy(np.asarray(a)).to(dev)
+    return x.requires_grad_(True) if grad else x
+
+
+def close(a, b, rtol=1e-5, atol=1e-6):
+    np.testing.assert_allclose(a.detach().cpu().numpy(), b, rtol=rtol, atol=atol)
+
+
+def test_check_layer(cuda, fx):
+    x = t(fx["x"], cuda, True)
+    out = CheckLayer()(x, torch.from_numpy(fx["check_LLR"]))
+    assert np.array_equal(out.detach().cpu().numpy(), fx["check_out"])
+    (out * t(fx["check_grad_out"], cuda)).sum().backward()
+    close(x.grad, fx["check_grad_in"])
+
+
+def test_variable_layer(cuda, fx):
+    llr, msgs = t(fx["llr"], cuda, True), t(fx["check_out"], cuda, True)
+    out = VariableLayer()(llr, msgs, torch.from_numpy(fx["var_LLR"]))
+    close(out, fx["var_out"], atol=1e-5)
+    (out * t(fx["var_grad_out"], cuda)).sum().backward()
+    close(msgs.grad, fx["var_grad_msgs"], atol=1e-5)
+    close(llr.grad, fx["var_grad_llr"], rtol=0, atol=0)
+
+
+def test_residual_layer(cuda, fx):
+    E = fx["x"].shape[1]
+    res = ResidualLayer(E, depth_L=2).to(cuda)
+    with torch.no_grad():
+        res.w_ch.copy_(t(fx["res_w_ch"], cuda))
+        res.w_res.copy_(t(fx["res_w_res"], cuda))
+    prevs = [t(p, cuda, True) for p in fx["res_prev"]]
+    cm, llr = t(fx["res_cm"], cuda, True), t(fx["llr"], cuda, True)
+    out = res(llr, cm, prevs)
+    assert np.array_equal(out.detach().cpu().numpy(), fx["res_out"])
+    (out * t(fx["res_grad_out"], cuda)).sum().backward()
+    close(res.w_ch.grad, fx["res_grad_w_ch"])
+    close(res.w_res.grad, fx["res_grad_w_res"], atol=1e-4)
+    close(cm.grad, fx["res_grad_cm"], rtol=0, atol=0)
+    close(llr.grad, fx["res_grad_llr"])
+    for i in range(2):
+        close(prevs[i].grad, fx["res_grad_prev"][i])
+    assert prevs[2].grad is None  # beyond depth_L: not part of the graph
+
+
+def test_output_layer(cuda, fx):
+    fin = t(fx["out_final"], cuda, True)
+    llr = t(fx["llr"], cuda)
+    soft, loss = OutputLayer()(fin, llr, t(fx["out_gt"], cuda))
+    close(soft, fx["out_soft"], rtol=0, atol=2e-6)
+    close(loss, fx["out_max_loss"], rtol=1e-5, atol=2e-6)
+    ((soft * t(fx["out_grad_soft"], cuda)).sum() + (loss * t(fx["out_grad_loss"], cuda)).sum()).backward()
+    close(fin.grad, fx["out_grad_final"], atol=2e-6)
+    s2, none = OutputLayer()(fin.detach(), llr)
+    assert none is None
+    close(s2, fx["out_soft_nogt"], rtol=0, atol=2e-6)
+
+
+def test_unrolled_decoder_z32_vs_oracle(cuda, oracle_mod):
+    """A small neural min-sum decoder built from the four layers at BG2 Z=32 (E = 6304), forward
+    and backward through 3 iterations, against the same chain on the oracle with autograd."""
+    torch.manual_seed(4)
+    H = expand_base_matrix(load_base_matrix(code_path(32)), 32)
+    _, chk, var, _ = create_LLR_mapping(H.T)
+    E, B, iters = chk.shape[0], 4, 3
+    llr0 = torch.randn(B, E) * 2 + 1
+    gt = (torch.rand(B, E) < 0.1).float()
+    w_ch = torch.rand(E) + 0.5
+    w_res = torch.tensor([0.5, 0.25])
+
+    def run(layers, dev, w_ch_t, w_res_t):
+        ck, vl, rs, ol = layers
+        llr = llr0.to(dev)
+        v, prev = llr, []
+        for _ in range(iters):
+            c = ck(v)
+            v = rs(llr, vl(llr, c), prev, w_ch_t, w_res_t)
+            prev = [v] + prev
+        return ol(v, llr, gt.to(dev))
+
+    res = ResidualLayer(E).to(cuda)
+    with torch.no_grad():
+        res.w_ch.copy_(w_ch)
+        res.w_res.copy_(w_res)
+    hip_layers = (lambda v: CheckLayer()(v, chk), lambda l, c: VariableLayer()(l, c, var),
+                  lambda l, cm, prev, a, b: res(l, cm, prev), lambda f, l, g: OutputLayer()(f, l, g))
+    soft, loss = run(hip_layers, cuda, None, None)
+    loss.sum().backward()
+
+    w_ch_o, w_res_o = w_ch.clone().requires_grad_(True), w_res.clone().requires_grad_(True)
+    ora = (lambda v: oracle_mod.check_layer(v, chk), lambda l, c: oracle_mod.variable_layer(l, c, var),
+           lambda l, cm, prev, a, b: oracle_mod.residual_layer(l, cm, prev, a, b),
+           lambda f, l, g: oracle_mod.output_layer(f, l, g))
+    soft_o, loss_o = run(ora, "cpu", w_ch_o, w_res_o)
+    loss_o.sum().backward()
+    close(soft, soft_o.detach().numpy(), rtol=1e-4, atol=1e-5)
+    close(loss, loss_o.detach().numpy(), rtol=1e-4, atol=1e-5)
+    close(res.w_ch.grad, w_ch_o.grad.numpy(), rtol=1e-3, atol=1e-5)
+    close(res.w_res.grad, w_res_o.grad.numpy(), rtol=1e-3, atol=1e-4)
