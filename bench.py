@@ -17,6 +17,8 @@ Workloads (BASELINE.json configs):
   gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate),
               per-frame early-termination syndrome check after every layer (avg_layers reported)
   gnn-z32-bf16-i10  cfg4 shape (10 layers) on the bf16 path: the north-star "10 iterations" GNN line
+  lay-z32     the index-gather layers (models/layers.py): 10 iterations of CheckLayer ->
+              VariableLayer -> ResidualLayer(depth 2) + OutputLayer on the var-major edge vector
   gnn-train-z32 / gnn-train-z4  one training step (fp32 forward saving features, BCE, HIP backward,
                 SGD with the trainer's momentum 0.9 / weight decay 1e-4), frames/s
 """
@@ -48,6 +50,7 @@ WORKLOADS = {
     "gnn-z4-bf16": ("gnn-bf16", 4, 5, 4096, 2.0),
     "gnn-z32-bf16-i10": ("gnn-bf16", 32, 10, 32768, 2.0),
     "gnn-train-z32": ("gnn-train", 32, 10, 256, 2.0),
+    "lay-z32": ("lay", 32, 10, 4096, 2.0),
     "gnn-train-z4": ("gnn-train", 4, 5, 4096, 2.0),
 }
 
@@ -160,6 +163,32 @@ def cpu_baseline(workload, z, iters, target_s):
                           f"{'forward + BCE + autograd backward' if train else 'forward'}, "
                           f"oracle.gnn_forward (torch CPU, segment means) on {cpu} with "
                           f"{torch.get_num_threads()} threads, {dt:.1f} s"}
+    if kind == "lay":
+        _, chk, var, oidx = oracle.llr_mapping(H)
+        E = chk.shape[0]
+        w_ch, w_res = torch.ones(E), torch.ones(2)
+
+        def run_lay(b):
+            llr = torch.from_numpy(sample(b))[:, oidx[0]].contiguous()
+            with torch.no_grad():
+                v, prev = llr, []
+                for _ in range(iters):
+                    v = oracle.residual_layer(llr, oracle.variable_layer(llr, oracle.check_layer(v, chk), var),
+                                              prev, w_ch, w_res)
+                    prev = [v] + prev
+                oracle.output_layer(v, llr)
+        run_lay(1)
+        b = 2
+        t0 = time.perf_counter()
+        run_lay(b)
+        dt = max(time.perf_counter() - t0, 1e-6)
+        b = int(min(4096, max(2, b * target_s / dt)))
+        t0 = time.perf_counter()
+        run_lay(b)
+        dt = time.perf_counter() - t0
+        return {"value": b / dt, "unit": "codewords/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"{b} frames, BG2 Z={z} (E={E} edge LLRs), {iters} iterations of the index-gather "
+                          f"layers, oracle (torch CPU) on {cpu} with {torch.get_num_threads()} threads, {dt:.1f} s"}
     algo = "minsum" if kind == "minsum" else "bp"
     b = 16
     t0 = time.perf_counter()
@@ -209,6 +238,31 @@ def main():
         per_launch_alg = flood_bytes_per_cw(g.E, g.N, iters) * B
         bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
         dominant = "flood_kernel<minsum>" if kind == "minsum" else "flood_kernel<bp>"
+    elif kind == "lay":
+        from ldpc_neural_decoder.models import CheckLayer, OutputLayer, ResidualLayer, VariableLayer
+        from ldpc_neural_decoder.utils import create_LLR_mapping
+        _, chk, var, out_idx = create_LLR_mapping(H.T)
+        E = chk.shape[0]
+        chk_d, var_d = chk.to(dev), var.to(dev)
+        # edge-vector LLRs: each edge carries its variable's channel LLR (out_idx = variable of edge)
+        ellr = llr[:, out_idx[0].to(dev)].contiguous()
+        ck, vl, ol = CheckLayer(), VariableLayer(), OutputLayer()
+        rs = ResidualLayer(E, depth_L=2).to(dev)
+
+        def step(count):
+            with torch.no_grad():
+                v, prev = ellr, []
+                for _ in range(iters):
+                    v = rs(ellr, vl(ellr, ck(v, chk_d), var_d), prev)
+                    prev = [v] + prev
+                ol(v, ellr)
+
+        dtype = "f32"
+        # per frame-iteration: read v + write c (check), read c + llr + write (variable),
+        # read llr, c-sum, 2 prev + write (residual) -- 11 passes over the E-vector, fp32
+        per_launch_alg = iters * 11 * 4 * E * B
+        bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+        dominant = "index-gather layers (all iterations)"
     else:
         from ldpc_neural_decoder.models import create_message_gnn_decoder
         torch.manual_seed(7)
@@ -324,8 +378,8 @@ def main():
             "config": {"workload": a.workload, "code": f"5G NR BG2 Z={z} (N={n})",
                        "decoder": kind, "iterations": iters, "batch_per_gpu": B,
                        "global_batch": B * world, "snr_db": snr, "parallelism": f"dp{world}"},
-            "ber": be / max(fr * n, 1),
-            "fer": fe / max(fr, 1),
+            "ber": None if kind == "lay" else be / max(fr * n, 1),
+            "fer": None if kind == "lay" else fe / max(fr, 1),
             "roofline": {"bound": bound, "kernel": dominant, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": achieved / peak, "traffic": traffic,
                          "kernel_ms": kern_ms,

@@ -181,7 +181,8 @@ int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                       float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream);
 
 /* ---- index-gather neural-BP layers (models/layers.py) ------------------
- * Index tensors are (n_out, K) int64 with -1 = padding (a zero value); inputs (B, n_in) fp32.
+ * d_idx is the reference's (n_out, K) index tensor transposed to (K, n_out) int32, -1 = padding
+ * (a zero value): d_idx[k * n_out + i]; inputs (B, n_in) fp32.
  * ldpc_gather_minsum   CheckLayer.forward (layers.py:14-66): out = prod sign(v + 1e-10) * min |v|
  *                      (|0| -> 1e10); d_argmin (B, n_out) int32 (optional) keeps torch.min's index.
  * ldpc_gather_sum      VariableLayer.forward (layers.py:78-125): out = llr + sum of gathered msgs.
@@ -190,14 +191,14 @@ int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
  * ldpc_output_layer    OutputLayer.forward (layers.py:180-208): soft = sigmoid(final + llr); with
  *                      d_gt, max over n of the elementwise BCE (+ its argmax for the backward).
  * The *_backward entry points write torch autograd's input gradients of the same functions. */
-int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const int64_t *d_idx, int n_out, int K,
+int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const int32_t *d_idx, int n_out, int K,
                        float *d_out, int32_t *d_argmin, void *stream);
 int ldpc_gather_minsum_backward(const float *d_grad_out, const float *d_in, int64_t B, int n_in,
-                                const int64_t *d_idx, int n_out, int K, const int32_t *d_argmin,
+                                const int32_t *d_idx, int n_out, int K, const int32_t *d_argmin,
                                 float *d_grad_in, void *stream);
-int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t B, int n_in, const int64_t *d_idx,
+int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t B, int n_in, const int32_t *d_idx,
                     int n_out, int K, float *d_out, void *stream);
-int ldpc_gather_sum_backward(const float *d_grad_out, int64_t B, int n_in, const int64_t *d_idx, int n_out,
+int ldpc_gather_sum_backward(const float *d_grad_out, int64_t B, int n_in, const int32_t *d_idx, int n_out,
                              int K, float *d_grad_msgs, void *stream);
 int ldpc_residual(const float *d_llr, const float *d_w_ch, const float *d_cm, const float *d_w_res,
                   const float *const *h_prev, int depth, int64_t B, int n, float *d_out, void *stream);

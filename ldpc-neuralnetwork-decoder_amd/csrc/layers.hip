@@ -3,7 +3,9 @@
 // The reference's CheckLayer / VariableLayer (layers.py:5-125) expand the (B, n) input to
 // (n_out, B, n + 1), gather it through an (n_out, K) index tensor (-1 = padding -> a zero
 // column) and reduce over K.  Here one thread owns one output (b, i) and walks its K indices:
-// no expanded copies, every gathered value read once.  ResidualLayer (:128-168) and OutputLayer
+// no expanded copies, every gathered value read once.  The index comes transposed, int32
+// (K, n_out) -- prepared once per index tensor by the Python layer -- so that consecutive
+// threads (consecutive i) read consecutive index words.  ResidualLayer (:128-168) and OutputLayer
 // (:171-208) are elementwise / per-frame kernels.  Each forward has a backward that reproduces
 // torch autograd through the reference's ops (gather -> scatter-add, min -> its argmin, the
 // in-place masked writes -> zero gradient).
@@ -15,6 +17,8 @@
 namespace ldpc {
 namespace {
 
+constexpr int kFB = 4;  // frames per thread in the forward gathers: one index read serves all four
+
 __device__ __forceinline__ float torch_sign(float x) {  // torch.sign: NaN -> NaN, 0 -> 0
     return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : x * 0.0f);
 }
@@ -23,48 +27,58 @@ __device__ __forceinline__ float torch_sign(float x) {  // torch.sign: NaN -> Na
 // v_k = in[b][idx[i][k]] (0 for idx -1) and |v|' replaces 0 by 1e10; torch.min propagates NaN and
 // returns the first index of the minimum (kept for the backward).
 __global__ void gather_minsum_kernel(const float *__restrict__ in, int64_t B, int n_in,
-                                     const int64_t *__restrict__ idx, int n_out, int K, float *__restrict__ out,
+                                     const int32_t *__restrict__ idx, int n_out, int K, float *__restrict__ out,
                                      int32_t *__restrict__ argmin) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B * n_out) return;
-    const int64_t b = t / n_out;
-    const int i = (int)(t - b * n_out);
-    const float *x = in + b * n_in;
-    const int64_t *row = idx + (int64_t)i * K;
-    float sp = 1.0f, m = 0.0f;
-    int am = 0;
+    const int64_t ng = (B + kFB - 1) / kFB;
+    if (t >= ng * n_out) return;
+    const int64_t b0 = (t / n_out) * kFB;
+    const int i = (int)(t % n_out);
+    const int nb = (int)min<int64_t>(kFB, B - b0);
+    float sp[kFB], m[kFB];
+    int am[kFB];
+#pragma unroll
+    for (int f = 0; f < kFB; ++f) { sp[f] = 1.0f; m[f] = 0.0f; am[f] = 0; }
     for (int k = 0; k < K; ++k) {
-        const int64_t j = row[k];
-        const float v = j < 0 ? 0.0f : x[j];
-        sp = sp * torch_sign(v + 1e-10f);
-        float a = fabsf(v);
-        if (a == 0.0f) a = 1e10f;
-        if (k == 0 || (!isnan(m) && (a < m || isnan(a)))) {
-            m = a;
-            am = k;
+        const int j = idx[(int64_t)k * n_out + i];  // one index read serves kFB frames
+#pragma unroll
+        for (int f = 0; f < kFB; ++f) {
+            if (f >= nb) break;
+            const float v = j < 0 ? 0.0f : in[(b0 + f) * n_in + j];
+            sp[f] = sp[f] * torch_sign(v + 1e-10f);
+            float a = fabsf(v);
+            if (a == 0.0f) a = 1e10f;
+            if (k == 0 || (!isnan(m[f]) && (a < m[f] || isnan(a)))) {
+                m[f] = a;
+                am[f] = k;
+            }
         }
     }
-    out[t] = sp * m;
-    if (argmin) argmin[t] = am;
+#pragma unroll
+    for (int f = 0; f < kFB; ++f) {
+        if (f >= nb) break;
+        const int64_t o = (b0 + f) * n_out + i;
+        out[o] = sp[f] * m[f];
+        if (argmin) argmin[o] = am[f];
+    }
 }
 
 // d in[b][idx[i][k*]] += g[b][i] * sign_product * sgn(v_k*)  (k* = argmin; sgn(0) = 0 covers the
 // padded and zero entries, whose |v| was overwritten in place)
 __global__ void gather_minsum_bwd_kernel(const float *__restrict__ g, const float *__restrict__ in, int64_t B,
-                                         int n_in, const int64_t *__restrict__ idx, int n_out, int K,
+                                         int n_in, const int32_t *__restrict__ idx, int n_out, int K,
                                          const int32_t *__restrict__ argmin, float *__restrict__ gin) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= B * n_out) return;
     const int64_t b = t / n_out;
     const int i = (int)(t - b * n_out);
     const float *x = in + b * n_in;
-    const int64_t *row = idx + (int64_t)i * K;
     float sp = 1.0f;
     for (int k = 0; k < K; ++k) {
-        const int64_t j = row[k];
+        const int j = idx[(int64_t)k * n_out + i];
         sp = sp * torch_sign((j < 0 ? 0.0f : x[j]) + 1e-10f);
     }
-    const int64_t j = row[argmin[t]];
+    const int j = idx[(int64_t)argmin[t] * n_out + i];
     if (j < 0) return;
     const float v = x[j];
     const float s = v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f);
@@ -74,31 +88,43 @@ __global__ void gather_minsum_bwd_kernel(const float *__restrict__ g, const floa
 
 // VariableLayer (layers.py:78-125): out[b][i] = llr[b][i] + sum_k msgs[b][idx[i][k]] (0 for -1)
 __global__ void gather_sum_kernel(const float *__restrict__ llr, const float *__restrict__ msgs, int64_t B, int n_in,
-                                  const int64_t *__restrict__ idx, int n_out, int K, float *__restrict__ out) {
+                                  const int32_t *__restrict__ idx, int n_out, int K, float *__restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B * n_out) return;
-    const int64_t b = t / n_out;
-    const int i = (int)(t - b * n_out);
-    const float *x = msgs + b * n_in;
-    const int64_t *row = idx + (int64_t)i * K;
-    float s = 0.0f;
+    const int64_t ng = (B + kFB - 1) / kFB;
+    if (t >= ng * n_out) return;
+    const int64_t b0 = (t / n_out) * kFB;
+    const int i = (int)(t % n_out);
+    const int nb = (int)min<int64_t>(kFB, B - b0);
+    float s[kFB];
+#pragma unroll
+    for (int f = 0; f < kFB; ++f) s[f] = 0.0f;
     for (int k = 0; k < K; ++k) {
-        const int64_t j = row[k];
-        s += j < 0 ? 0.0f : x[j];
+        const int j = idx[(int64_t)k * n_out + i];
+#pragma unroll
+        for (int f = 0; f < kFB; ++f) {
+            if (f >= nb) break;
+            s[f] += j < 0 ? 0.0f : msgs[(b0 + f) * n_in + j];
+        }
     }
-    out[t] = llr[t] + s;
+#pragma unroll
+    for (int f = 0; f < kFB; ++f) {
+        if (f >= nb) break;
+        const int64_t o = (b0 + f) * n_out + i;
+        out[o] = llr[o] + s[f];
+    }
 }
 
 __global__ void gather_sum_bwd_kernel(const float *__restrict__ g, int64_t B, int n_in,
-                                      const int64_t *__restrict__ idx, int n_out, int K, float *__restrict__ gmsgs) {
+                                      const int32_t *__restrict__ idx, int n_out, int K, float *__restrict__ gmsgs) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= B * n_out) return;
     const int64_t b = t / n_out;
     const int i = (int)(t - b * n_out);
-    const int64_t *row = idx + (int64_t)i * K;
     const float d = g[t];
-    for (int k = 0; k < K; ++k)
-        if (row[k] >= 0) atomicAdd(&gmsgs[b * n_in + row[k]], d);
+    for (int k = 0; k < K; ++k) {
+        const int j = idx[(int64_t)k * n_out + i];
+        if (j >= 0) atomicAdd(&gmsgs[b * n_in + j], d);
+    }
 }
 
 // ResidualLayer (layers.py:143-168): r = llr * w_ch + cm, then r = r + w_res[i] * prev_i, i < D
@@ -222,19 +248,20 @@ inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
 using namespace ldpc;
 
-extern "C" int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const int64_t *d_idx, int n_out, int K,
+extern "C" int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const int32_t *d_idx, int n_out, int K,
                                   float *d_out, int32_t *d_argmin, void *stream) {
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
     if (!d_in || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
-    hipLaunchKernelGGL(gather_minsum_kernel, grid_for(B * n_out), dim3(256), 0, static_cast<hipStream_t>(stream), d_in,
+    hipLaunchKernelGGL(gather_minsum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_in,
                        B, n_in, d_idx, n_out, K, d_out, d_argmin);
     LDPC_CHECK_LAUNCH("gather_minsum_kernel");
     return LDPC_OK;
 }
 
 extern "C" int ldpc_gather_minsum_backward(const float *d_grad_out, const float *d_in, int64_t B, int n_in,
-                                           const int64_t *d_idx, int n_out, int K, const int32_t *d_argmin,
+                                           const int32_t *d_idx, int n_out, int K, const int32_t *d_argmin,
                                            float *d_grad_in, void *stream) {
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -247,18 +274,19 @@ extern "C" int ldpc_gather_minsum_backward(const float *d_grad_out, const float 
     return LDPC_OK;
 }
 
-extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t B, int n_in, const int64_t *d_idx,
+extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t B, int n_in, const int32_t *d_idx,
                                int n_out, int K, float *d_out, void *stream) {
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
     if (!d_llr || !d_msgs || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
-    hipLaunchKernelGGL(gather_sum_kernel, grid_for(B * n_out), dim3(256), 0, static_cast<hipStream_t>(stream), d_llr,
+    hipLaunchKernelGGL(gather_sum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_llr,
                        d_msgs, B, n_in, d_idx, n_out, K, d_out);
     LDPC_CHECK_LAUNCH("gather_sum_kernel");
     return LDPC_OK;
 }
 
-extern "C" int ldpc_gather_sum_backward(const float *d_grad_out, int64_t B, int n_in, const int64_t *d_idx, int n_out,
+extern "C" int ldpc_gather_sum_backward(const float *d_grad_out, int64_t B, int n_in, const int32_t *d_idx, int n_out,
                                         int K, float *d_grad_msgs, void *stream) {
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     hipStream_t s = static_cast<hipStream_t>(stream);
