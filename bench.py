@@ -73,7 +73,7 @@ def roofline_notes(kind, B, n, kern_ms, traffic):
             "compulsory_GBps": comp / (kern_ms * 1e-3) / 1e9,
             "compulsory_frac_of_hbm_peak": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "traffic_over_compulsory": (traffic / comp) if traffic else None,
-            "actual_bound": "LDS/VALU issue (profiles/r01_pmc_minsum_z32.json)"}
+            "actual_bound": "LDS latency + VALU issue, two barriers per iteration (profiles/r01s2_pmc_minsum_z32.json)"}
 
 
 def parse():
@@ -349,7 +349,7 @@ def main():
         value = total_frames / elapsed
         achieved = per_launch_alg / (kern_ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
         traffic = None
-        tj = a.traffic_json or os.path.join(ROOT, "profiles", f"r01_pmc_{a.workload.replace('-', '_')}.json")
+        tj = a.traffic_json or os.path.join(ROOT, "profiles", f"r01s2_pmc_{a.workload.replace('-', '_')}.json")
         if os.path.exists(tj):
             tjd = json.load(open(tj))
             # the PMC pass ran the same workload at the default batch; scale per launch to this B

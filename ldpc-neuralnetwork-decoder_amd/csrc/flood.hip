@@ -72,6 +72,7 @@ __device__ __forceinline__ void put_bit(void *bits, int out_dtype, int64_t idx, 
 }
 
 __device__ __forceinline__ bool is_zero_sign(float x) { return !(x > 0.0f || x < 0.0f); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Min-sum statistics of one check row (traditional_decoders.py:207-232):
 //   c2v_e = prod_{e'!=e} sign(v) * (alpha * min_{e'!=e} |v|)
@@ -95,6 +96,31 @@ struct MinSumStats {
         const int zex = nz - (int)is_zero_sign(x);
         const float s = zex > 0 ? 0.0f : ((neg ^ (x < 0.0f)) ? -1.0f : 1.0f);
         return s * (alpha * m);
+    }
+};
+
+// Fast path of the same update for a row with no zero and no NaN message (every row, in practice;
+// a wave takes it when none of its 64 rows has one).  Then torch.sign is +-1, so
+//   * the sign parity is the XOR of the sign bits, and the output sign is parity ^ signbit(x);
+//   * the two smallest magnitudes are a min/max network (v_min/v_max are exact, NaN-free here);
+//   * the excluded minimum is m2 exactly when |x| == m1: a tie at m1 puts m1 in m2 as well, so
+//     no first-index bookkeeping is needed.
+// Every output is bit-identical to MinSumStats::c2v: +-(alpha * m) with the same alpha * m.
+struct MinSumFast {
+    float m1 = INFINITY, m2 = INFINITY;
+    uint32_t par = 0;
+    bool special = false;  // a zero or NaN message: the row needs MinSumStats
+    __device__ __forceinline__ void add(float x) {
+        const float a = fabsf(x);
+        special |= is_zero_sign(x);
+        par ^= __float_as_uint(x);
+        m2 = fminf(m2, fmaxf(m1, a));
+        m1 = fminf(m1, a);
+    }
+    __device__ __forceinline__ float c2v(float x, float am1, float am2) const {
+        const float am = fabsf(x) == m1 ? am2 : am1;
+        // sign bit of parity ^ x over the magnitude bits of alpha * m (v_xor + v_bfi)
+        return __uint_as_float(((par ^ __float_as_uint(x)) & 0x80000000u) | (__float_as_uint(am) & 0x7fffffffu));
     }
 };
 
@@ -160,11 +186,20 @@ __device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, const in
             ext_decision(C, L, lo, (w[e] >> kShiftBit) & 0xFF, v[e] + o, errs);
     };
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
-        MinSumStats st;
+        MinSumFast fs;
 #pragma unroll
-        for (int e = 0; e < DC; ++e) st.add(e, v[e]);
+        for (int e = 0; e < DC; ++e) fs.add(v[e]);
+        if (!__any(fs.special)) {  // wave-uniform
+            const float am1 = C.alpha * fs.m1, am2 = C.alpha * fs.m2;
 #pragma unroll
-        for (int e = 0; e < DC; ++e) emit(e, st.c2v(e, v[e], C.alpha));
+            for (int e = 0; e < DC; ++e) emit(e, fs.c2v(v[e], am1, am2));
+        } else {
+            MinSumStats st;
+#pragma unroll
+            for (int e = 0; e < DC; ++e) st.add(e, v[e]);
+#pragma unroll
+            for (int e = 0; e < DC; ++e) emit(e, st.c2v(e, v[e], C.alpha));
+        }
     } else {
         // sum-product (traditional_decoders.py:72-81): c2v_e = 2 atanh(prod_{e'!=e} tanh(v/2)),
         // product from 1.0 in ascending e'.  acc[e] = P_e * t_{e+1} * ... built column by column.
@@ -545,9 +580,16 @@ __device__ __forceinline__ void fx_check_row(const Ctx &C, const Lane &L, int &e
         }
     };
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
-        MinSumStats st;
-        sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
-        sfor<DC>([&](auto e) { emit(e, st.c2v(decltype(e)::value, v[decltype(e)::value], C.alpha)); });
+        MinSumFast fs;
+        sfor<DC>([&](auto e) { fs.add(v[decltype(e)::value]); });
+        if (!__any(fs.special)) {  // wave-uniform
+            const float am1 = C.alpha * fs.m1, am2 = C.alpha * fs.m2;
+            sfor<DC>([&](auto e) { emit(e, fs.c2v(v[decltype(e)::value], am1, am2)); });
+        } else {
+            MinSumStats st;
+            sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
+            sfor<DC>([&](auto e) { emit(e, st.c2v(decltype(e)::value, v[decltype(e)::value], C.alpha)); });
+        }
     } else {
         float acc[DC];
         float P = 1.0f;
@@ -568,20 +610,29 @@ __device__ __forceinline__ void fx_var_col(const Ctx &C, const Lane &L, bool wri
     constexpr int ZM4 = 4 * G::Z - 1;
     float P = L.llr_at(COL * 4 * G::Z + L.k4);
     if constexpr (DV > 0) {
-        float acc[DV];
+        // acc[e] = P_e + c_{e+1} + ... in pairs: one v_pk_add_f32 adds c to two running sums (two
+        // independent IEEE fp32 adds, the same sequence per element as the scalar form)
+        f32x2 acc[(DV + 1) / 2];
         sfor<DV>([&](auto jj) {
             constexpr int J = decltype(jj)::value;
             constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
             const float c = lds_rd(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4));
-            sfor<J>([&](auto e) { acc[decltype(e)::value] = acc[decltype(e)::value] + c; });
-            acc[J] = P;
+            const f32x2 cc = {c, c};
+            sfor<J / 2>([&](auto p) { acc[decltype(p)::value] = acc[decltype(p)::value] + cc; });
+            if constexpr (J % 2 == 1) {
+                acc[J / 2].x = acc[J / 2].x + c;
+                acc[J / 2].y = P;
+            } else {
+                acc[J / 2].x = P;
+            }
             P = P + c;
         });
         if (write) {
             sfor<DV>([&](auto jj) {
                 constexpr int J = decltype(jj)::value;
                 constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
-                lds_wr(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4), acc[J]);
+                lds_wr(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4),
+                       J % 2 == 0 ? acc[J / 2].x : acc[J / 2].y);
             });
         }
     }
