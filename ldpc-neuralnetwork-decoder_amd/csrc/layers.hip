@@ -110,7 +110,7 @@ __global__ void gather_sum_kernel(const float *__restrict__ llr, const float *__
     for (int f = 0; f < kFB; ++f) {
         if (f >= nb) break;
         const int64_t o = (b0 + f) * n_out + i;
-        out[o] = llr[o] + s[f];
+        out[o] = llr ? llr[o] + s[f] : s[f];
     }
 }
 
@@ -278,7 +278,7 @@ extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t 
                                int n_out, int K, float *d_out, void *stream) {
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
-    if (!d_llr || !d_msgs || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
+    if (!d_msgs || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
     hipLaunchKernelGGL(gather_sum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_llr,
                        d_msgs, B, n_in, d_idx, n_out, K, d_out);

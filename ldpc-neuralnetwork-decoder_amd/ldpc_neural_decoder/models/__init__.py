@@ -1,12 +1,13 @@
 """Decoders (drop-in for the reference's models/__init__.py:7-30, hot-path subset)."""
 from ldpc_neural_decoder.models.layers import CheckLayer, VariableLayer, ResidualLayer, OutputLayer
+from ldpc_neural_decoder.models.decoder import LDPCNeuralDecoder
 from ldpc_neural_decoder.models.traditional_decoders import (
     BeliefPropagationDecoder, MinSumScaledDecoder)
 from ldpc_neural_decoder.models.message_gnn_decoder import (
     MessageGNNLayer, MessageGNNDecoder, TannerToMessageGraph, create_message_gnn_decoder)
 
 __all__ = [
-    "CheckLayer", "VariableLayer", "ResidualLayer", "OutputLayer",
+    "CheckLayer", "VariableLayer", "ResidualLayer", "OutputLayer", "LDPCNeuralDecoder",
     "BeliefPropagationDecoder", "MinSumScaledDecoder",
     "MessageGNNLayer", "MessageGNNDecoder", "TannerToMessageGraph", "create_message_gnn_decoder",
 ]

@@ -90,6 +90,36 @@ class _VarFn(torch.autograd.Function):
         return g, gm, None
 
 
+class _SumFn(torch.autograd.Function):
+    """out[:, i] = sum_k msgs[:, idx[k, i]] (ldpc_gather_sum with no LLR term)."""
+
+    @staticmethod
+    def forward(ctx, msgs, idx):
+        B, n_in = msgs.shape
+        K, n_out = idx.shape
+        out = torch.empty((B, n_out), dtype=torch.float32, device=msgs.device)
+        N.check(N.lib().ldpc_gather_sum(None, N.ptr(msgs), B, n_in, N.ptr(idx), n_out, K, N.ptr(out),
+                                        N.stream_ptr(msgs.device)))
+        ctx.save_for_backward(idx)
+        ctx.shape = (B, n_in)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        B, n_in = ctx.shape
+        K, n_out = idx.shape
+        gm = torch.empty((B, n_in), dtype=torch.float32, device=g.device)
+        N.check(N.lib().ldpc_gather_sum_backward(N.ptr(g.contiguous()), B, n_in, N.ptr(idx), n_out, K, N.ptr(gm),
+                                                 N.stream_ptr(g.device)))
+        return gm, None
+
+
+def gather_sum(msgs, prepared_idx):
+    """Device-side segment sum over a prepared (K, n_out) int32 index (see _check_index)."""
+    return _SumFn.apply(msgs, prepared_idx)
+
+
 class _ResFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, llr, cm, w_ch, w_res, *prevs):

@@ -63,17 +63,25 @@ def _dist_all_reduce():
 
 
 class ComparativeEvaluator:
-    """comparative_evaluation.py:10-106 on the GPU (BP and min-sum: 50 iterations, batch-global
-    early stop, alpha 0.75, as :34-35).  ``neural_decoder`` may be a MessageGNNDecoder with its
-    TannerToMessageGraph passed as ``converter``."""
+    """comparative_evaluation.py:10-106,335-390 on the GPU (BP and min-sum: 50 iterations,
+    batch-global early stop, alpha 0.75, as :34-35).  ``neural_decoder`` is either a decoder of
+    the reference protocol (``decode(llrs, check_index_tensor, var_index_tensor)``, evaluated when
+    evaluate_all gets both index tensors, as :77) or a MessageGNNDecoder with its
+    TannerToMessageGraph passed as ``converter``.  ``device`` is where results and decoders live;
+    the compute always runs on the HIP device (a CPU ``device`` selects the current one)."""
 
-    def __init__(self, H, neural_decoder=None, device=None, converter=None, seed=0):
+    def __init__(self, H, neural_decoder=None, device=None, converter=None, seed=0, message_types=None):
         from ldpc_neural_decoder import _native as N
         from ldpc_neural_decoder.models import BeliefPropagationDecoder, MinSumScaledDecoder
         self.device = N.device_of(None) if device is None else torch.device(device)
+        self._dev = self.device if self.device.type == "cuda" else N.device_of(None)
         self.H = H
         self.neural_decoder = neural_decoder
+        if neural_decoder is not None:
+            neural_decoder.to(self._dev)
+            neural_decoder.eval()
         self.converter = converter
+        self.message_types = message_types
         self.seed = seed
         self.bp_decoder = BeliefPropagationDecoder(H, max_iterations=50, early_stopping=True)
         self.ms_decoder = MinSumScaledDecoder(H, max_iterations=50, scaling_factor=0.75, early_stopping=True)
@@ -81,7 +89,7 @@ class ComparativeEvaluator:
 
     def _llr_fn(self):
         from ldpc_neural_decoder.utils.channel import awgn_llr
-        dev, seed = self.device, self.seed
+        dev, seed = self._dev, self.seed
         return lambda b, n, snr, off: awgn_llr(b, n, snr, seed=seed, frame_offset=off, device=dev)
 
     def _flood(self, dec, snr_range, batch_size, num_trials):
@@ -92,19 +100,37 @@ class ComparativeEvaluator:
             dec.decode(llr, out_dtype=torch.uint8, counters=counters)
 
         counts = run_sweep(decode, self._llr_fn(), snr_range, batch_size, num_trials, n, rank, world,
-                           self.device, ar)
+                           self._dev, ar)
         return rates(counts, n)
 
     def _evaluate_traditional_decoder(self, decoder, snr_range, batch_size, num_trials, variable_bit_length=None):
         return self._flood(decoder, snr_range, batch_size, num_trials)
 
-    def _evaluate_neural_decoder(self, snr_range, batch_size, num_trials):
-        ber, fer = evaluate_message_gnn(self.neural_decoder, self.converter, snr_range, batch_size,
-                                        num_trials, self.device, seed=self.seed)
+    def _evaluate_neural_decoder(self, snr_range, batch_size, num_trials, variable_bit_length=None,
+                                 check_index_tensor=None, var_index_tensor=None):
+        """:168-223 -> (ber list, fer list)."""
+        if self.converter is not None:
+            return evaluate_message_gnn(self.neural_decoder, self.converter, snr_range, batch_size,
+                                        num_trials, self._dev, seed=self.seed, message_types=self.message_types)
+        from ldpc_neural_decoder.utils.channel import count_errors
+        ar, rank, world = _dist_all_reduce()
+        n = self.H.shape[1] if variable_bit_length is None else variable_bit_length
+        cidx, vidx = check_index_tensor.to(self._dev), var_index_tensor.to(self._dev)
+        dec = self.neural_decoder
+
+        def decode(llr, counters):
+            with torch.no_grad():
+                count_errors(dec.decode(llr, cidx, vidx).to(self._dev), counters=counters)
+
+        counts = run_sweep(decode, self._llr_fn(), snr_range, batch_size, num_trials, n, rank, world,
+                           self._dev, ar)
+        ber, fer, _ = rates(counts, n)
         return ber, fer
 
     def evaluate_all(self, snr_range, batch_size=32, num_trials=100, variable_bit_length=None,
                      check_index_tensor=None, var_index_tensor=None):
+        """:40-106.  The results dict holds plain Python lists (loadable with weights_only=True)."""
+        snr_range = list(snr_range)
         bp = self._flood(self.bp_decoder, snr_range, batch_size, num_trials)
         ms = self._flood(self.ms_decoder, snr_range, batch_size, num_trials)
         self.results = {
@@ -112,14 +138,77 @@ class ComparativeEvaluator:
             "belief_propagation": {"ber": bp[0], "fer": bp[1], "avg_iterations": bp[2]},
             "min_sum_scaled": {"ber": ms[0], "fer": ms[1], "avg_iterations": ms[2]},
         }
-        if self.neural_decoder is not None and self.converter is not None:
-            ber, fer = self._evaluate_neural_decoder(snr_range, batch_size, num_trials)
+        if self.neural_decoder is not None and (
+                self.converter is not None or (check_index_tensor is not None and var_index_tensor is not None)):
+            ber, fer = self._evaluate_neural_decoder(snr_range, batch_size, num_trials, variable_bit_length,
+                                                     check_index_tensor, var_index_tensor)
             self.results["neural_decoder"] = {"ber": ber, "fer": fer}
         return self.results
 
+    def _plot(self, field, ylabel, save_path, log=True):
+        """:225-333 (presentation only): one curve per decoder that has `field`."""
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+        fig, ax = plt.subplots(figsize=(10, 6))
+        snr = self.results["snr_range"]
+        for key, label, style in (("belief_propagation", "Belief Propagation", "o-"),
+                                  ("min_sum_scaled", "Min-Sum Scaled", "s-"), ("neural_decoder", "Neural Decoder", "^-")):
+            if field in self.results.get(key, {}):
+                (ax.semilogy if log else ax.plot)(snr, self.results[key][field], style, label=label)
+        ax.set_xlabel("SNR (dB)")
+        ax.set_ylabel(ylabel)
+        ax.grid(True)
+        ax.legend()
+        if save_path:
+            fig.savefig(save_path)
+        return fig
 
-def evaluate_message_gnn(decoder, converter, snr_range, batch_size, num_trials, device=None, seed=0):
-    """run_comparison_all.py:245-295 on the GPU -> (ber list, fer list)."""
+    def plot_ber_comparison(self, save_path=None):
+        return self._plot("ber", "Bit Error Rate (BER)", save_path)
+
+    def plot_fer_comparison(self, save_path=None):
+        return self._plot("fer", "Frame Error Rate (FER)", save_path)
+
+    def plot_iterations_comparison(self, save_path=None):
+        return self._plot("avg_iterations", "Average Iterations", save_path, log=False)
+
+    def save_results(self, path):
+        """:335-345."""
+        if not self.results:
+            raise ValueError("No results to save. Run evaluate_all() first.")
+        torch.save(self.results, path)
+
+    def load_results(self, path):
+        """:347-354 (weights_only: the file holds lists and floats)."""
+        self.results = torch.load(path, weights_only=True)
+
+    def print_summary(self):
+        """:356-390."""
+        if not self.results:
+            raise ValueError("No results to summarize. Run evaluate_all() first.")
+        print("Evaluation Summary")
+        print("=================")
+        print(f"SNR Range: {self.results['snr_range']}")
+        print()
+        for key, title in (("belief_propagation", "Belief Propagation Decoder"),
+                           ("min_sum_scaled", "Min-Sum Scaled Decoder"), ("neural_decoder", "Neural Decoder")):
+            if key not in self.results:
+                continue
+            r = self.results[key]
+            print(title)
+            print("-" * len(title))
+            print(f"BER: {r['ber']}")
+            print(f"FER: {r['fer']}")
+            if "avg_iterations" in r:
+                print(f"Average Iterations: {r['avg_iterations']}")
+            print()
+
+
+def evaluate_message_gnn(decoder, converter, snr_range, batch_size, num_trials, device=None, seed=0,
+                         message_types=None):
+    """run_comparison_all.py:245-295 on the GPU -> (ber list, fer list).  message_types=None uses
+    converter.get_message_types() (all zero) as :273 does."""
     from ldpc_neural_decoder import _native as N
     from ldpc_neural_decoder.utils.channel import awgn_llr, count_errors
     dev = N.device_of(None) if device is None else torch.device(device)
@@ -129,7 +218,8 @@ def evaluate_message_gnn(decoder, converter, snr_range, batch_size, num_trials, 
     io = converter.message_to_var_index().to(dev).to(torch.int32)
     T = decoder.gnn_layers[0].message_type_embeddings.shape[0]
     from ldpc_neural_decoder.models.message_gnn_decoder import _types_for
-    types = _types_for(converter.get_message_types(), len(converter.messages), T, dev)
+    types = _types_for(converter.get_message_types() if message_types is None else message_types,
+                       len(converter.messages), T, dev)
     vg, cg = converter.var_groups, converter.check_groups
 
     def decode(llr, counters):

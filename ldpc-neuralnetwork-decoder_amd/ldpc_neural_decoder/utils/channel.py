@@ -96,6 +96,8 @@ def awgn_llr(batch, n, snr_db, seed=0, frame_offset=0, bits=None, bpsk=False, de
     Returns float32 (batch, n).
     """
     dev = N.device_of(bits if bits is not None else out) if device is None else torch.device(device)
+    if dev.type != "cuda":
+        raise N.NativeError(f"awgn_llr runs on a HIP device, not {dev} (no CPU path)")
     if out is None:
         out = torch.empty((batch, n), dtype=torch.float32, device=dev)
     assert out.shape == (batch, n) and out.dtype == torch.float32 and out.is_contiguous()
@@ -112,6 +114,7 @@ def count_errors(bits, ref=None, counters=None):
     """uint64 counters [bit errors, frame errors, frames] (+= if `counters` is given) of hard
     decisions `bits` (B, N) (uint8 or float32) against `ref` (None = all-zero codeword)."""
     dev = N.device_of(bits)
+    bits = bits.to(dev)
     if counters is None:
         counters = torch.zeros(4, dtype=torch.int64, device=dev)
     if bits.dtype == torch.float32:
@@ -123,7 +126,9 @@ def count_errors(bits, ref=None, counters=None):
         kind = N.LDPC_OUT_U8
     bits = bits.contiguous()
     if ref is not None:
-        ref = (ref != 0).to(torch.uint8).contiguous()
+        ref = (ref.to(dev) != 0).to(torch.uint8).contiguous()
+    if counters.device != dev or counters.dtype != torch.int64 or not counters.is_contiguous():
+        raise ValueError("counters must be a contiguous int64 tensor on the bits' HIP device")
     N.check(N.lib().ldpc_count_errors(N.ptr(bits), kind, N.ptr(ref), bits.shape[0], bits.shape[1],
                                       N.ptr(counters), N.stream_ptr(dev)))
     return counters

@@ -239,6 +239,24 @@ def output_layer(final, llr, gt=None):
     return soft, torch.max(F.binary_cross_entropy(soft, gt, reduction="none"), dim=1).values
 
 
+def neural_decoder(params, llr, check_idx, var_idx, var_of_edge, depth_L, gt=None):
+    """models/decoder.py's LDPCNeuralDecoder composed from the layer restatements above (the
+    reference's models/decoder.py is missing: the composition is the build's definition, the
+    layers are the reference's).  params: [(w_ch, w_res)] per variable layer; var_of_edge (E,)."""
+    import torch
+    n = llr.shape[1]
+    x0 = llr[:, var_of_edge]
+    v, prevs = x0, []
+    zero = torch.zeros_like(x0)
+    for w_ch, w_res in params:
+        c = check_layer(v, check_idx)
+        v = residual_layer(x0, variable_layer(zero, c, var_idx), prevs, w_ch, w_res)
+        prevs = [v] + prevs[:max(depth_L - 1, 0)]
+    c = check_layer(v, check_idx)
+    app = torch.zeros((llr.shape[0], n), dtype=llr.dtype).index_add(1, var_of_edge, c)
+    return output_layer(-app, -llr, gt)
+
+
 # --------------------------------------------------------------------------- Philox-4x32-10
 def philox4x32_10(ctr, key):
     """Random123 Philox-4x32-10 (Salmon et al., SC'11) on uint32 arrays.
