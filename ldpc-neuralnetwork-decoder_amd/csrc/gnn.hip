@@ -515,6 +515,8 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         }
     };
     add_tiles(vptr, vmem, n_vgroups, 0);
+    int n_v1 = 0;  // var tiles come first, sorted by degree: the degree-1 ones lead
+    while (2 * n_v1 < (int)gt_meta.size() && gt_meta[2 * n_v1] == 1) ++n_v1;
     add_tiles(cptr, cmem, n_cgroups, n_vgroups);
     std::vector<int32_t> blob;
     blob.insert(blob.end(), h_vgroup, h_vgroup + E);
@@ -526,6 +528,7 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     const size_t gt_words = gt_meta.size() + gt_grp.size() + gt_mem.size();
     auto *p = new ldpc_gnn_plan();
     p->n_gtiles = (int)(gt_meta.size() / 2);
+    p->n_gtiles_v1 = n_v1;
     p->E = E;
     p->Gv = n_vgroups;
     p->Gc = n_cgroups;

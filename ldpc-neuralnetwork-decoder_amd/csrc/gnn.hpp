@@ -16,6 +16,7 @@ struct ldpc_gnn_plan {
     //   gt_meta[t] = {degree, offset into gt_mem}, gt_grp[8 t + q] = group id (check groups
     //   offset by Gv; -1 = padding), gt_mem[off + 8 i + q] = i-th member message of group q.
     int n_gtiles = 0;
+    int n_gtiles_v1 = 0;  // the leading tiles whose groups are var groups of degree 1
     int32_t *d_gt = nullptr;
     const int2 *gt_meta = nullptr;
     const int32_t *gt_grp = nullptr, *gt_mem = nullptr;

@@ -11,6 +11,9 @@
 //   two more constant vectors (U, V) and GEMM1 over x disappears.
 //   The group means keep the emb part: g = mean(x) + mean(emb[type]) where the second term is
 //   a per-(layer, group) constant (gnn_bf16_memb_kernel).
+//   A var group of degree 1 (1216 of 1664 at BG2 Z = 32) has g = c = x + emb[type]: from layer 1
+//   on its message skips the group-mean row altogether and feeds its own x as g, with
+//   W1_v,right emb[type] folded into a third type constant D1[t] (no Mv write, no Mv gather).
 //
 // Feature storage order.  A 64-feature row is stored permuted: stored position p = 16 s + 8 h + i
 // holds logical unit pi(p) = 32 (s>>1) + 16 (s&1) + 8 (i>>2) + 4 h + (i&3).  Then the 16-byte
@@ -74,8 +77,10 @@ __host__ __device__ inline LayerW layer_w(const float *blob, int T, int l) {
 }
 
 // derived constants per layer (floats): K[T + 2][2 sides][64 acc order] (rows T, T+1 = U, V of
-// layer 0), then b2v + b2c [64 acc], wo [64 acc]
-__host__ __device__ inline int64_t kd_floats(int T) { return (int64_t)(T + 2) * 128 + 128; }
+// layer 0), then b2v + b2c [64 acc], wo [64 acc], then D1[T][64 acc] = K[t][var side] +
+// W1_v,right emb[t] (degree-1 var groups)
+__host__ __device__ inline int64_t kd_floats(int T) { return (int64_t)(T + 2) * 128 + 128 + (int64_t)T * 64; }
+__host__ __device__ inline int64_t kd_d1(int T) { return (int64_t)(T + 3) * 128; }
 
 __global__ __launch_bounds__(128) void gnn_bf16_kconst_kernel(const float *blob, int T, float *kd) {
     const int l = blockIdx.x, t = blockIdx.y, side = threadIdx.x >> 6, a = threadIdx.x & 63;
@@ -87,22 +92,33 @@ __global__ __launch_bounds__(128) void gnn_bf16_kconst_kernel(const float *blob,
     for (int k = 0; k < H; ++k) s = fmaf(W1[k], v[k], s);
     float *out = kd + (int64_t)l * kd_floats(T);
     out[(int64_t)t * 128 + side * 64 + a] = s;
+    if (t < T && side == 0) {
+        float d = s;
+        for (int k = 0; k < H; ++k) d = fmaf(W1[H + k], v[k], d);
+        out[kd_d1(T) + (int64_t)t * 64 + a] = d;
+    }
     if (t == 0 && side == 0) {
         out[(int64_t)(T + 2) * 128 + a] = w.b2v[u] + w.b2c[u];
         out[(int64_t)(T + 2) * 128 + 64 + a] = w.wo[u];
     }
 }
 
-__global__ void gnn_bf16_info_kernel(int E, const int32_t *vgroup, const int32_t *cgroup, const int32_t *msg_type,
-                                     const int32_t *msg_var, int4 *info) {
+// info.x = var group, or ~var group (< 0) for a degree-1 var group when `d1` (see header)
+__global__ void gnn_bf16_info_kernel(int E, const int32_t *vgroup, const int32_t *vg_ptr, int d1,
+                                     const int32_t *cgroup, const int32_t *msg_type, const int32_t *msg_var,
+                                     int4 *info) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m < E) info[m] = make_int4(vgroup[m], cgroup[m], msg_type[m], msg_var[m]);
+    if (m >= E) return;
+    const int g = vgroup[m];
+    const bool one = d1 && vg_ptr[g + 1] - vg_ptr[g] == 1;
+    info[m] = make_int4(one ? ~g : g, cgroup[m], msg_type[m], msg_var[m]);
 }
 
 struct GtArgs {
     const int2 *meta;
     const int32_t *grp, *mem;
     int n_tiles;
+    int first;  // group-mean launches start at this tile (skipping degree-1 var tiles)
 };
 
 // memb[l][g][p] = mean over group g's messages of emb_l[type][pi(p)]  (one wave per (l, tile))
@@ -143,8 +159,9 @@ struct GmArgs {
 
 __global__ __launch_bounds__(256) void gnn_bf16_gm_kernel(GmArgs A) {
     const uint32_t w = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
-    if (w >= (uint32_t)(A.B * A.G.n_tiles)) return;
-    const uint32_t b = w / (uint32_t)A.G.n_tiles, t = w - b * (uint32_t)A.G.n_tiles;
+    const uint32_t nt = (uint32_t)(A.G.n_tiles - A.G.first);
+    if (w >= (uint32_t)A.B * nt) return;
+    const uint32_t b = w / nt, t = w - b * nt + (uint32_t)A.G.first;
     if (A.active && !A.active[b]) return;
     const int lane = threadIdx.x & 63, q = lane >> 3, p0 = 8 * (lane & 7);
     const int2 md = A.G.meta[t];
@@ -198,7 +215,9 @@ constexpr int kW1B = 64 * 136 * 2, kW2B = 64 * 72 * 2;
 constexpr int kOffW1v = 0, kOffW1c = kW1B, kOffW2v = 2 * kW1B, kOffW2c = 2 * kW1B + kW2B;
 constexpr int kOffK = 2 * kW1B + 2 * kW2B;
 constexpr int kKStride = 132;
-inline size_t mlp_lds_bytes(int T) { return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 192) * 4; }
+inline size_t mlp_lds_bytes(int T, bool d1) {
+    return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * 64 : 0)) * 4;
+}
 
 struct MlpArgs {
     const __bf16 *x_in;  // null at layer 0
@@ -210,6 +229,7 @@ struct MlpArgs {
     const float *kd;                     // this layer's derived constants
     const float *bo;                     // output_projection bias (device)
     int T, Gv, Gc, E, N, tpf;            // tpf = 32-message tiles per frame
+    int d1;                              // degree-1 var groups use D1 (info.x < 0), layers >= 1
     int64_t B;
     float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
     const uint8_t *active;               // early termination: frames still decoding (null = all)
@@ -244,6 +264,7 @@ struct TileIn {
     bf16x8 xf[4], af[4], cf[4];
     float l;
     int ty, var;
+    bool one;  // degree-1 var group (D1 constant instead of K[ty][var side])
     int64_t row, b;
     bool ok, on;  // on: the frame is still decoding (early termination)
 };
@@ -272,6 +293,9 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     float *tail = Ks + (A.T + 2) * kKStride;  // b2 [64], wo [64]
     if (tid < 128) tail[tid] = A.kd[nk + tid];
     if (A.kd_last && tid < 64) tail[128 + tid] = A.kd_last[nk + 64 + tid];  // wo of the last layer
+    float *D1s = tail + 192;  // D1 [T][64]
+    if (A.d1)
+        for (int i = tid; i < A.T * 64; i += NT) D1s[i] = A.kd[nk + 128 + i];
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
@@ -295,11 +319,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         const int64_t bb = t < tw.end ? b : fb;
         I.ty = inf.z;
         I.var = inf.w;
+        I.one = !layer0 && A.d1 && inf.x < 0;
         I.row = bb * A.E + m;
         I.b = bb;
         I.on = !A.active || A.active[bb];
         if (!I.on) return I;  // a terminated frame: nothing to load (uniform over the tile)
-        const char *ma = reinterpret_cast<const char *>(A.Mv + (bb * A.Gv + inf.x) * H) + 16 * h;
+        const int vg = inf.x < 0 ? ~inf.x : inf.x;
+        const char *ma = reinterpret_cast<const char *>(A.Mv + (bb * A.Gv + vg) * H) + 16 * h;
         const char *mc = reinterpret_cast<const char *>(A.Mc + (bb * A.Gc + inf.y) * H) + 16 * h;
         if constexpr (!layer0) {
             const char *xr = reinterpret_cast<const char *>(A.x_in + I.row * H) + 16 * h;
@@ -309,8 +335,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         } else {
             I.l = A.llr[bb * A.N + I.var];
         }
+        if (layer0 || !A.d1 || inf.x >= 0) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
+            for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
+        } else {  // degree-1 var group: g = x, its emb part is in D1
+#pragma unroll
+            for (int s = 0; s < 4; ++s) I.af[s] = I.xf[s];
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) I.cf[s] = ld8(mc + 32 * s);
         return I;
@@ -326,7 +357,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         for (int side = 0; side < 2; ++side) {
             const char *W1 = smem + (side == 0 ? kOffW1v : kOffW1c);
             const char *W2 = smem + (side == 0 ? kOffW2v : kOffW2c);
-            f32x16 h0 = ld16(Kt + side * 64 + 16 * h), h1 = ld16(Kt + side * 64 + 32 + 16 * h);
+            const float *K0 = side == 0 && I.one ? D1s + I.ty * 64 : Kt + side * 64;
+            f32x16 h0 = ld16(K0 + 16 * h), h1 = ld16(K0 + 32 + 16 * h);
             if constexpr (layer0) {  // + llr * (W1 w_in) + W1 b_in
                 const float *U = Ks + A.T * kKStride + side * 64 + 16 * h, *V = U + kKStride;
 #pragma unroll
@@ -567,7 +599,14 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     const int64_t tpf = (p->E + 31) / 32;
     if (B * tpf >= (1LL << 31) || B * p->n_gtiles >= (1LL << 31) || p->E >= (1LL << 31))
         return fail(LDPC_EUNSUPPORTED, "batch too large for one launch (chunk it)");
-    const size_t lds = mlp_lds_bytes(T);
+    // degree-1 skip when its D1 table still lets two 256-thread workgroups share a CU's LDS
+    // (LDPC_GNN_BF16_D1=0 disables it, for A/B runs)
+    static const int d1_env = [] {
+        const char *e = std::getenv("LDPC_GNN_BF16_D1");
+        return e ? std::atoi(e) : 1;
+    }();
+    const bool d1 = d1_env && p->n_gtiles_v1 > 0 && 2 * mlp_lds_bytes(T, true) <= 160 * 1024;
+    const size_t lds = mlp_lds_bytes(T, d1);
     if (T > kBf16MaxTypes || lds > 160 * 1024)
         return fail(LDPC_EUNSUPPORTED, "too many message types for the bf16 LDS image");
     if (!g_cus) {
@@ -575,10 +614,10 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         LDPC_HIP(hipGetDevice(&dev));
         LDPC_HIP(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    const GtArgs G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles};
+    const GtArgs G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles, 0};
     const int Gtot = p->Gv + p->Gc;
     hipLaunchKernelGGL(gnn_bf16_info_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, (int)p->E,
-                       p->vgroup, p->cgroup, d_msg_type, d_msg_var, w.info);
+                       p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, d_msg_type, d_msg_var, w.info);
     LDPC_CHECK_LAUNCH("gnn_bf16_info_kernel");
     hipLaunchKernelGGL(gnn_bf16_kconst_kernel, dim3(L, T + 2), dim3(128), 0, s, d_weights, T, w.kd);
     LDPC_CHECK_LAUNCH("gnn_bf16_kconst_kernel");
@@ -606,6 +645,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.b_in = d_weights + H;
         gm.memb = w.memb + (int64_t)l * Gtot * H;
         gm.G = G;
+        if (d1 && l > 0) gm.G.first = p->n_gtiles_v1;
         gm.Mv = w.Mv;
         gm.Mc = w.Mc;
         gm.Gv = p->Gv;
@@ -614,7 +654,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.N = N;
         gm.B = B;
         gm.active = active;
-        const int64_t gwaves = B * p->n_gtiles;
+        const int64_t gwaves = B * (gm.G.n_tiles - gm.G.first);
         hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, s, gm);
         LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
 
@@ -637,6 +677,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.E = (int)p->E;
         m.N = N;
         m.tpf = (int)tpf;
+        m.d1 = d1 ? 1 : 0;
         m.B = B;
         m.msg_out = w.msg_out;
         m.active = active;
