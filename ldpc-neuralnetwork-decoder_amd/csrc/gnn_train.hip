@@ -24,10 +24,13 @@
 // decode batches, and every product is an exact fp32 fma chain):
 //   train_group_mean_kernel  group means of c (or of any (B, E, H) array), one wave per group
 //   train_mlp_bwd_kernel     recompute u, h; dh, dz; writes c, h_v, h_c, dh_v, dh_c, dz parts
+//   train_mlp_bwd_mfma_kernel  the same for H = 64 on fp32 MFMA (default; bit-for-bit fmaf chains
+//                            in a different summation order than the VALU kernel)
 //   train_combine_kernel     dc and dx_l
 //   train_outer_kernel       weight gradients sum_r A_r (x) Z_r (+ bias sums), split over rows
 //   train_vec_kernel         emb / input-embedding / output-projection gradients
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "common.hpp"
@@ -107,6 +110,59 @@ __global__ __launch_bounds__(256) void train_group_mean_kernel(GmT A) {
     float s = 0.0f;
     for (int q = A.ptr[g]; q < A.ptr[g + 1]; ++q) s += c_value(A, b, A.mem[q], u);
     A.dst[w * A.H + u] = s * A.inv[g];
+}
+
+// H = 64: 16 lanes per group (float4 each), 4 groups per wave, members unrolled by 4 (the
+// kernel above keeps one 256-B row in flight per wave and is latency-bound)
+__device__ __forceinline__ float4 c_value4(const GmT &A, int64_t b, int64_t m, int q) {
+    float4 v;
+    if (A.src_mode == 2) {
+        const float l = A.llr[b * A.N + A.msg_var[m]];
+        const float4 w = reinterpret_cast<const float4 *>(A.w_in)[q], bi = reinterpret_cast<const float4 *>(A.b_in)[q];
+        v = make_float4(w.x * l + bi.x, w.y * l + bi.y, w.z * l + bi.z, w.w * l + bi.w);
+    } else {
+        v = reinterpret_cast<const float4 *>(A.src + (b * A.E + m) * 64)[q];
+    }
+    if (A.src_mode != 0) {
+        const float4 e = reinterpret_cast<const float4 *>(A.emb + A.msg_type[m] * 64)[q];
+        v = make_float4(v.x + e.x, v.y + e.y, v.z + e.z, v.w + e.w);
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void train_group_mean_h64_kernel(GmT A) {
+    const int lane = threadIdx.x & 63, q = lane & 15;
+    const int64_t gid = (xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
+    if (gid >= A.B * A.G) return;
+    const int64_t b = gid / A.G;
+    const int g = (int)(gid - b * A.G);
+    const int p0 = A.ptr[g], p1 = A.ptr[g + 1];
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    int p = p0;
+    for (; p + 4 <= p1; p += 4) {  // loads first; the adds keep the member order of the kernel above
+        const float4 v0 = c_value4(A, b, A.mem[p], q), v1 = c_value4(A, b, A.mem[p + 1], q);
+        const float4 v2 = c_value4(A, b, A.mem[p + 2], q), v3 = c_value4(A, b, A.mem[p + 3], q);
+        acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
+        acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
+        acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
+        acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
+    }
+    for (; p < p1; ++p) {
+        const float4 v = c_value4(A, b, A.mem[p], q);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    const float inv = A.inv[g];
+    reinterpret_cast<float4 *>(A.dst + gid * 64)[q] = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+}
+
+int launch_group_mean(const GmT &g, hipStream_t s) {
+    const int64_t n = g.B * g.G;
+    if (g.H == 64)
+        hipLaunchKernelGGL(train_group_mean_h64_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, g);
+    else
+        hipLaunchKernelGGL(train_group_mean_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, g);
+    LDPC_CHECK_LAUNCH("train_group_mean_kernel");
+    return LDPC_OK;
 }
 
 // ------------------------------------------------------------------------ MLP backward
@@ -256,6 +312,196 @@ __global__ __launch_bounds__(256) void train_mlp_bwd_kernel(MlpT A) {
     }
 }
 
+// ---- H = 64 on v_mfma_f32_32x32x2_f32: the same three products per message as the kernel above,
+// in the forward's transposed orientation (hidden units / input features on the MFMA rows,
+// 32 messages of a tile on the columns; lane (j, h) = message j, half h):
+//   GEMM1  u = W1 [c; g]       A = W1[u][k]   B = in[k]: half 0 lanes carry c, half 1 lanes g
+//                               (k-step kk pairs input k = kk with k = 64 + kk)
+//   GEMM2' d = W2^T dX         A = W2[o][u]   B = dX[o]: half h carries o = 32 h + kk
+//   GEMM3' dz = W1^T dh        A = W1[u][k]   B = dh straight from GEMM2's accumulators (step
+//                               (rt, r) pairs unit 32 rt + crow(r, 0) with 32 rt + crow(r, 1))
+// One padded row-major copy of each W1 ([64][129]) serves GEMM1 (lanes walk u: stride 129 words,
+// conflict-free within each 32-lane ds_read_b32 group) and GEMM3' (lanes walk k: consecutive
+// words); W2 is [64][65].  The dz of the c part of both sides accumulates in one register tile
+// (dco); the group parts go out per side.
+constexpr int kS1 = 129, kS2 = 65;
+inline size_t mlp_bwd_mfma_lds() { return ((size_t)2 * 64 * kS1 + 2 * 64 * kS2 + 128) * 4; }
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+struct F64 {
+    float v[64];
+    __device__ __forceinline__ float &operator[](int i) { return v[i]; }
+    __device__ __forceinline__ float operator[](int i) const { return v[i]; }
+};
+__device__ __forceinline__ int crow_t(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+template <int NT>
+__global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd_mfma_kernel(MlpT A) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    constexpr int H = 64;
+    float *W1v = sm, *W1c = W1v + H * kS1, *W2v = W1c + H * kS1, *W2c = W2v + H * kS2;
+    float *b1 = W2c + H * kS2;  // b1v [64], b1c [64]
+    for (int i = threadIdx.x; i < H * 2 * H; i += NT) {
+        const int o = i >> 7, k = i & 127;
+        W1v[o * kS1 + k] = A.w1v[i];
+        W1c[o * kS1 + k] = A.w1c[i];
+    }
+    for (int i = threadIdx.x; i < H * H; i += NT) {
+        const int o = i >> 6, k = i & 63;
+        W2v[o * kS2 + k] = A.w2v[i];
+        W2c[o * kS2 + k] = A.w2c[i];
+    }
+    if (threadIdx.x < H) {
+        b1[threadIdx.x] = A.b1v[threadIdx.x];
+        b1[H + threadIdx.x] = A.b1c[threadIdx.x];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 31, half = lane >> 5, wave = threadIdx.x >> 6;
+    const int64_t ntiles = (A.R + 31) / 32;
+    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
+    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+        const int64_t row = t * 32 + j;
+        const bool ok = row < A.R;
+        const int64_t rr = ok ? row : A.R - 1;
+        const int64_t b = rr / A.E, m = rr - b * A.E;
+        // B operand of GEMM1, rebuilt per side so it is not live across GEMM3': half 0 lanes c =
+        // x (or w_in llr + b_in) + emb[type] (written to cbuf on side 0 for the weight gradients),
+        // half 1 lanes the side's group mean
+        auto load_in = [&](int side) {
+            F64 in;
+            if (half == 0) {
+                const float4 *e = reinterpret_cast<const float4 *>(A.emb + A.msg_type[m] * H);
+                if (A.x) {
+                    const float4 *xr = reinterpret_cast<const float4 *>(A.x + rr * H);
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const float4 v = xr[q], ev = e[q];
+                        in[4 * q] = v.x + ev.x; in[4 * q + 1] = v.y + ev.y;
+                        in[4 * q + 2] = v.z + ev.z; in[4 * q + 3] = v.w + ev.w;
+                    }
+                } else {
+                    const float l = A.llr[b * A.N + A.msg_var[m]];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const float4 ev = e[q];
+                        const float4 w = reinterpret_cast<const float4 *>(A.w_in)[q];
+                        const float4 bi = reinterpret_cast<const float4 *>(A.b_in)[q];
+                        in[4 * q] = (w.x * l + bi.x) + ev.x; in[4 * q + 1] = (w.y * l + bi.y) + ev.y;
+                        in[4 * q + 2] = (w.z * l + bi.z) + ev.z; in[4 * q + 3] = (w.w * l + bi.w) + ev.w;
+                    }
+                }
+                if (side == 0 && ok) {
+                    float4 *cb = reinterpret_cast<float4 *>(A.cbuf + row * H);
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        cb[q] = make_float4(in[4 * q], in[4 * q + 1], in[4 * q + 2], in[4 * q + 3]);
+                }
+            } else {
+                const float4 *g = reinterpret_cast<const float4 *>(
+                    side == 0 ? A.Mv + (b * A.Gv + A.vgroup[m]) * H : A.Mc + (b * A.Gc + A.cgroup[m]) * H);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const float4 v = g[q];
+                    in[4 * q] = v.x; in[4 * q + 1] = v.y; in[4 * q + 2] = v.z; in[4 * q + 3] = v.w;
+                }
+            }
+            return in;
+        };
+        f32x16 dco0 = {}, dco1 = {};
+        int l1 = j * kS1 + 64 * half, l2 = (32 * half) * kS2 + j, l3 = j;  // per-lane LDS bases
+        asm volatile("" : "+v"(l1), "+v"(l2), "+v"(l3));
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const float *W1 = side == 0 ? W1v : W1c, *W2 = side == 0 ? W2v : W2c, *bs = b1 + 64 * side;
+            // GEMM2' first (dX is re-read per side, L2-hot, so it is not live across GEMM1):
+            // d[u][msg] = sum_o W2[o][u] dX[o]; A = W2[32 half + kk][32 rt + j]
+            f32x16 d0 = {}, d1 = {};
+            {
+                float dx[32];
+                const float4 *dp = reinterpret_cast<const float4 *>(A.dX + rr * H + 32 * half);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float4 v = dp[q];
+                    dx[4 * q] = v.x; dx[4 * q + 1] = v.y; dx[4 * q + 2] = v.z; dx[4 * q + 3] = v.w;
+                }
+#pragma unroll
+                for (int kk = 0; kk < 32; ++kk) {
+                    const float *wr = W2 + l2 + kk * kS2;
+                    d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[0], dx[kk], d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32], dx[kk], d1, 0, 0, 0);
+                }
+            }
+            // GEMM1: u[32 rt + i][msg]; A = W1[32 rt + j][64 half + kk]
+            f32x16 u0 = {}, u1 = {};
+            {
+                const F64 in = load_in(side);
+#pragma unroll
+                for (int kk = 0; kk < 64; ++kk) {
+                    const float *wr = W1 + l1 + kk;
+                    u0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[0], in[kk], u0, 0, 0, 0);
+                    u1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32 * kS1], in[kk], u1, 0, 0, 0);
+                }
+            }
+            // bias, relu, mask: lane holds units 32 rt + crow(r, half)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float a0 = u0[r] + bs[crow_t(r, half)], a1 = u1[r] + bs[32 + crow_t(r, half)];
+                u0[r] = fmaxf(a0, 0.0f);
+                u1[r] = fmaxf(a1, 0.0f);
+                d0[r] = a0 > 0.0f ? d0[r] : 0.0f;
+                d1[r] = a1 > 0.0f ? d1[r] : 0.0f;
+            }
+            if (ok) {
+                float *ho = (side == 0 ? A.hv : A.hc) + row * H, *dho = (side == 0 ? A.dhv : A.dhc) + row * H;
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const f32x16 &uu = rt ? u1 : u0, &dd = rt ? d1 : d0;
+                        const int o0 = 32 * rt + 8 * q + 4 * half;
+                        *reinterpret_cast<float4 *>(ho + o0) =
+                            make_float4(uu[4 * q], uu[4 * q + 1], uu[4 * q + 2], uu[4 * q + 3]);
+                        *reinterpret_cast<float4 *>(dho + o0) =
+                            make_float4(dd[4 * q], dd[4 * q + 1], dd[4 * q + 2], dd[4 * q + 3]);
+                    }
+            }
+            // GEMM3': dz[k][msg] = sum_u W1[u][k] dh[u]; A = W1[32 rt + crow(r, half)][32 kt + j]
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                f32x16 acc = kt == 0 ? dco0 : kt == 1 ? dco1 : f32x16{};
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float w = W1[l3 + (32 * rt + crow_t(r, half)) * kS1 + 32 * kt];
+                        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w, rt ? d1[r] : d0[r], acc, 0, 0, 0);
+                    }
+                __builtin_amdgcn_sched_barrier(0);  // keep each kt's 32 A reads next to their MFMAs
+                if (kt == 0) dco0 = acc;
+                else if (kt == 1) dco1 = acc;
+                else if (ok) {  // group part: k = 64 + 32 (kt - 2) + unit
+                    float *go = (side == 0 ? A.da : A.db) + row * H + 32 * (kt - 2);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        *reinterpret_cast<float4 *>(go + 8 * q + 4 * half) =
+                            make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                }
+            }
+        }
+        if (ok) {
+            float *co = A.dco + row * H;
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const f32x16 &cc = rt ? dco1 : dco0;
+                    *reinterpret_cast<float4 *>(co + 32 * rt + 8 * q + 4 * half) =
+                        make_float4(cc[4 * q], cc[4 * q + 1], cc[4 * q + 2], cc[4 * q + 3]);
+                }
+        }
+    }
+}
+
 // dc = dco + mean_var(da) + mean_chk(db) -> dco (kept for demb); dx_l = dc (+ dX)
 __global__ void train_combine_kernel(float *__restrict__ dco, const float *__restrict__ Mda,
                                      const float *__restrict__ Mdb, const float *__restrict__ dX,
@@ -355,48 +601,69 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
 #pragma unroll
         for (int jt = 0; jt < NJT; ++jt) acc[it][jt] = f32x16{};
     float bsum[NIT] = {};
-    auto zval = [&](int64_t r, int j) -> float {
+    auto zval = [&](int64_t r, int64_t b, int64_t m, int j) -> float {
         if (j >= J) return 0.0f;
         if (j < H) return P.zsrc[r * H + j];
-        const int64_t b = r / P.E, m = r - b * P.E;
         return P.G[(b * P.Gn + P.grp[m]) * H + (j - H)];
     };
-    for (int64_t r0 = r_begin; r0 < r_end; r0 += 2) {
-        const int64_t r = r0 + k;
-        const bool ok = r < r_end;
-        float a[NIT], z[NJT];
+    // (frame, message) of row r0 + k, stepped along with r0 (no 64-bit division per row)
+    int64_t bb = (r_begin + k) / P.E, mm = r_begin + k - bb * P.E;
+    // KU k-steps (2 KU rows) of fragments are loaded before their MFMAs, so each wave keeps
+    // 2 KU (NIT + NJT) independent loads in flight instead of waiting on one k-step at a time
+    constexpr int KU = 8;
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * KU) {
+        float a[KU][NIT], z[KU][NJT];
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int i = 32 * it + col;
-            a[it] = ok && i < H ? P.A[r * H + i] : 0.0f;
+        for (int u = 0; u < KU; ++u) {
+            const int64_t r = r0 + 2 * u + k;
+            const bool ok = r < r_end;
+            int64_t bu = bb, mu = mm + 2 * u;
+            while (mu >= P.E) { mu -= P.E; ++bu; }
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                const int i = 32 * it + col;
+                a[u][it] = ok && i < H ? P.A[r * H + i] : 0.0f;
+            }
+#pragma unroll
+            for (int jt = 0; jt < NJT; ++jt) z[u][jt] = ok ? zval(r, bu, mu, 32 * jt + col) : 0.0f;
         }
+        mm += 2 * KU;
+        while (mm >= P.E) { mm -= P.E; ++bb; }
 #pragma unroll
-        for (int jt = 0; jt < NJT; ++jt) z[jt] = ok ? zval(r, 32 * jt + col) : 0.0f;
+        for (int u = 0; u < KU; ++u)
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            bsum[it] += a[it];
+            for (int it = 0; it < NIT; ++it) {
+                bsum[it] += a[u][it];
 #pragma unroll
-            for (int jt = 0; jt < NJT; ++jt)
-                acc[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[it], z[jt], acc[it][jt], 0, 0, 0);
-        }
+                for (int jt = 0; jt < NJT; ++jt)
+                    acc[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][it], z[u][jt], acc[it][jt], 0, 0, 0);
+            }
     }
-    if (r_begin >= r_end) return;
-    // D[i][j]: register q of lane l holds i = 8 (q >> 2) + 4 k + (q & 3), j = col
+    // D[i][j]: register q of lane l holds i = 8 (q >> 2) + 4 k + (q & 3), j = col.  The four waves'
+    // tiles are summed in LDS first, so each workgroup issues one global atomic per gradient entry
+    // (per-wave atomics put thousands of adds on every address).
+    __shared__ float red[NIT * 32 * NJT * 32], bred[NIT * 32];
+    for (int e = threadIdx.x; e < NIT * 32 * NJT * 32; e += 256) red[e] = 0.0f;
+    if (threadIdx.x < NIT * 32) bred[threadIdx.x] = 0.0f;
+    __syncthreads();
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
 #pragma unroll
-        for (int jt = 0; jt < NJT; ++jt) {
-            const int j = 32 * jt + col;
+        for (int jt = 0; jt < NJT; ++jt)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int i = 32 * it + 8 * (q >> 2) + 4 * k + (q & 3);
-                if (i < H && j < J) atomicAdd(&P.out[i * J + j], acc[it][jt][q]);
+                atomicAdd(&red[i * (NJT * 32) + 32 * jt + col], acc[it][jt][q]);
             }
-        }
-        float s = bsum[it] + __shfl_xor(bsum[it], 32, 64);
-        const int i = 32 * it + col;
-        if (P.bias && k == 0 && i < H) atomicAdd(&P.bias[i], s);
+        const float s = bsum[it] + __shfl_xor(bsum[it], 32, 64);
+        if (k == 0) atomicAdd(&bred[32 * it + col], s);
     }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NIT * 32 * NJT * 32; e += 256) {
+        const int i = e / (NJT * 32), j = e - i * (NJT * 32);
+        if (i < H && j < J) atomicAdd(&P.out[i * J + j], red[e]);
+    }
+    if (P.bias && threadIdx.x < H) atomicAdd(&P.bias[threadIdx.x], bred[threadIdx.x]);
 }
 
 int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
@@ -497,6 +764,14 @@ TrainWs carve_train(const ldpc_gnn_plan *p, int H, int N, int64_t B, void *base)
 
 int g_cus_t = 0;
 
+int bwd_mfma() {
+    static const int v = [] {
+        const char *e = std::getenv("LDPC_GNN_TRAIN_MFMA");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
 }  // namespace
 }  // namespace ldpc
 
@@ -550,6 +825,10 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
     const size_t lds_mlp = mlp_bwd_lds(H);
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_kernel),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_mlp));
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<512>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<256>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     auto blocks = [](int64_t work, int per) { return dim3((unsigned)((work + per - 1) / per)); };
     const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * 4);
 
@@ -587,10 +866,9 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         g.msg_type = d_msg_type; g.msg_var = d_msg_var;
         g.src_mode = x ? 1 : 2; g.H = H; g.N = N; g.E = E; g.B = B;
         g.ptr = p->vg_ptr; g.mem = p->vg_mem; g.inv = p->inv_v; g.G = p->Gv; g.dst = w.Mv;
-        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gv, 4), dim3(256), 0, s, g);
+        if (int rc = launch_group_mean(g, s)) return rc;
         g.ptr = p->cg_ptr; g.mem = p->cg_mem; g.inv = p->inv_c; g.G = p->Gc; g.dst = w.Mc;
-        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gc, 4), dim3(256), 0, s, g);
-        LDPC_CHECK_LAUNCH("train_group_mean_kernel");
+        if (int rc = launch_group_mean(g, s)) return rc;
         // MLP backward
         MlpT m{};
         m.x = x; m.llr = d_llr; m.w_in = d_weights; m.b_in = d_weights + H;
@@ -600,17 +878,26 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         m.cbuf = w.cbuf; m.hv = w.hv; m.hc = w.hc; m.dhv = w.dhv; m.dhc = w.dhc;
         m.dco = w.dco; m.da = w.da; m.db = w.db;
         m.H = H; m.N = N; m.Gv = p->Gv; m.Gc = p->Gc; m.E = E; m.R = R;
-        const unsigned mgrid = (unsigned)std::min<int64_t>((R + 4 * kNM - 1) / (4 * kNM), (int64_t)g_cus_t * 2);
-        hipLaunchKernelGGL(train_mlp_bwd_kernel, dim3(mgrid), dim3(256), lds_mlp, s, m);
-        LDPC_CHECK_LAUNCH("train_mlp_bwd_kernel");
+        if (H == 64 && bwd_mfma()) {  // LDPC_GNN_TRAIN_MFMA=0 selects the VALU kernel (A/B runs)
+            const int nt = bwd_mfma() == 2 ? 256 : 512;  // =2: 256 threads, 1 wave per SIMD
+            const unsigned grid = (unsigned)std::min<int64_t>((R + 32 * (nt / 64) - 1) / (32 * (nt / 64)), (int64_t)g_cus_t);
+            if (nt == 256)
+                hipLaunchKernelGGL(train_mlp_bwd_mfma_kernel<256>, dim3(grid), dim3(256), mlp_bwd_mfma_lds(), s, m);
+            else
+                hipLaunchKernelGGL(train_mlp_bwd_mfma_kernel<512>, dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);
+            LDPC_CHECK_LAUNCH("train_mlp_bwd_mfma_kernel");
+        } else {
+            const unsigned mgrid = (unsigned)std::min<int64_t>((R + 4 * kNM - 1) / (4 * kNM), (int64_t)g_cus_t * 2);
+            hipLaunchKernelGGL(train_mlp_bwd_kernel, dim3(mgrid), dim3(256), lds_mlp, s, m);
+            LDPC_CHECK_LAUNCH("train_mlp_bwd_kernel");
+        }
         // group means of the aggregated-input gradients (the mean operator is symmetric)
         GmT d{};
         d.src_mode = 0; d.H = H; d.N = N; d.E = E; d.B = B;
         d.src = w.da; d.ptr = p->vg_ptr; d.mem = p->vg_mem; d.inv = p->inv_v; d.G = p->Gv; d.dst = w.Mda;
-        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gv, 4), dim3(256), 0, s, d);
+        if (int rc = launch_group_mean(d, s)) return rc;
         d.src = w.db; d.ptr = p->cg_ptr; d.mem = p->cg_mem; d.inv = p->inv_c; d.G = p->Gc; d.dst = w.Mdb;
-        hipLaunchKernelGGL(train_group_mean_kernel, blocks(B * p->Gc, 4), dim3(256), 0, s, d);
-        LDPC_CHECK_LAUNCH("train_group_mean_kernel");
+        if (int rc = launch_group_mean(d, s)) return rc;
         hipLaunchKernelGGL(train_combine_kernel, blocks(n, 256), dim3(256), 0, s, w.dco, w.Mda, w.Mdb, w.dX,
                            p->vgroup, p->cgroup, H, p->Gv, p->Gc, E, n, l > 0 ? 1 : 0, w.dXp);
         LDPC_CHECK_LAUNCH("train_combine_kernel");

@@ -15,7 +15,7 @@ def main(d, frames=None):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        m = re.search(r"((?:gnn|flood|bf16|qpsk|count|batch)\w*(<[^>]*>)?)", n)
+        m = re.search(r"((?:gnn|flood|bf16|qpsk|count|batch|train|csr|gather|residual|output_layer)\w*(<[^>]*>)?)", n)
         agg[m.group(1) if m else n[:40]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for n, v in sorted(agg.items(), key=lambda x: -sum(x[1]))[:10]:
         v = sorted(v)
