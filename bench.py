@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--workload", default="minsum-z32", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="frames per GPU (0 = workload default)")
     ap.add_argument("--snr", type=float, default=None)
+    ap.add_argument("--early-termination", choices=("auto", "on", "off"), default="auto",
+                    help="bf16 GNN per-frame early termination (auto: on for gnn-z32-bf16 = cfg5 only)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
                     help="target CPU work for the oracle baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=None,
@@ -272,7 +274,8 @@ def main():
         if kind == "gnn-bf16":
             gdec.precision = "bf16"
             # cfg5 = 15 iterations + per-frame early-termination syndrome check
-            gdec.early_termination = a.workload == "gnn-z32-bf16"
+            gdec.early_termination = (a.workload == "gnn-z32-bf16" if a.early_termination == "auto"
+                                      else a.early_termination == "on")
         types = conv.get_message_types(base, z).to(dev).to(torch.int32)
         io = conv.message_to_var_index().to(dev).to(torch.int32)
         probs = torch.empty((B, n), dtype=torch.float32, device=dev)
