@@ -352,7 +352,12 @@ def main():
         value = total_frames / elapsed
         achieved = per_launch_alg / (kern_ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
         traffic = None
-        tj = a.traffic_json or os.path.join(ROOT, "profiles", f"r01s2_pmc_{a.workload.replace('-', '_')}.json")
+        tj = a.traffic_json
+        if tj is None:  # the newest PMC summary of this workload (profiles/<round>_pmc_<workload>.json)
+            for tag in ("r01s3", "r01s2"):
+                tj = os.path.join(ROOT, "profiles", f"{tag}_pmc_{a.workload.replace('-', '_')}.json")
+                if os.path.exists(tj):
+                    break
         if os.path.exists(tj):
             tjd = json.load(open(tj))
             # the PMC pass ran the same workload at the default batch; scale per launch to this B

@@ -1,4 +1,4 @@
-# Bench lines for every workload (+ kernel-trace stats for the GNN ones) into gpurun_out/bench_all.
+# Bench lines for every workload into gpurun_out/bench_all (one JSON line each).
 set -o pipefail
 R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/bench_all; mkdir -p $OUT
 cd $R
@@ -13,4 +13,8 @@ run gnn-z4 --workload gnn-z4 --steps 10 --warmup 3 --cpu-baseline-seconds 10
 run gnn-z4-bf16 --workload gnn-z4-bf16 --steps 10 --warmup 3 --cpu-baseline-seconds 0
 run gnn-z32 --workload gnn-z32 --steps 3 --warmup 1 --cpu-baseline-seconds 10
 run gnn-z32-bf16 --workload gnn-z32-bf16 --steps 3 --warmup 1 --cpu-baseline-seconds 0
+run gnn-z32-bf16-noet --workload gnn-z32-bf16 --early-termination off --steps 3 --warmup 1 --cpu-baseline-seconds 0
 run gnn-z32-bf16-i10 --workload gnn-z32-bf16-i10 --steps 3 --warmup 1 --cpu-baseline-seconds 10
+run gnn-train-z32 --workload gnn-train-z32 --steps 5 --warmup 2 --cpu-baseline-seconds 10
+run gnn-train-z4 --workload gnn-train-z4 --steps 5 --warmup 2 --cpu-baseline-seconds 10
+run lay-z32 --workload lay-z32 --steps 10 --warmup 3 --cpu-baseline-seconds 10

@@ -6,7 +6,7 @@ the bytes of a wide coalesced streaming read, so bytes = (2 * FETCH_SIZE + WRITE
 (the counters are in KB).  Here the doubling is checked against a known byte count: the LLR
 input of the flood decoder is B*N*4 bytes and it is read exactly once.
 
-    python tools/pmc_summary.py gpurun_out/prof_<tag>_<w> <kernel-substring> <out.json> [expected_read_bytes]
+    python tools/pmc_summary.py gpurun_out/prof_<tag>_<w> <kernel-substring> <out.json> [expected_read_bytes|-] [per-call-kernel]
 """
 import collections
 import csv
@@ -15,16 +15,29 @@ import os
 import sys
 
 
-def main(d, kern, out, expected_read=None):
+def main(d, kern, out, expected_read=None, per_call=None):
+    """per_call: a kernel-name substring launched once per call (e.g. once per GNN forward); when
+    given, counters are summed over every kernel matching `kern` and divided by the number of
+    such calls, so "per launch" means per call of a multi-kernel path."""
     agg = collections.defaultdict(list)
+    calls = collections.Counter()
     for sub in sorted(os.listdir(d)):
         f = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
+        seen = set()
         for r in csv.DictReader(open(f)):
-            if kern in r["Kernel_Name"]:
+            if per_call and per_call in r["Kernel_Name"]:
+                key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), r["Counter_Name"])
+                if key not in seen:
+                    seen.add(key)
+                    calls[r["Counter_Name"]] += 1
+            if any(k in r["Kernel_Name"] for k in kern.split("|")):  # '|' separates alternatives
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    res = {k: sum(v) / len(v) for k, v in agg.items()}
+    if per_call:
+        res = {k: sum(v) / max(calls[k], 1) for k, v in agg.items()}
+    else:
+        res = {k: sum(v) / len(v) for k, v in agg.items()}
     waves = res.get("SQ_WAVES")
     out_d = {"kernel_substring": kern, "counters_per_launch": res}
     if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
@@ -43,4 +56,7 @@ def main(d, kern, out, expected_read=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    a = sys.argv[1:]
+    if len(a) > 3 and a[3] == "-":
+        a[3] = None
+    main(*a)
