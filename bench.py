@@ -99,8 +99,15 @@ def setup_dist():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # BENCH_DIST_BACKEND=gloo with more ranks than GPUs is a rehearsal of the multi-rank path
+        # on a 1-GPU box (ranks share the card); the measured runs use RCCL ("nccl"), one GPU each
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        dev_i = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
+        torch.cuda.set_device(dev_i)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_i))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, torch.device("cuda", torch.cuda.current_device())
