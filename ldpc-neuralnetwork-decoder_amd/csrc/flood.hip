@@ -106,6 +106,19 @@ struct MinSumStats {
 //   * the excluded minimum is m2 exactly when |x| == m1: a tie at m1 puts m1 in m2 as well, so
 //     no first-index bookkeeping is needed.
 // Every output is bit-identical to MinSumStats::c2v: +-(alpha * m) with the same alpha * m.
+// xor of the messages' bit patterns (its sign bit = the row's sign parity): v_bitop3_b32 with the
+// three-input xor table (0x96) takes two messages per instruction (the compiler keeps a chain of
+// two-input xors here)
+template <int DC>
+__device__ __forceinline__ uint32_t sign_parity(const float (&v)[DC]) {
+    uint32_t p = __float_as_uint(v[0]);
+#pragma unroll
+    for (int e = 1; e + 1 < DC; e += 2)
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(p) : "v"(p), "v"(v[e]), "v"(v[e + 1]));
+    if constexpr (DC % 2 == 0) p ^= __float_as_uint(v[DC - 1]);
+    return p;
+}
+
 struct MinSumFast {
     float m1 = INFINITY, m2 = INFINITY;
     uint32_t par = 0;
@@ -113,14 +126,23 @@ struct MinSumFast {
     __device__ __forceinline__ void add(float x) {
         const float a = fabsf(x);
         special |= is_zero_sign(x);
-        par ^= __float_as_uint(x);
-        m2 = fminf(m2, fmaxf(m1, a));
-        m1 = fminf(m1, a);
+        // m2 = min(m2, max(m1, a)) = median(m1, a, m2) since m1 <= m2: one v_med3_f32 with |x|
+        // as a source modifier.  m1 = min(m1, |x|) as one v_min_f32 in asm: fminf (and a med3
+        // with -inf, which the compiler turns back into it) adds a NaN-quieting v_max per edge,
+        // and this path never sees a NaN (special -> MinSumStats).
+        m2 = __builtin_amdgcn_fmed3f(m1, a, m2);
+        asm("v_min_f32 %0, %1, |%2|" : "=v"(m1) : "v"(m1), "v"(x));
     }
-    __device__ __forceinline__ float c2v(float x, float am1, float am2) const {
-        const float am = fabsf(x) == m1 ? am2 : am1;
-        // sign bit of parity ^ x over the magnitude bits of alpha * m (v_xor + v_bfi)
-        return __uint_as_float(((par ^ __float_as_uint(x)) & 0x80000000u) | (__float_as_uint(am) & 0x7fffffffu));
+    // s1 / s2 = |alpha m1| / |alpha m2| with the row's sign parity in the sign bit (sel_words);
+    // the message's own sign bit is xored back out: out = (x & SIGN) ^ sel (one v_bitop3)
+    __device__ __forceinline__ float c2v(float x, uint32_t s1, uint32_t s2) const {
+        const uint32_t sel = fabsf(x) == m1 ? s2 : s1;
+        return __uint_as_float((__float_as_uint(x) & 0x80000000u) ^ sel);
+    }
+    __device__ __forceinline__ void sel_words(float alpha, uint32_t &s1, uint32_t &s2) const {
+        const uint32_t ps = par & 0x80000000u;
+        s1 = __float_as_uint(fabsf(alpha * m1)) | ps;
+        s2 = __float_as_uint(fabsf(alpha * m2)) | ps;
     }
 };
 
@@ -189,10 +211,12 @@ __device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, const in
         MinSumFast fs;
 #pragma unroll
         for (int e = 0; e < DC; ++e) fs.add(v[e]);
+        fs.par = sign_parity(v);
         if (!__any(fs.special)) {  // wave-uniform
-            const float am1 = C.alpha * fs.m1, am2 = C.alpha * fs.m2;
+            uint32_t s1, s2;
+            fs.sel_words(C.alpha, s1, s2);
 #pragma unroll
-            for (int e = 0; e < DC; ++e) emit(e, fs.c2v(v[e], am1, am2));
+            for (int e = 0; e < DC; ++e) emit(e, fs.c2v(v[e], s1, s2));
         } else {
             MinSumStats st;
 #pragma unroll
@@ -582,9 +606,11 @@ __device__ __forceinline__ void fx_check_row(const Ctx &C, const Lane &L, int &e
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
         MinSumFast fs;
         sfor<DC>([&](auto e) { fs.add(v[decltype(e)::value]); });
+        fs.par = sign_parity(v);
         if (!__any(fs.special)) {  // wave-uniform
-            const float am1 = C.alpha * fs.m1, am2 = C.alpha * fs.m2;
-            sfor<DC>([&](auto e) { emit(e, fs.c2v(v[decltype(e)::value], am1, am2)); });
+            uint32_t s1, s2;
+            fs.sel_words(C.alpha, s1, s2);
+            sfor<DC>([&](auto e) { emit(e, fs.c2v(v[decltype(e)::value], s1, s2)); });
         } else {
             MinSumStats st;
             sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
