@@ -11,6 +11,7 @@
 // in-place masked writes -> zero gradient).
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -61,6 +62,99 @@ __global__ void gather_minsum_kernel(const float *__restrict__ in, int64_t B, in
         out[o] = sp[f] * m[f];
         if (argmin) argmin[o] = am[f];
     }
+}
+
+// LDS-staged form of the gathers (used for CheckLayer): a workgroup stages FPW whole input rows (frames) into LDS
+// with coalesced 16-byte loads, then gathers from LDS.  The global kernels above gather 4-byte
+// words at random columns of a row (a check's or variable's other edges are far apart in the
+// var-major numbering), which is bound by address processing at ~0.8 TB/s; here the row is read
+// once, contiguously.  Per output the arithmetic is the same sequence, so results are identical.
+template <int FPW, bool MINSUM>
+__global__ __launch_bounds__(512) void gather_lds_kernel(const float *__restrict__ in, const float *__restrict__ llr,
+                                                         int64_t B, int n_in, const int32_t *__restrict__ idx, int n_out,
+                                                         int K, float *__restrict__ out, int32_t *__restrict__ argmin) {
+    extern __shared__ __attribute__((aligned(16))) float rows[];  // [FPW][n_in]
+    const int64_t b0 = (int64_t)blockIdx.x * FPW;
+    const int nb = (int)min<int64_t>(FPW, B - b0);
+    const float *src = in + b0 * n_in;
+    const int total = nb * n_in;
+    if ((n_in & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(src);
+        float4 *r4 = reinterpret_cast<float4 *>(rows);
+        for (int e = threadIdx.x; e < total / 4; e += blockDim.x) r4[e] = s4[e];
+    } else {
+        for (int e = threadIdx.x; e < total; e += blockDim.x) rows[e] = src[e];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n_out; i += blockDim.x) {
+        float acc[FPW], m[FPW];
+        int am[FPW];
+#pragma unroll
+        for (int f = 0; f < FPW; ++f) { acc[f] = MINSUM ? 1.0f : 0.0f; m[f] = 0.0f; am[f] = 0; }
+        for (int k = 0; k < K; ++k) {
+            const int j = idx[(int64_t)k * n_out + i];
+#pragma unroll
+            for (int f = 0; f < FPW; ++f) {
+                if (f >= nb) break;
+                const float v = j < 0 ? 0.0f : rows[f * n_in + j];
+                if constexpr (MINSUM) {  // gather_minsum_kernel's update
+                    acc[f] = acc[f] * torch_sign(v + 1e-10f);
+                    float a = fabsf(v);
+                    if (a == 0.0f) a = 1e10f;
+                    if (k == 0 || (!isnan(m[f]) && (a < m[f] || isnan(a)))) {
+                        m[f] = a;
+                        am[f] = k;
+                    }
+                } else {  // gather_sum_kernel's update
+                    acc[f] += v;
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < FPW; ++f) {
+            if (f >= nb) break;
+            const int64_t o = (b0 + f) * n_out + i;
+            if constexpr (MINSUM) {
+                out[o] = acc[f] * m[f];
+                if (argmin) argmin[o] = am[f];
+            } else {
+                out[o] = llr ? llr[o] + acc[f] : acc[f];
+            }
+        }
+    }
+}
+
+constexpr size_t kGatherLds = 64 * 1024;  // LDS per workgroup for the staged rows
+
+// frames per workgroup for the staged gathers (0: a row does not fit, use the global kernel)
+int gather_fpw(int n_in) {
+    const size_t row = (size_t)n_in * 4;
+    for (int f = 8; f >= 1; f /= 2)
+        if ((size_t)f * row <= kGatherLds) return f;
+    return 0;
+}
+
+template <bool MINSUM>
+int launch_gather_lds(int fpw, const float *in, const float *llr, int64_t B, int n_in, const int32_t *idx, int n_out,
+                      int K, float *out, int32_t *argmin, hipStream_t s) {
+    const dim3 grid((unsigned)((B + fpw - 1) / fpw));
+    const size_t lds = (size_t)fpw * n_in * 4;
+    switch (fpw) {
+        case 8: hipLaunchKernelGGL((gather_lds_kernel<8, MINSUM>), grid, dim3(512), lds, s, in, llr, B, n_in, idx, n_out, K, out, argmin); break;
+        case 4: hipLaunchKernelGGL((gather_lds_kernel<4, MINSUM>), grid, dim3(512), lds, s, in, llr, B, n_in, idx, n_out, K, out, argmin); break;
+        case 2: hipLaunchKernelGGL((gather_lds_kernel<2, MINSUM>), grid, dim3(512), lds, s, in, llr, B, n_in, idx, n_out, K, out, argmin); break;
+        default: hipLaunchKernelGGL((gather_lds_kernel<1, MINSUM>), grid, dim3(512), lds, s, in, llr, B, n_in, idx, n_out, K, out, argmin); break;
+    }
+    LDPC_CHECK_LAUNCH("gather_lds_kernel");
+    return LDPC_OK;
+}
+
+bool gather_lds_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("LDPC_GATHER_LDS");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
 }
 
 // d in[b][idx[i][k*]] += g[b][i] * sign_product * sgn(v_k*)  (k* = argmin; sgn(0) = 0 covers the
@@ -253,6 +347,9 @@ extern "C" int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const 
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
     if (!d_in || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
+    if (const int fpw = gather_lds_enabled() ? gather_fpw(n_in) : 0)
+        return launch_gather_lds<true>(fpw, d_in, nullptr, B, n_in, d_idx, n_out, K, d_out, d_argmin,
+                                       static_cast<hipStream_t>(stream));
     hipLaunchKernelGGL(gather_minsum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_in,
                        B, n_in, d_idx, n_out, K, d_out, d_argmin);
@@ -279,6 +376,9 @@ extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t 
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
     if (!d_msgs || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
+    // (the LDS-staged form is slower here: VariableLayer's index is padded to the largest
+    // variable degree -- K = 22 at BG2 -- and the global kernel spreads each index read over 4
+    // frames instead of 2)
     hipLaunchKernelGGL(gather_sum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_llr,
                        d_msgs, B, n_in, d_idx, n_out, K, d_out);

@@ -33,7 +33,7 @@ import torch.nn as nn
 
 from ldpc_neural_decoder import _native as N
 from ldpc_neural_decoder.models.layers import (
-    OutputLayer, ResidualLayer, _CheckFn, _check_index, gather_sum)
+    OutputLayer, ResidualLayer, _check_index, check_minsum, gather_sum)
 
 _STRUCT = {}
 
@@ -103,10 +103,10 @@ class LDPCNeuralDecoder(nn.Module):
         x0 = gather_sum(llr, x0_idx)
         v, prevs = x0, []
         for res in self.residual_layers:
-            c = _CheckFn.apply(v, cidx)
+            c = check_minsum(v, cidx)
             v = res(x0, gather_sum(c, vidx), prevs)
             prevs = [v] + prevs[:max(self.depth_L - 1, 0)]
-        app = gather_sum(_CheckFn.apply(v, cidx), app_idx)
+        app = gather_sum(check_minsum(v, cidx), app_idx)
         gt = None if ground_truth is None else ground_truth.to(dev, torch.float32)
         soft, loss = self.output_layer(-app, -llr, gt)
         if loss is None:

@@ -66,6 +66,19 @@ class _CheckFn(torch.autograd.Function):
         return gin, None
 
 
+def check_minsum(x, idx):
+    """CheckLayer's min-sum on a prepared index.  Without autograd (inference, or an input that
+    needs no gradient) the argmin the backward would need is not written."""
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _CheckFn.apply(x, idx)
+    B, n_in = x.shape
+    K, n_out = idx.shape
+    out = torch.empty((B, n_out), dtype=torch.float32, device=x.device)
+    N.check(N.lib().ldpc_gather_minsum(N.ptr(x), B, n_in, N.ptr(idx), n_out, K, N.ptr(out), None,
+                                       N.stream_ptr(x.device)))
+    return out
+
+
 class _VarFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, llr, msgs, idx):
@@ -186,7 +199,7 @@ class CheckLayer(nn.Module):
         home, dev = _home_and_dev(input_tensor)
         x = _dev_f32(input_tensor, dev)
         idx = _check_index(check_index_tensor, x.shape[1], dev)
-        return _CheckFn.apply(x, idx).to(home)
+        return check_minsum(x, idx).to(home)
 
 
 class VariableLayer(nn.Module):
