@@ -28,7 +28,7 @@
 //                            in a different summation order than the VALU kernel)
 //   train_combine_kernel     dc and dx_l
 //   train_outer_kernel       weight gradients sum_r A_r (x) Z_r (+ bias sums), split over rows
-//   train_vec_kernel         emb / input-embedding / output-projection gradients
+//   train_colsum_kernel + train_vecfinal_kernel  emb / input-embedding / output-projection gradients
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -90,6 +90,7 @@ struct GmT {
     const float *inv;
     float *dst;  // (B, G, H)
     int src_mode, G, H, N;
+    int sum_only = 0;  // 1: plain group sums (inv ignored)
     int64_t E, B;
 };
 
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(256) void train_group_mean_kernel(GmT A) {
     const int g = (int)(w - b * A.G);
     float s = 0.0f;
     for (int q = A.ptr[g]; q < A.ptr[g + 1]; ++q) s += c_value(A, b, A.mem[q], u);
-    A.dst[w * A.H + u] = s * A.inv[g];
+    A.dst[w * A.H + u] = A.sum_only ? s : s * A.inv[g];
 }
 
 // H = 64: 16 lanes per group (float4 each), 4 groups per wave, members unrolled by 4 (the
@@ -151,8 +152,11 @@ __global__ __launch_bounds__(256) void train_group_mean_h64_kernel(GmT A) {
         const float4 v = c_value4(A, b, A.mem[p], q);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    const float inv = A.inv[g];
-    reinterpret_cast<float4 *>(A.dst + gid * 64)[q] = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    if (!A.sum_only) {
+        const float inv = A.inv[g];
+        acc = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    }
+    reinterpret_cast<float4 *>(A.dst + gid * 64)[q] = acc;
 }
 
 int launch_group_mean(const GmT &g, hipStream_t s) {
@@ -525,6 +529,7 @@ struct OuterT {
     const int32_t *grp;
     float *out, *bias;
     int H, J, Gn;
+    int ld = 0, col0 = 0;  // out[i * ld + col0 + j] (ld 0 = J): one half of a [H][2H] gradient
     int64_t E, R;
 };
 constexpr int kRB = 16;  // rows staged per step
@@ -574,7 +579,7 @@ __global__ __launch_bounds__(256) void train_outer_kernel(OuterT P) {
     if (i < H) {
 #pragma unroll
         for (int k = 0; k < 32; ++k)
-            if (k < JW) atomicAdd(&P.out[i * J + jq * JW + k], acc[k]);
+            if (k < JW) atomicAdd(&P.out[i * (P.ld ? P.ld : J) + P.col0 + jq * JW + k], acc[k]);
         if (jq == 0 && P.bias) atomicAdd(&P.bias[i], bacc);
     }
 }
@@ -661,7 +666,7 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     __syncthreads();
     for (int e = threadIdx.x; e < NIT * 32 * NJT * 32; e += 256) {
         const int i = e / (NJT * 32), j = e - i * (NJT * 32);
-        if (i < H && j < J) atomicAdd(&P.out[i * J + j], red[e]);
+        if (i < H && j < J) atomicAdd(&P.out[i * (P.ld ? P.ld : J) + P.col0 + j], red[e]);
     }
     if (P.bias && threadIdx.x < H) atomicAdd(&P.bias[threadIdx.x], bred[threadIdx.x]);
 }
@@ -689,47 +694,67 @@ struct VecT {
     int64_t E, R;
 };
 
-__global__ __launch_bounds__(256) void train_vec_kernel(VecT P) {
-    extern __shared__ float acc[];  // mode 0: [T][H]; else [4 waves][2][H]
-    const int wave = threadIdx.x >> 6, u = threadIdx.x & 63, H = P.H;
-    const int nacc = P.mode == 0 ? P.T * H : 4 * 2 * H;
-    for (int e = threadIdx.x; e < nacc; e += 256) acc[e] = 0.0f;
-    __syncthreads();
+// The same three reductions in two coalesced passes: first over the frames, per (message, unit)
+// -- consecutive threads read consecutive words of each frame's (E, H) slab --, then over the
+// messages into the gradient (a row walk with a per-type LDS accumulation ran at ~0.8 TB/s).
+__global__ void train_colsum_kernel(VecT P, float *__restrict__ S0, float *__restrict__ S1) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t EH = P.E * P.H;
+    if (t >= EH) return;
+    const int64_t m = t / P.H;
+    const int64_t B = P.R / P.E;
     float s0 = 0.0f, s1 = 0.0f;
-    if (u < H) {
-        for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < P.R; r += (int64_t)gridDim.x * 4) {
-            const int64_t b = r / P.E, m = r - b * P.E;
-            const float v = P.src[r * H + u];
-            if (P.mode == 0) {
-                atomicAdd(&acc[P.msg_type[m] * H + u], v);
-            } else if (P.mode == 1) {
-                s0 = fmaf(v, P.llr[b * P.N + P.msg_var[m]], s0);
-                s1 += v;
-            } else {
-                const float d = P.dz[b * P.N + P.msg_var[m]];
-                s0 = fmaf(d, v, s0);
-                s1 += d;
-            }
-        }
-        if (P.mode != 0) {
-            acc[(wave * 2) * H + u] = s0;
-            acc[(wave * 2 + 1) * H + u] = s1;
+    const int var = P.mode != 0 ? P.msg_var[m] : 0;
+    for (int64_t b = 0; b < B; ++b) {
+        const float v = P.src[b * EH + t];
+        if (P.mode == 0) {
+            s0 += v;
+        } else if (P.mode == 1) {
+            s0 = fmaf(v, P.llr[b * P.N + var], s0);
+            s1 += v;
+        } else {
+            const float d = P.dz[b * P.N + var];
+            s0 = fmaf(d, v, s0);
+            s1 += d;
         }
     }
-    __syncthreads();
-    if (P.mode == 0) {
-        for (int e = threadIdx.x; e < nacc; e += 256) atomicAdd(&P.g0[e], acc[e]);
-    } else if (threadIdx.x < H) {
-        const int k = threadIdx.x;
-        const float t0 = ((acc[k] + acc[2 * H + k]) + acc[4 * H + k]) + acc[6 * H + k];
-        const float t1 = ((acc[H + k] + acc[3 * H + k]) + acc[5 * H + k]) + acc[7 * H + k];
-        atomicAdd(&P.g0[k], t0);
-        if (P.mode == 1) atomicAdd(&P.g1[k], t1);
-        else if (k == 0) {  // dbo: every lane summed the same dz; take lane 0's
-            atomicAdd(&P.g1[0], t1);
+    S0[t] = s0;
+    if (P.mode != 0) S1[t] = s1;
+}
+
+__global__ void train_vecfinal_kernel(VecT P, const float *__restrict__ S0, const float *__restrict__ S1, int chunk) {
+    const int u = threadIdx.x;
+    if (u >= P.H) return;
+    const int64_t m0 = (int64_t)blockIdx.x * chunk, m1 = min<int64_t>(m0 + chunk, P.E);
+    float a0 = 0.0f, a1 = 0.0f;
+    for (int64_t m = m0; m < m1; ++m) {
+        const float v = S0[m * P.H + u];
+        if (P.mode == 0) {
+            atomicAdd(&P.g0[P.msg_type[m] * P.H + u], v);
+        } else {
+            a0 += v;
+            a1 += S1[m * P.H + u];
         }
+    }
+    if (P.mode == 1) {
+        atomicAdd(&P.g0[u], a0);
+        atomicAdd(&P.g1[u], a1);
+    } else if (P.mode == 2) {
+        atomicAdd(&P.g0[u], a0);
+        if (u == 0) atomicAdd(&P.g1[0], a1);  // dbo: S1 is the same for every unit
     }
 }
+
+int launch_vec(const VecT &v, float *S0, float *S1, hipStream_t s) {
+    const int64_t EH = v.E * v.H;
+    hipLaunchKernelGGL(train_colsum_kernel, dim3((unsigned)((EH + 255) / 256)), dim3(256), 0, s, v, S0, S1);
+    const int chunk = 16;
+    hipLaunchKernelGGL(train_vecfinal_kernel, dim3((unsigned)((v.E + chunk - 1) / chunk)), dim3(64), 0, s, v, S0, S1,
+                       chunk);
+    LDPC_CHECK_LAUNCH("train_vec_kernel");
+    return LDPC_OK;
+}
+
 
 struct TrainWs {
     float *Mv, *Mc, *dz, *dX, *dXp, *cbuf, *hv, *hc, *dhv, *dhc, *dco, *da, *db, *Mda, *Mdb;
@@ -851,8 +876,7 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         v.g0 = GL[9];
         v.g1 = GL[10];
         v.H = H; v.T = T; v.N = N; v.mode = 2; v.E = E; v.R = R;
-        hipLaunchKernelGGL(train_vec_kernel, dim3(red_grid), dim3(256), (size_t)8 * H * 4, s, v);
-        LDPC_CHECK_LAUNCH("train_vec_kernel");
+        if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
     }
     for (int l = L - 1; l >= 0; --l) {
         const float *W[11];
@@ -908,21 +932,37 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         if (int rc = launch_outer(o, red_grid, s)) return rc;
         o.zsrc = w.hc; o.out = Gw[7]; o.bias = Gw[8];
         if (int rc = launch_outer(o, red_grid, s)) return rc;
-        o.A = w.dhv; o.zsrc = w.cbuf; o.J = 2 * H; o.G = w.Mv; o.grp = p->vgroup; o.Gn = p->Gv;
-        o.out = Gw[1]; o.bias = Gw[2];
-        if (int rc = launch_outer(o, red_grid, s)) return rc;
-        o.A = w.dhc; o.G = w.Mc; o.grp = p->cgroup; o.Gn = p->Gc; o.out = Gw[5]; o.bias = Gw[6];
-        if (int rc = launch_outer(o, red_grid, s)) return rc;
+        // dW1_s = sum_m dh_s[m] (x) [c_m; g_s(group(m))]: the c half row by row; the group half as
+        // sum_groups (sum_{m in group} dh_s[m]) (x) g_s(group) -- contiguous group rows instead of
+        // a gathered group row per message (Mda / Mdb are free again after the combine step)
+        for (int side = 0; side < 2; ++side) {
+            const float *dh = side ? w.dhc : w.dhv, *Gs = side ? w.Mc : w.Mv;
+            float *dhsum = side ? w.Mdb : w.Mda, *gw = side ? Gw[5] : Gw[1], *gb = side ? Gw[6] : Gw[2];
+            const int Gn = side ? p->Gc : p->Gv;
+            OuterT c{};
+            c.H = H; c.E = E; c.R = R; c.A = dh; c.zsrc = w.cbuf; c.J = H; c.ld = 2 * H; c.col0 = 0;
+            c.out = gw; c.bias = gb;
+            if (int rc = launch_outer(c, red_grid, s)) return rc;
+            GmT gs{};
+            gs.src = dh; gs.src_mode = 0; gs.sum_only = 1; gs.H = H; gs.N = N; gs.E = E; gs.B = B;
+            gs.ptr = side ? p->cg_ptr : p->vg_ptr; gs.mem = side ? p->cg_mem : p->vg_mem;
+            gs.inv = side ? p->inv_c : p->inv_v; gs.G = Gn; gs.dst = dhsum;
+            if (int rc = launch_group_mean(gs, s)) return rc;
+            OuterT g{};
+            g.H = H; g.E = (int64_t)Gn; g.R = B * Gn; g.A = dhsum; g.zsrc = Gs; g.J = H; g.ld = 2 * H; g.col0 = H;
+            g.out = gw; g.bias = nullptr;
+            const unsigned ggrid = (unsigned)std::min<int64_t>((g.R + 63) / 64, (int64_t)g_cus_t * 4);
+            if (int rc = launch_outer(g, ggrid, s)) return rc;
+        }
         VecT v{};
         v.src = w.dco; v.llr = d_llr; v.msg_type = d_msg_type; v.msg_var = d_msg_var;
         v.H = H; v.T = T; v.N = N; v.E = E; v.R = R;
         v.mode = 0; v.g0 = Gw[0];
-        hipLaunchKernelGGL(train_vec_kernel, dim3(red_grid), dim3(256), (size_t)std::max(T * H, 8 * H) * 4, s, v);
+        if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
         if (l == 0) {
             v.mode = 1; v.g0 = d_grad_weights; v.g1 = d_grad_weights + H;
-            hipLaunchKernelGGL(train_vec_kernel, dim3(red_grid), dim3(256), (size_t)8 * H * 4, s, v);
+            if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
         }
-        LDPC_CHECK_LAUNCH("train_vec_kernel");
         std::swap(w.dX, w.dXp);
     }
     return LDPC_OK;
