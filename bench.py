@@ -61,19 +61,30 @@ def flood_bytes_per_cw(E, N, iters):
     return iters * 8 * (E + N) + 5 * N
 
 
-def roofline_notes(kind, B, n, kern_ms, traffic):
+def roofline_notes(kind, B, n, kern_ms, traffic, pmc=None, pmc_path=None):
     """The flood decoder keeps every message in LDS, so SURVEY §8(d)'s streaming byte model
-    (algorithmic bytes) overstates what reaches HBM; report the compulsory bytes beside it."""
+    (algorithmic bytes) overstates what reaches HBM; report the compulsory bytes beside it, and
+    the VALU issue utilisation from the PMC pass (the kernel's real bound): a wave64 VALU
+    instruction holds its SIMD for 4 cycles, 1024 SIMDs, cycles = GRBM_GUI_ACTIVE / 8 XCDs."""
     if kind not in ("minsum", "bp"):
         return None
     comp = 5 * n * B  # LLR read (4N) + uint8 decision written (N)
-    return {"model": "SURVEY 8(d) algorithmic bytes = messages streamed through HBM every iteration; "
-                     "this decoder is LDS-resident, hence frac > 1",
-            "compulsory_bytes_per_launch": comp,
-            "compulsory_GBps": comp / (kern_ms * 1e-3) / 1e9,
-            "compulsory_frac_of_hbm_peak": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "traffic_over_compulsory": (traffic / comp) if traffic else None,
-            "actual_bound": "LDS latency + VALU issue, two barriers per iteration (profiles/r01s2_pmc_minsum_z32.json)"}
+    out = {"model": "SURVEY 8(d) algorithmic bytes = messages streamed through HBM every iteration; "
+                    "this decoder is LDS-resident, hence frac > 1",
+           "compulsory_bytes_per_launch": comp,
+           "compulsory_GBps": comp / (kern_ms * 1e-3) / 1e9,
+           "compulsory_frac_of_hbm_peak": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "traffic_over_compulsory": (traffic / comp) if traffic else None,
+           "actual_bound": "VALU issue (the reference's exact float32 order: quadratic var-node adds), "
+                           "then LDS latency and two barriers per iteration"}
+    c = (pmc or {}).get("counters_per_launch", {})
+    if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
+        cycles = c["GRBM_GUI_ACTIVE"] / 8
+        out["valu_busy_frac"] = c["SQ_INSTS_VALU"] * 4 / (1024 * cycles)
+        if c.get("SQ_INSTS_LDS"):
+            out["lds_insts_per_cycle_per_cu"] = c["SQ_INSTS_LDS"] / (256 * cycles)
+        out["pmc_source"] = os.path.relpath(pmc_path, ROOT) if pmc_path else None
+    return out
 
 
 def parse():
@@ -361,10 +372,11 @@ def main():
         traffic = None
         tj = a.traffic_json
         if tj is None:  # the newest PMC summary of this workload (profiles/<round>_pmc_<workload>.json)
-            for tag in ("r01s3", "r01s2"):
+            for tag in ("r01s4", "r01s3", "r01s2"):
                 tj = os.path.join(ROOT, "profiles", f"{tag}_pmc_{a.workload.replace('-', '_')}.json")
                 if os.path.exists(tj):
                     break
+        tjd = None
         if os.path.exists(tj):
             tjd = json.load(open(tj))
             # the PMC pass ran the same workload at the default batch; scale per launch to this B
@@ -399,7 +411,7 @@ def main():
                          "unit": unit, "frac": achieved / peak, "traffic": traffic,
                          "kernel_ms": kern_ms,
                          "algorithmic_per_launch": per_launch_alg},
-            "roofline_notes": roofline_notes(kind, B, n, kern_ms, traffic),
+            "roofline_notes": roofline_notes(kind, B, n, kern_ms, traffic, tjd, tj),
             "avg_layers": avg_layers,
             "cpu_baseline": cpu,
         }
