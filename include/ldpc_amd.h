@@ -186,7 +186,8 @@ int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
  * ldpc_gather_minsum   CheckLayer.forward (layers.py:14-66): out = prod sign(v + 1e-10) * min |v|
  *                      (|0| -> 1e10); d_argmin (B, n_out) int32 (optional) keeps torch.min's index.
  * ldpc_gather_sum      VariableLayer.forward (layers.py:78-125): out = llr + sum of gathered msgs
- *                      (d_llr NULL: out = the sum alone).
+ *                      (d_llr NULL: out = the sum alone).  A row ends at its first -1: put the
+ *                      padding last (for a sum, padding anywhere adds an exact +0.0).
  * ldpc_residual        ResidualLayer.forward (layers.py:143-168), h_prev = host array of `depth`
  *                      device pointers (depth <= 8).
  * ldpc_output_layer    OutputLayer.forward (layers.py:180-208): soft = sigmoid(final + llr); with

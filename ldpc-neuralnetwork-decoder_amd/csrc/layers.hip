@@ -93,6 +93,7 @@ __global__ __launch_bounds__(512) void gather_lds_kernel(const float *__restrict
         for (int f = 0; f < FPW; ++f) { acc[f] = MINSUM ? 1.0f : 0.0f; m[f] = 0.0f; am[f] = 0; }
         for (int k = 0; k < K; ++k) {
             const int j = idx[(int64_t)k * n_out + i];
+            if (!MINSUM && j < 0) break;  // sum rows end at their first padding entry
 #pragma unroll
             for (int f = 0; f < FPW; ++f) {
                 if (f >= nb) break;
@@ -180,7 +181,9 @@ __global__ void gather_minsum_bwd_kernel(const float *__restrict__ g, const floa
     if (d != 0.0f) atomicAdd(&gin[b * n_in + j], d);
 }
 
-// VariableLayer (layers.py:78-125): out[b][i] = llr[b][i] + sum_k msgs[b][idx[i][k]] (0 for -1)
+// VariableLayer (layers.py:78-125): out[b][i] = llr[b][i] + sum_k msgs[b][idx[i][k]] (0 for -1).
+// Padding adds +0.0 to a sum that starts at +0.0 and so is never -0.0: an exact identity.  The
+// Python layer therefore moves each row's padding to its end, and the loop stops at the first -1.
 __global__ void gather_sum_kernel(const float *__restrict__ llr, const float *__restrict__ msgs, int64_t B, int n_in,
                                   const int32_t *__restrict__ idx, int n_out, int K, float *__restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -194,10 +197,11 @@ __global__ void gather_sum_kernel(const float *__restrict__ llr, const float *__
     for (int f = 0; f < kFB; ++f) s[f] = 0.0f;
     for (int k = 0; k < K; ++k) {
         const int j = idx[(int64_t)k * n_out + i];
+        if (j < 0) break;  // a row ends at its first padding entry (see ldpc_gather_sum)
 #pragma unroll
         for (int f = 0; f < kFB; ++f) {
             if (f >= nb) break;
-            s[f] += j < 0 ? 0.0f : msgs[(b0 + f) * n_in + j];
+            s[f] += msgs[(b0 + f) * n_in + j];
         }
     }
 #pragma unroll
@@ -217,7 +221,8 @@ __global__ void gather_sum_bwd_kernel(const float *__restrict__ g, int64_t B, in
     const float d = g[t];
     for (int k = 0; k < K; ++k) {
         const int j = idx[(int64_t)k * n_out + i];
-        if (j >= 0) atomicAdd(&gmsgs[b * n_in + j], d);
+        if (j < 0) break;
+        atomicAdd(&gmsgs[b * n_in + j], d);
     }
 }
 
@@ -376,9 +381,15 @@ extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t 
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
     if (!d_msgs || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
-    // (the LDS-staged form is slower here: VariableLayer's index is padded to the largest
-    // variable degree -- K = 22 at BG2 -- and the global kernel spreads each index read over 4
-    // frames instead of 2)
+    // the LDS-staged form is opt-in here (LDPC_GATHER_SUM_LDS=1): measured 12 % slower at BG2 Z=32,
+    // the index (K = 22, rows ending early) is then read once per 2 frames instead of 4
+    static const bool sum_lds = [] {
+        const char *e = std::getenv("LDPC_GATHER_SUM_LDS");
+        return e && std::atoi(e) != 0;
+    }();
+    if (const int fpw = sum_lds ? gather_fpw(n_in) : 0)
+        return launch_gather_lds<false>(fpw, d_msgs, d_llr, B, n_in, d_idx, n_out, K, d_out, nullptr,
+                                        static_cast<hipStream_t>(stream));
     hipLaunchKernelGGL(gather_sum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_llr,
                        d_msgs, B, n_in, d_idx, n_out, K, d_out);

@@ -99,7 +99,7 @@ class LDPCNeuralDecoder(nn.Module):
         if E != self.num_nodes:
             raise RuntimeError(f"index tensors describe {E} LLR indices, decoder built for {self.num_nodes}")
         cidx = _check_index(check_index_tensor, E, dev)
-        vidx = _check_index(var_index_tensor, E, dev)
+        vidx = _check_index(var_index_tensor, E, dev, compact=True)
         x0 = gather_sum(llr, x0_idx)
         v, prevs = x0, []
         for res in self.residual_layers:

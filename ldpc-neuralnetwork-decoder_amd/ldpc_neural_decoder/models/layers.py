@@ -20,13 +20,15 @@ def _dev_f32(t, dev):
 _PREPARED = {}  # (tensor identity, version, n_in, device) -> (K, n_out) int32 device index
 
 
-def _check_index(idx, n_in, dev):
+def _check_index(idx, n_in, dev, compact=False):
     """The reference gathers from (B, n_in + 1) after mapping -1 to the zero column n_in: any
     other index outside [0, n_in] is torch.gather's out-of-bounds RuntimeError.  Returns the
     kernels' layout -- transposed (K, n_out) int32, -1 for padding -- built and validated once
-    per index tensor (the decoders call every layer with the same index tensors)."""
+    per index tensor (the decoders call every layer with the same index tensors).  compact (for
+    the sums): each row's padding moved to its end, order of the real entries kept, K cut to the
+    longest row -- padding adds an exact +0.0, and the sum kernels stop at the first -1."""
     idx = torch.as_tensor(idx)
-    key = (id(idx), idx.data_ptr(), idx._version, tuple(idx.shape), n_in, str(dev))
+    key = (id(idx), idx.data_ptr(), idx._version, tuple(idx.shape), n_in, str(dev), compact)
     hit = _PREPARED.get(key)
     if hit is not None and hit[0] is idx:
         return hit[1]
@@ -36,7 +38,13 @@ def _check_index(idx, n_in, dev):
         raise RuntimeError("gather(): Expected dtype int64 for index")
     if idx.numel() and (int(idx.max()) > n_in or int(idx.min()) < -1):
         raise RuntimeError(f"index out of bounds for a dimension of size {n_in + 1}")
-    prepared = torch.where(idx == n_in, torch.full_like(idx, -1), idx).to(torch.int32).t().contiguous().to(dev)
+    prepared = torch.where(idx == n_in, torch.full_like(idx, -1), idx)
+    if compact and prepared.numel():
+        order = torch.argsort((prepared < 0).to(torch.int8), dim=1, stable=True)
+        prepared = torch.gather(prepared, 1, order)
+        keep = max(int((prepared >= 0).sum(dim=1).max()), 1)
+        prepared = prepared[:, :keep]
+    prepared = prepared.to(torch.int32).t().contiguous().to(dev)
     if len(_PREPARED) > 16:
         _PREPARED.clear()
     _PREPARED[key] = (idx, prepared)
@@ -208,7 +216,7 @@ class VariableLayer(nn.Module):
     def forward(self, input_llr, check_messages, var_index_tensor):
         home, dev = _home_and_dev(check_messages)
         msgs = _dev_f32(check_messages, dev)
-        idx = _check_index(var_index_tensor, msgs.shape[1], dev)
+        idx = _check_index(var_index_tensor, msgs.shape[1], dev, compact=True)
         llr = _dev_f32(input_llr, dev)
         if llr.shape != (msgs.shape[0], idx.shape[1]):
             raise RuntimeError(f"input_llr of shape {tuple(llr.shape)} does not match the summed messages "
