@@ -175,3 +175,18 @@ def test_cli_train_evaluate_compare_visualize(cuda, tmp_path, model_type):
     cli.main(["--mode", "visualize"] + common)
     for f in ("training_loss.png", "ber_vs_snr.png", "fer_vs_snr.png", "ber_comparison.png", "performance.png"):
         assert os.path.exists(tmp_path / "r" / f), f
+
+
+def test_cli_default_example_code(cuda, tmp_path):
+    """The reference CLI's default code is the 3x4 example H (main.py:93-98): E = 7 edges, a
+    degree-1 variable, rows of unequal degree -- the smallest graph the layer kernels see."""
+    from ldpc_neural_decoder import main as cli
+    common = ["--num_iterations", "3", "--batch_size", "8", "--snr_min", "0", "--snr_max", "2", "--snr_step", "2",
+              "--num_trials", "2", "--model_path", str(tmp_path / "model.pt"), "--results_dir", str(tmp_path / "r"),
+              "--device", "cuda"]
+    trainer = cli.main(["--mode", "train", "--num_epochs", "2"] + common)
+    assert len(trainer.train_losses) == 2 and all(np.isfinite(trainer.train_losses))
+    res = cli.main(["--mode", "evaluate"] + common)
+    assert res["snr_range"] == [0, 2] and all(0 <= x <= 1 for x in res["ber_results"] + res["fer_results"])
+    cmp_ = cli.main(["--mode", "compare", "--compare_with_traditional"] + common)
+    assert set(cmp_) == {"snr_range", "belief_propagation", "min_sum_scaled", "neural_decoder"}
