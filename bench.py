@@ -44,6 +44,7 @@ WORKLOADS = {
     # name: (decoder, Z, iterations, default batch per GPU, SNR dB)
     "minsum-z32": ("minsum", 32, 10, 65536, 2.0),
     "bp-z4": ("bp", 4, 5, 64, 2.0),
+    "bp-z32": ("bp", 32, 10, 65536, 2.0),
     "gnn-z4": ("gnn", 4, 5, 4096, 2.0),
     "gnn-z32": ("gnn", 32, 10, 32768, 2.0),
     "gnn-z32-bf16": ("gnn-bf16", 32, 15, 32768, 2.0),

@@ -18,8 +18,8 @@
 // v2c_i = (((llr + c_0) + c_1) ...) over i' != i in ascending check order; we compute it as the
 // prefix P_i followed by the same tail adds, i.e. the identical operation sequence.  Min-sum's
 // sign/min is order-free.  BP's exclusive product is prefix-then-tail as well; tanh/atanh are
-// evaluated in double and rounded (the reference uses torch-CPU SLEEF float versions, which are
-// not correctly rounded, so BP parity is "within float32 tolerance", not bitwise).
+// float32 library calls (the reference uses torch-CPU SLEEF float versions; neither is correctly
+// rounded, so BP parity is "within float32 tolerance", not bitwise).
 // Compile with -ffp-contract=off: no a*b+c may fuse on this path.
 #include <cmath>
 #include <cstdint>
@@ -146,8 +146,10 @@ struct MinSumFast {
     }
 };
 
-__device__ __forceinline__ float tanh_half(float v) { return (float)tanh((double)(v / 2.0f)); }
-__device__ __forceinline__ float two_atanh(float p) { return 2.0f * (float)atanh((double)p); }
+// float32 library tanhf / atanhf (ROCm device libm, a few ulp), like the reference's float32 SLEEF
+// calls; evaluating them in double and rounding once cost 16x the min-sum time per edge.
+__device__ __forceinline__ float tanh_half(float v) { return tanhf(v / 2.0f); }
+__device__ __forceinline__ float two_atanh(float p) { return 2.0f * atanhf(p); }
 
 struct Ctx {
     FloodTables T;

@@ -12,8 +12,11 @@
 // Kernels per layer (no E x E matrix anywhere):
 //   gnn_group_mean_kernel   one wave per (frame, group): mean of c over the group's messages,
 //                           H lanes, 256-B coalesced rows.  Layer 0 builds c from the LLRs.
-//   gnn_mlp_mfma_kernel     H = 64.  Persistent, one 256-thread workgroup per CU holding the
-//                           layer's four weight matrices (96 KB fp32) in LDS; every wave owns a
+//                           H = 64 runs gnn_group_mean_tile_kernel instead: one wave per 8 groups
+//                           of one degree (the plan's group tiles), 8 lanes x 32 B per row.
+//   gnn_mlp_mfma_kernel     H = 64.  Persistent, one 512-thread workgroup per CU holding the
+//                           layer's four weight matrices (100 KB fp32, rows padded so one
+//                           ds_read_b128 feeds four MFMA k-steps) in LDS; every wave owns a
 //                           32-message tile and runs the four GEMMs on v_mfma_f32_32x32x2_f32 in
 //                           the transposed orientation (hidden units on the MFMA rows, messages
 //                           on the lanes), so GEMM1's accumulator IS GEMM2's B operand with no
@@ -42,6 +45,14 @@ int mlp_threads() {
     static int t = [] {
         const char *e = std::getenv("LDPC_GNN_MLP_THREADS");
         return (e && std::atoi(e) == 256) ? 256 : 512;
+    }();
+    return t;
+}
+// LDPC_GNN_GM=0 selects the per-group fp32 group-mean kernel (A/B runs); default: group tiles
+bool gm_tiles() {
+    static bool t = [] {
+        const char *e = std::getenv("LDPC_GNN_GM");
+        return !(e && std::atoi(e) == 0);
     }();
     return t;
 }
@@ -146,10 +157,74 @@ __global__ __launch_bounds__(256) void gnn_group_mean_h64_kernel(GnnLayer P) {
     *dst = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
 }
 
+// H = 64 fp32 on the plan's group tiles (gnn.hpp): one wave sums 8 groups of ONE degree, so no
+// lane idles behind a longer group of its wave; 8 lanes x 32 B per 256-B row, members unrolled
+// by 4 (8 x 16 B of features in flight per lane).  Same per-message sum order as above
+// (ascending members, x + emb first), so the rows are bit-identical.
+struct GtTiles {
+    const int2 *meta;
+    const int32_t *grp, *mem;
+    int n_tiles;
+};
+
+__global__ __launch_bounds__(256) void gnn_group_mean_tile_kernel(GnnLayer P, GtTiles G) {
+    const uint32_t w = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    const uint32_t nt = (uint32_t)G.n_tiles;
+    if (w >= (uint32_t)P.B * nt) return;
+    const uint32_t b = w / nt, t = w - b * nt;
+    const int lane = threadIdx.x & 63, q = lane >> 3, p0 = 8 * (lane & 7);
+    const int2 md = G.meta[t];
+    const int g = G.grp[8 * t + q];
+    const int32_t *mem = G.mem + md.y + q;
+    float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), a1 = a0;
+    auto add = [](float4 &acc, float4 x, float4 e) {
+        acc.x += x.x + e.x; acc.y += x.y + e.y; acc.z += x.z + e.z; acc.w += x.w + e.w;
+    };
+    const float4 *emb = reinterpret_cast<const float4 *>(P.emb + p0);
+    if (P.x_in) {
+        const float4 *xb = reinterpret_cast<const float4 *>(P.x_in + (int64_t)b * P.E * 64 + p0);
+        int i = 0;
+        for (; i + 4 <= md.x; i += 4) {
+            const int m0 = mem[8 * i], m1 = mem[8 * i + 8], m2 = mem[8 * i + 16], m3 = mem[8 * i + 24];
+            const float4 x00 = xb[m0 * 16], x01 = xb[m0 * 16 + 1], x10 = xb[m1 * 16], x11 = xb[m1 * 16 + 1];
+            const float4 x20 = xb[m2 * 16], x21 = xb[m2 * 16 + 1], x30 = xb[m3 * 16], x31 = xb[m3 * 16 + 1];
+            const int t0 = P.msg_type[m0] * 16, t1 = P.msg_type[m1] * 16;
+            const int t2 = P.msg_type[m2] * 16, t3 = P.msg_type[m3] * 16;
+            add(a0, x00, emb[t0]); add(a1, x01, emb[t0 + 1]);
+            add(a0, x10, emb[t1]); add(a1, x11, emb[t1 + 1]);
+            add(a0, x20, emb[t2]); add(a1, x21, emb[t2 + 1]);
+            add(a0, x30, emb[t3]); add(a1, x31, emb[t3 + 1]);
+        }
+        for (; i < md.x; ++i) {
+            const int m = mem[8 * i], tt = P.msg_type[m] * 16;
+            add(a0, xb[m * 16], emb[tt]); add(a1, xb[m * 16 + 1], emb[tt + 1]);
+        }
+    } else {
+        const float4 w0 = reinterpret_cast<const float4 *>(P.w_in + p0)[0], w1 = reinterpret_cast<const float4 *>(P.w_in + p0)[1];
+        const float4 c0 = reinterpret_cast<const float4 *>(P.b_in + p0)[0], c1 = reinterpret_cast<const float4 *>(P.b_in + p0)[1];
+        for (int i = 0; i < md.x; ++i) {
+            const int m = mem[8 * i], tt = P.msg_type[m] * 16;
+            const float l = P.llr[(int64_t)b * P.N + P.msg_var[m]];
+            add(a0, make_float4(l * w0.x + c0.x, l * w0.y + c0.y, l * w0.z + c0.z, l * w0.w + c0.w), emb[tt]);
+            add(a1, make_float4(l * w1.x + c1.x, l * w1.y + c1.y, l * w1.z + c1.z, l * w1.w + c1.w), emb[tt + 1]);
+        }
+    }
+    if (g < 0) return;
+    const bool isv = g < P.Gv;
+    const int gg = isv ? g : g - P.Gv;
+    const float inv = isv ? P.inv_v[gg] : P.inv_c[gg];
+    float4 *dst = reinterpret_cast<float4 *>((isv ? P.Mv + ((int64_t)b * P.Gv + gg) * 64 : P.Mc + ((int64_t)b * P.Gc + gg) * 64) + p0);
+    dst[0] = make_float4(a0.x * inv, a0.y * inv, a0.z * inv, a0.w * inv);
+    dst[1] = make_float4(a1.x * inv, a1.y * inv, a1.z * inv, a1.w * inv);
+}
+
 // ------------------------------------------------------------------------ fused MLP, H = 64
 // LDS image (floats): W1vT[128][64] W2vT[64][64] W1cT[128][64] W2cT[64][64]
 //                     b1v b2v b1c b2c wo [64 each]  emb[T][64]
-constexpr int kW1 = 128 * 64, kW2 = 64 * 64;
+// Weights are stored row-major per output unit, rows padded (132 / 68 floats: a 16-lane phase of
+// ds_read_b128 then hits 64 distinct banks), so one ds_read_b128 feeds four MFMA k-steps.
+constexpr int kS1 = 132, kS2 = 68;
+constexpr int kW1 = 64 * kS1, kW2 = 64 * kS2;
 constexpr int kOffW1v = 0, kOffW2v = kW1, kOffW1c = kW1 + kW2, kOffW2c = 2 * kW1 + kW2;
 constexpr int kOffBias = 2 * kW1 + 2 * kW2;  // b1v, b2v, b1c, b2c, wo
 constexpr int kOffEmb = kOffBias + 5 * 64;
@@ -165,15 +240,15 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
     constexpr int H = kMfmaH;
     const int tid = threadIdx.x;
     // stage the layer's weights, transposed so lanes read consecutive output units
-    for (int i = tid; i < kW1; i += kMlpThreads) {
+    for (int i = tid; i < 128 * 64; i += kMlpThreads) {
         const int o = i / 128, k = i - o * 128;
-        lds[kOffW1v + k * 64 + o] = P.w1v[i];
-        lds[kOffW1c + k * 64 + o] = P.w1c[i];
+        lds[kOffW1v + o * kS1 + k] = P.w1v[i];
+        lds[kOffW1c + o * kS1 + k] = P.w1c[i];
     }
-    for (int i = tid; i < kW2; i += kMlpThreads) {
+    for (int i = tid; i < 64 * 64; i += kMlpThreads) {
         const int o = i / 64, k = i - o * 64;
-        lds[kOffW2v + k * 64 + o] = P.w2v[i];
-        lds[kOffW2c + k * 64 + o] = P.w2c[i];
+        lds[kOffW2v + o * kS2 + k] = P.w2v[i];
+        lds[kOffW2c + o * kS2 + k] = P.w2c[i];
     }
     if (tid < 64) {
         lds[kOffBias + tid] = P.b1v[tid];
@@ -228,7 +303,7 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
         }
         f32x16 y0 = {}, y1 = {};
         // per-lane weight offsets, made opaque so the loop-invariant LDS reads are not hoisted
-        int w1lane = half * 64 * 64 + j, w2lane = j;
+        int w1lane = j * kS1 + half * 64, w2lane = j * kS2 + 4 * half;
         asm volatile("" : "+v"(w1lane), "+v"(w2lane));
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
@@ -245,10 +320,15 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
             // GEMM1^T: h[u][msg] = sum_k W1[u][k] * in[k][msg], k = half*64 + kk
             f32x16 h0 = {}, h1 = {};
 #pragma unroll
-            for (int kk = 0; kk < 64; ++kk) {
-                const float *wr = W1 + w1lane + kk * 64;
-                h0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[0], in[kk], h0, 0, 0, 0);
-                h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32], in[kk], h1, 0, 0, 0);
+            for (int kk = 0; kk < 64; kk += 4) {
+                const float4 wa = *reinterpret_cast<const float4 *>(W1 + w1lane + kk);
+                const float4 wb = *reinterpret_cast<const float4 *>(W1 + w1lane + 32 * kS1 + kk);
+                const float a4[4] = {wa.x, wa.y, wa.z, wa.w}, b4[4] = {wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    h0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i], in[kk + i], h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b4[i], in[kk + i], h1, 0, 0, 0);
+                }
             }
             // bias + ReLU; register r of row tile rt holds unit 32*rt + crow(r, half)
 #pragma unroll
@@ -259,13 +339,23 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
             // GEMM2^T: y[o][msg] += sum_u W2[o][u] * h[u][msg]; step (rt, r) pairs unit
             // crow(r,0) (half 0) with crow(r,1) (half 1) -- exactly the registers each lane holds
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float *wa = W2 + w2lane + (crow(r, half)) * 64;
-                const float *wb = W2 + w2lane + (32 + crow(r, half)) * 64;
-                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[0], h0[r], y0, 0, 0, 0);
-                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[32], h0[r], y1, 0, 0, 0);
-                y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[0], h1[r], y0, 0, 0, 0);
-                y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[32], h1[r], y1, 0, 0, 0);
+            for (int rq = 0; rq < 4; ++rq) {
+                // registers 4 rq .. 4 rq + 3 hold units crow(4 rq + i, half) = 8 rq + 4 half + i
+                const float *w = W2 + w2lane + 8 * rq;
+                const float4 a0 = *reinterpret_cast<const float4 *>(w);                 // o = j,      u
+                const float4 a1 = *reinterpret_cast<const float4 *>(w + 32 * kS2);      // o = 32 + j, u
+                const float4 c0 = *reinterpret_cast<const float4 *>(w + 32);            // o = j,      32 + u
+                const float4 c1 = *reinterpret_cast<const float4 *>(w + 32 * kS2 + 32); // o = 32 + j, 32 + u
+                const float A0[4] = {a0.x, a0.y, a0.z, a0.w}, A1[4] = {a1.x, a1.y, a1.z, a1.w};
+                const float C0[4] = {c0.x, c0.y, c0.z, c0.w}, C1[4] = {c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 4 * rq + i;
+                    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[i], h0[r], y0, 0, 0, 0);
+                    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[i], h0[r], y1, 0, 0, 0);
+                    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(C0[i], h1[r], y0, 0, 0, 0);
+                    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(C1[i], h1[r], y1, 0, 0, 0);
+                }
             }
         }
         // epilogue: + b2v + b2c (+ residual); lane holds units 32*ot + crow(r, half) of message j
@@ -640,7 +730,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H : L.last ? nullptr : (l % 2 == 0) ? w.xa : w.xb;
         L.msg_out = w.msg_out;
         const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
-        if (H == 64)
+        if (H == 64 && gm_tiles()) {
+            const GtTiles G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles};
+            const int64_t twaves = B * (int64_t)p->n_gtiles;
+            hipLaunchKernelGGL(gnn_group_mean_tile_kernel, dim3((unsigned)((twaves + 3) / 4)), dim3(256), 0, s, L, G);
+        } else if (H == 64)
             hipLaunchKernelGGL(gnn_group_mean_h64_kernel, dim3((unsigned)((waves + 15) / 16)), dim3(256), 0, s, L);
         else
             hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);

@@ -9,6 +9,7 @@ run() {  # name, args...
 }
 run minsum-z32 --steps 20 --warmup 3
 run bp-z4 --workload bp-z4 --batch 65536 --steps 10 --warmup 3 --cpu-baseline-seconds 5
+run bp-z32 --workload bp-z32 --steps 10 --warmup 3 --cpu-baseline-seconds 5
 run gnn-z4 --workload gnn-z4 --steps 10 --warmup 3 --cpu-baseline-seconds 10
 run gnn-z4-bf16 --workload gnn-z4-bf16 --steps 10 --warmup 3 --cpu-baseline-seconds 0
 run gnn-z32 --workload gnn-z32 --steps 3 --warmup 1 --cpu-baseline-seconds 10
