@@ -48,6 +48,14 @@ int mlp_threads() {
     }();
     return t;
 }
+// LDPC_GNN_D1=0 keeps the Mv rows of degree-1 var groups (A/B runs)
+bool d1_skip() {
+    static bool t = [] {
+        const char *e = std::getenv("LDPC_GNN_D1");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return t;
+}
 // LDPC_GNN_GM=0 selects the per-group fp32 group-mean kernel (A/B runs); default: group tiles
 bool gm_tiles() {
     static bool t = [] {
@@ -79,6 +87,7 @@ struct GnnLayer {
     float *x_out;    // (B, E, H); null on the last layer unless training saves its features
     float *msg_out;  // (B, E) projected message LLRs, last layer only
     int residual, last;
+    int d1;          // degree-1 var groups have no Mv row: the MLP uses the message's own c as g
 };
 
 // feature u of message m of frame b *before* the type embedding
@@ -165,13 +174,14 @@ struct GtTiles {
     const int2 *meta;
     const int32_t *grp, *mem;
     int n_tiles;
+    int first;  // P.d1: the leading degree-1 var tiles are skipped (their mean is c itself)
 };
 
 __global__ __launch_bounds__(256) void gnn_group_mean_tile_kernel(GnnLayer P, GtTiles G) {
     const uint32_t w = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
-    const uint32_t nt = (uint32_t)G.n_tiles;
+    const uint32_t nt = (uint32_t)(G.n_tiles - G.first);
     if (w >= (uint32_t)P.B * nt) return;
-    const uint32_t b = w / nt, t = w - b * nt;
+    const uint32_t b = w / nt, t = w - b * nt + (uint32_t)G.first;
     const int lane = threadIdx.x & 63, q = lane >> 3, p0 = 8 * (lane & 7);
     const int2 md = G.meta[t];
     const int g = G.grp[8 * t + q];
@@ -274,7 +284,11 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
         // B operands: half 0 lanes carry c (k = 0..63), half 1 lanes carry a, then b (k = 64..127)
         float in[H];
         const float4 *grp = nullptr;  // half 1: the group-mean row of the current side
-        if (half == 0) {
+        // a degree-1 var group's mean is the message's own c (x + emb, times 1/1): half 1 builds
+        // it exactly as half 0 does, so the group-mean launch writes no row for it
+        const int vg = P.vgroup[m];
+        const bool self_g = P.d1 && half == 1 && P.vg_ptr[vg + 1] - P.vg_ptr[vg] == 1;
+        if (half == 0 || self_g) {
             const int ty = P.msg_type[m];
             const float *e = lds + kOffEmb + ty * kEmbStride;
             if (P.x_in) {
@@ -293,14 +307,14 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
                 for (int u = 0; u < H; ++u) in[u] = (l * P.w_in[u] + P.b_in[u]) + e[u];
             }
         } else {
-            grp = reinterpret_cast<const float4 *>(P.Mv + (b * P.Gv + P.vgroup[m]) * H);
+            grp = reinterpret_cast<const float4 *>(P.Mv + (b * P.Gv + vg) * H);
 #pragma unroll
             for (int q = 0; q < H / 4; ++q) {
                 const float4 v = grp[q];
                 in[4 * q + 0] = v.x; in[4 * q + 1] = v.y; in[4 * q + 2] = v.z; in[4 * q + 3] = v.w;
             }
-            grp = reinterpret_cast<const float4 *>(P.Mc + (b * P.Gc + P.cgroup[m]) * H);
         }
+        if (half == 1) grp = reinterpret_cast<const float4 *>(P.Mc + (b * P.Gc + P.cgroup[m]) * H);
         f32x16 y0 = {}, y1 = {};
         // per-lane weight offsets, made opaque so the loop-invariant LDS reads are not hoisted
         int w1lane = j * kS1 + half * 64, w2lane = j * kS2 + 4 * half;
@@ -730,9 +744,10 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H : L.last ? nullptr : (l % 2 == 0) ? w.xa : w.xb;
         L.msg_out = w.msg_out;
         const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
+        L.d1 = H == 64 && gm_tiles() && d1_skip();
         if (H == 64 && gm_tiles()) {
-            const GtTiles G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles};
-            const int64_t twaves = B * (int64_t)p->n_gtiles;
+            const GtTiles G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles, L.d1 ? p->n_gtiles_v1 : 0};
+            const int64_t twaves = B * (int64_t)(G.n_tiles - G.first);
             hipLaunchKernelGGL(gnn_group_mean_tile_kernel, dim3((unsigned)((twaves + 3) / 4)), dim3(256), 0, s, L, G);
         } else if (H == 64)
             hipLaunchKernelGGL(gnn_group_mean_h64_kernel, dim3((unsigned)((waves + 15) / 16)), dim3(256), 0, s, L);

@@ -5,8 +5,8 @@ R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/gm_ab; mkdir -p $OUT
 cd $R
 timeout -k 10 300 python -u -m pytest tests/test_gnn_gpu.py tests/test_train_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -20 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
-for V in 0 1; do
-  LDPC_GNN_GM=$V timeout -k 10 200 python3 bench.py --workload gnn-z32 --steps 5 --warmup 2 --batch ${BATCH:-8192} --cpu-baseline-seconds 0 > $OUT/v$V.json 2> $OUT/v$V.err || { echo "bench rc=$? v$V"; exit 1; }
+for V in ${VARIANTS:-0 1}; do
+  env "${KNOB:-LDPC_GNN_GM}=$V" timeout -k 10 200 python3 bench.py --workload gnn-z32 --steps 5 --warmup 2 --batch ${BATCH:-8192} --cpu-baseline-seconds 0 > $OUT/v$V.json 2> $OUT/v$V.err || { echo "bench rc=$? v$V"; exit 1; }
   python3 -c "import json; d=json.load(open('$OUT/v$V.json')); print('v$V', round(d['value']), 'cw/s', round(d['roofline']['kernel_ms'],2), 'ms frac', round(d['roofline']['frac'],3))"
 done
 cd /tmp && export TMPDIR=/tmp
