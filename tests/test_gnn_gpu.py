@@ -126,3 +126,43 @@ def test_bf16_path_within_tolerance(cuda, oracle_mod, z, layers):
     agree = ((p > 0.5) == (ref > 0.5))[sure].mean()
     print(f"bf16 z={z}: mean {d.mean():.2e} max {d.max():.2e} agree {agree:.5f}")
     assert d.mean() <= 5e-3 and d.max() <= 0.1 and agree >= 0.995
+
+
+_KNOB_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from ldpc_neural_decoder.models import create_message_gnn_decoder
+from ldpc_neural_decoder.utils import expand_base_matrix, load_base_matrix
+d = torch.load(sys.argv[2], weights_only=True)
+base = load_base_matrix(d["code"]); H = expand_base_matrix(base, 32)
+dec, conv = create_message_gnn_decoder(H, num_iterations=3, hidden_dim=64, base_graph=base, Z=32)
+dec.load_state_dict(d["sd"]); dec = dec.to("cuda")
+p = dec(d["llr"].cuda(), conv.message_to_var_index(), conv.get_message_types(base, 32),
+        conv.var_to_check_adjacency, conv.check_to_var_adjacency)
+torch.save(p.detach().cpu(), sys.argv[3])
+"""
+
+
+def test_fp32_group_mean_variants_bit_identical(cuda, tmp_path):
+    """The group-tile group-mean kernel and the degree-1 skip (defaults) give the same probs,
+    bit for bit, as the per-group kernel with every Mv row written (LDPC_GNN_GM=0 LDPC_GNN_D1=0).
+    The knobs are read once per process, so the reference run is a child process."""
+    import os
+    import subprocess
+    import sys
+    base = load_base_matrix(code_path(32))
+    H = expand_base_matrix(base, 32)
+    torch.manual_seed(3)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=3, hidden_dim=64, base_graph=base, Z=32)
+    llr = torch.randn(37, H.shape[1]) * 3.0 + 2.0
+    torch.save({"code": code_path(32), "sd": dec.state_dict(), "llr": llr}, tmp_path / "in.pt")
+    dec = dec.to(cuda)
+    p = dec(llr.to(cuda), conv.message_to_var_index(), conv.get_message_types(base, 32),
+            conv.var_to_check_adjacency, conv.check_to_var_adjacency).detach().cpu()
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(
+        sys.modules["ldpc_neural_decoder"].__file__)))
+    env = dict(os.environ, LDPC_GNN_GM="0", LDPC_GNN_D1="0")
+    subprocess.run([sys.executable, "-c", _KNOB_SCRIPT, pkg, str(tmp_path / "in.pt"),
+                    str(tmp_path / "out.pt")], env=env, check=True, timeout=180)
+    q = torch.load(tmp_path / "out.pt", weights_only=True)
+    assert torch.equal(p, q)
