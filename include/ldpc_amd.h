@@ -195,6 +195,12 @@ int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
  * The *_backward entry points write torch autograd's input gradients of the same functions. */
 int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const int32_t *d_idx, int n_out, int K,
                        float *d_out, int32_t *d_argmin, void *stream);
+/* ldpc_check_groups_minsum: the same CheckLayer outputs (no argmin) when the index is a set of
+ * checks -- every edge's row holds exactly the other edges of its check (n_in == n_out == n), as
+ * create_LLR_mapping builds it.  d_gptr (G + 1) / d_gmem (n) list each check's edges; K is the
+ * index's row length (padding K > degree - 1 contributes the 1e10 of a zero entry). */
+int ldpc_check_groups_minsum(const float *d_in, int64_t B, int n, const int32_t *d_gptr, const int32_t *d_gmem,
+                             int G, int K, float *d_out, void *stream);
 int ldpc_gather_minsum_backward(const float *d_grad_out, const float *d_in, int64_t B, int n_in,
                                 const int32_t *d_idx, int n_out, int K, const int32_t *d_argmin,
                                 float *d_grad_in, void *stream);

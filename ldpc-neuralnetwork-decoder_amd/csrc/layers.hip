@@ -150,6 +150,73 @@ int launch_gather_lds(int fpw, const float *in, const float *llr, int64_t B, int
     return LDPC_OK;
 }
 
+// CheckLayer when its index is a set of checks (every edge's row = the other edges of its check,
+// as create_LLR_mapping builds it; detected once in Python): per (check, frame) one pass collects
+// the sign-zero / NaN counts, the parity of negative signs and the two smallest |v|' (|0| -> 1e10),
+// a second pass writes each edge's output, in place over its staged input, then the frame rows
+// are copied out coalesced.  Every output equals gather_lds_kernel's: the sign product is exact
+// (its value and the sign of a zero product follow from the counts and the parity), the min of
+// the others is min1, or min2 for the edge holding min1, NaN if another edge is NaN, capped at
+// 1e10 when the row has padding (K > degree - 1).  O(degree) per check instead of O(degree^2),
+// and the (K, n) index is not re-read per workgroup.
+template <int FPW>
+__global__ __launch_bounds__(512) void check_group_kernel(const float *__restrict__ in, int64_t B, int n,
+                                                          const int32_t *__restrict__ gptr,
+                                                          const int32_t *__restrict__ gmem, int G, int K,
+                                                          float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float rows[];  // [FPW][n]
+    const int64_t b0 = (int64_t)blockIdx.x * FPW;
+    const int nb = (int)min<int64_t>(FPW, B - b0);
+    const int total = nb * n;
+    const bool vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(in + b0 * n) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(out + b0 * n) & 15) == 0;
+    if (vec) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(in + b0 * n);
+        float4 *r4 = reinterpret_cast<float4 *>(rows);
+        for (int e = threadIdx.x; e < total / 4; e += blockDim.x) r4[e] = s4[e];
+    } else {
+        for (int e = threadIdx.x; e < total; e += blockDim.x) rows[e] = in[b0 * n + e];
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < G * nb; w += blockDim.x) {
+        const int g = w / nb, f = w - g * nb;
+        float *r = rows + f * n;
+        const int p0 = gptr[g], p1 = gptr[g + 1];
+        int zeros = 0, nans = 0, neg = 0, pos = -1;
+        float m1 = INFINITY, m2 = INFINITY;
+        for (int p = p0; p < p1; ++p) {
+            const float v = r[gmem[p]];
+            const float sv = v + 1e-10f;
+            zeros += sv == 0.0f;
+            nans += sv != sv;
+            neg ^= sv < 0.0f;
+            float a = fabsf(v);
+            if (a == 0.0f) a = 1e10f;
+            if (a < m1) { m2 = m1; m1 = a; pos = p; }
+            else if (a < m2) m2 = a;
+        }
+        const bool pad = K > p1 - p0 - 1;
+        for (int p = p0; p < p1; ++p) {
+            const int j = gmem[p];
+            const float v = r[j];
+            const float sv = v + 1e-10f;
+            const int z = zeros - (sv == 0.0f), nn = nans - (sv != sv), ng = neg ^ (sv < 0.0f);
+            float m = p == pos ? m2 : m1;
+            if (pad) m = fminf(m, 1e10f);
+            const float sp = z > 0 ? (ng ? -0.0f : 0.0f) : (ng ? -1.0f : 1.0f);
+            r[j] = nn > 0 ? __builtin_nanf("") : sp * m;
+        }
+    }
+    __syncthreads();
+    if (vec) {
+        const float4 *r4 = reinterpret_cast<const float4 *>(rows);
+        float4 *o4 = reinterpret_cast<float4 *>(out + b0 * n);
+        for (int e = threadIdx.x; e < total / 4; e += blockDim.x) o4[e] = r4[e];
+    } else {
+        for (int e = threadIdx.x; e < total; e += blockDim.x) out[b0 * n + e] = rows[e];
+    }
+}
+
 bool gather_lds_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("LDPC_GATHER_LDS");
@@ -359,6 +426,26 @@ extern "C" int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const 
                        static_cast<hipStream_t>(stream), d_in,
                        B, n_in, d_idx, n_out, K, d_out, d_argmin);
     LDPC_CHECK_LAUNCH("gather_minsum_kernel");
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_check_groups_minsum(const float *d_in, int64_t B, int n, const int32_t *d_gptr,
+                                        const int32_t *d_gmem, int G, int K, float *d_out, void *stream) {
+    if (B < 0 || n <= 0 || G < 0 || K <= 0) return fail(LDPC_EINVAL, "bad check-group dimensions");
+    if (!B || !G) return LDPC_OK;
+    if (!d_in || !d_gptr || !d_gmem || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
+    const int fpw = gather_fpw(n);
+    if (!fpw) return fail(LDPC_EUNSUPPORTED, "check-group rows do not fit LDS");
+    const dim3 grid((unsigned)((B + fpw - 1) / fpw));
+    const size_t lds = (size_t)fpw * n * 4;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (fpw) {
+        case 8: hipLaunchKernelGGL(check_group_kernel<8>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
+        case 4: hipLaunchKernelGGL(check_group_kernel<4>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
+        case 2: hipLaunchKernelGGL(check_group_kernel<2>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
+        default: hipLaunchKernelGGL(check_group_kernel<1>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
+    }
+    LDPC_CHECK_LAUNCH("check_group_kernel");
     return LDPC_OK;
 }
 

@@ -17,6 +17,7 @@ LDPC_ALGO_MINSUM, LDPC_ALGO_BP = 0, 1
 LDPC_ES_OFF, LDPC_ES_BATCH, LDPC_ES_FRAME = 0, 1, 2
 LDPC_OUT_U8, LDPC_OUT_F32 = 0, 1
 LDPC_GNN_EARLY_STOP = 1
+LDPC_EINVAL, LDPC_EHIP, LDPC_EUNSUPPORTED, LDPC_ENOMEM = -1, -2, -3, -4
 
 _P = ctypes.c_void_p
 _I32, _I64, _U64, _F32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
@@ -48,6 +49,7 @@ SIGNATURES = {
     "ldpc_gather_minsum": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P, _P]),
     "ldpc_gather_minsum_backward": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P,
                                                    _P, _P]),
+    "ldpc_check_groups_minsum": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
     "ldpc_gather_sum": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
     "ldpc_gather_sum_backward": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
     "ldpc_residual": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int, _I64, ctypes.c_int, _P, _P]),

@@ -51,6 +51,43 @@ def _check_index(idx, n_in, dev, compact=False):
     return prepared
 
 
+_GROUPS = {}  # (prepared index identity, n_in) -> (gptr, gmem) device int32, or None
+
+
+def _check_groups(idx, n_in):
+    """Checks of a prepared CheckLayer index, or None: usable when every row i holds exactly the
+    other members of one set S (i in S, no duplicates), and every member of S has that row --
+    the structure create_LLR_mapping gives (each edge's row = the other edges of its check).
+    Returns (gptr (G + 1), gmem (n)) int32 on the index's device, members ascending."""
+    key = (id(idx), idx.data_ptr(), n_in)
+    hit = _GROUPS.get(key)
+    if hit is not None and hit[0] is idx:
+        return hit[1]
+    res = None
+    K, n_out = idx.shape
+    if n_out == n_in:
+        rows = idx.t().cpu().tolist()
+        sets, ok = {}, True
+        for i, r in enumerate(rows):
+            real = [j for j in r if j >= 0]
+            s = frozenset(real)
+            if len(s) != len(real) or i in s:
+                ok = False
+                break
+            sets.setdefault(s | {i}, []).append(i)
+        if ok and all(sorted(m) == sorted(k) for k, m in sets.items()):
+            groups = sorted(sorted(m) for m in sets.values())
+            ptr = [0]
+            for m in groups:
+                ptr.append(ptr[-1] + len(m))
+            res = (torch.tensor(ptr, dtype=torch.int32, device=idx.device),
+                   torch.tensor([j for m in groups for j in m], dtype=torch.int32, device=idx.device))
+    if len(_GROUPS) > 16:
+        _GROUPS.clear()
+    _GROUPS[key] = (idx, res)
+    return res
+
+
 class _CheckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, idx):
@@ -82,6 +119,14 @@ def check_minsum(x, idx):
     B, n_in = x.shape
     K, n_out = idx.shape
     out = torch.empty((B, n_out), dtype=torch.float32, device=x.device)
+    grp = _check_groups(idx, n_in)
+    if grp is not None and B:
+        gptr, gmem = grp
+        rc = N.lib().ldpc_check_groups_minsum(N.ptr(x), B, n_in, N.ptr(gptr), N.ptr(gmem), gptr.numel() - 1, K,
+                                              N.ptr(out), N.stream_ptr(x.device))
+        if rc != N.LDPC_EUNSUPPORTED:  # rows too long for LDS: the per-edge gather below
+            N.check(rc)
+            return out
     N.check(N.lib().ldpc_gather_minsum(N.ptr(x), B, n_in, N.ptr(idx), n_out, K, N.ptr(out), None,
                                        N.stream_ptr(x.device)))
     return out

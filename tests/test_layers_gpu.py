@@ -121,3 +121,38 @@ def test_unrolled_decoder_z32_vs_oracle(cuda, oracle_mod):
     close(loss, loss_o.detach().numpy(), rtol=1e-4, atol=1e-5)
     close(res.w_ch.grad, w_ch_o.grad.numpy(), rtol=1e-3, atol=1e-5)
     close(res.w_res.grad, w_res_o.grad.numpy(), rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("z", [4, 32])
+def test_check_layer_groups_equal_gather(cuda, fx, z):
+    """Without autograd, CheckLayer runs the per-check kernel (ldpc_check_groups_minsum) on
+    create_LLR_mapping's index; its outputs are bit-identical to the per-edge gather kernel, on
+    values that hit every rule: exact zeros, v = -1e-10 (sign 0), +-inf, ties, and padding."""
+    from ldpc_neural_decoder import _native as N
+    from ldpc_neural_decoder.models.layers import _check_groups, _check_index
+    H = expand_base_matrix(load_base_matrix(code_path(z)), z)
+    _, chk, _, _ = create_LLR_mapping(H.T)
+    E = chk.shape[0]
+    idx = _check_index(chk, E, cuda)
+    assert _check_groups(idx, E) is not None
+    g = torch.Generator().manual_seed(z)
+    x = torch.randn(67, E, generator=g) * 4.0
+    x[:, ::7] = 0.0
+    x[:, 3::11] = -1e-10
+    x[1::5, 5::13] = float("inf")
+    x[2::5, 6::13] = -float("inf")
+    x[:, 8::17] = 1.5  # ties within a check
+    x = x.to(cuda)
+    with torch.no_grad():
+        got = CheckLayer()(x, chk)
+    K, n_out = idx.shape
+    ref = torch.empty_like(got)
+    N.check(N.lib().ldpc_gather_minsum(N.ptr(x), x.shape[0], E, N.ptr(idx), n_out, K, N.ptr(ref), None,
+                                       N.stream_ptr(x.device)))
+    torch.cuda.synchronize()
+    a, b = got.cpu().numpy(), ref.cpu().numpy()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))  # bitwise, incl. -0.0 and NaN
+    if z == 4:  # the reference's own vectors, through the no-autograd path
+        with torch.no_grad():
+            out = CheckLayer()(t(fx["x"], cuda), torch.from_numpy(fx["check_LLR"]))
+        assert np.array_equal(out.cpu().numpy(), fx["check_out"])
