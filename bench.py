@@ -373,10 +373,11 @@ def main():
         traffic = None
         tj = a.traffic_json
         if tj is None:  # the newest PMC summary of this workload (profiles/<round>_pmc_<workload>.json)
-            for tag in ("r01s4", "r01s3", "r01s2"):
-                tj = os.path.join(ROOT, "profiles", f"{tag}_pmc_{a.workload.replace('-', '_')}.json")
-                if os.path.exists(tj):
-                    break
+            import glob
+            import re
+            found = glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{a.workload.replace('-', '_')}.json"))
+            natural = lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))]
+            tj = max(found, key=natural) if found else ""
         tjd = None
         if os.path.exists(tj):
             tjd = json.load(open(tj))
