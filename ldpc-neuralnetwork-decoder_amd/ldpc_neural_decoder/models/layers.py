@@ -284,7 +284,16 @@ class ResidualLayer(nn.Module):
         prevs = [_dev_f32(p, dev) for p in list(prev_var_messages)[:self.depth_L]]
         if len(prevs) > 8:
             raise NotImplementedError("depth_L > 8")
-        out = _ResFn.apply(_dev_f32(input_llr, dev), _dev_f32(check_messages, dev), self.w_ch.to(dev),
+        llr, cm = _dev_f32(input_llr, dev), _dev_f32(check_messages, dev)
+        # the reference raises a broadcast error on these (layers.py:160-166); the kernel would
+        # read w_ch / prev out of bounds
+        if llr.dim() != 2 or self.w_ch.numel() != llr.shape[1]:
+            raise RuntimeError(f"w_ch has {self.w_ch.numel()} entries for LLRs of shape {tuple(llr.shape)}")
+        for i, t in enumerate([cm] + prevs):
+            if t.shape != llr.shape:
+                raise RuntimeError(f"{'check_messages' if i == 0 else f'prev_var_messages[{i - 1}]'} has shape "
+                                   f"{tuple(t.shape)}, expected {tuple(llr.shape)}")
+        out = _ResFn.apply(llr, cm, self.w_ch.to(dev),
                            self.w_res.to(dev), *prevs)
         return out.to(home)
 

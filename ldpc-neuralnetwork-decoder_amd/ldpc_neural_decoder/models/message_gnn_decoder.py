@@ -17,8 +17,10 @@ Compatibility notes (each mirrors the reference line cited):
     (normalized cliques of messages sharing a variable / a check, :410-469); the groups are read
     off the matrix once and verified by probing (A @ r == group-mean(r)).
   * the unused ``output_layer`` (:188) is kept so state_dicts round-trip.
-  * the forward is inference-only (no autograd through the HIP kernels yet; training backward is
-    SURVEY §8(f) rank 1).  ``ground_truth`` still returns (probs, BCE loss) as in :313-315.
+  * with grad enabled and trainable parameters, forward() runs the fp32 training path (every
+    layer's features saved for the HIP backward, csrc/gnn_train.hip); otherwise the inference
+    path (fp32 or bf16, chunked to LDPC_GNN_WORKSPACE_BYTES).  ``decode()`` is always inference.
+    ``ground_truth`` returns (probs, BCE loss) as in :313-315.
 """
 import os
 
@@ -252,9 +254,12 @@ class MessageGNNDecoder(nn.Module):
 
     def decode(self, input_llr, message_to_var_mapping, message_types=None,
                var_to_check_adjacency=None, check_to_var_adjacency=None):
-        """message_gnn_decoder.py:319-353: hard decision (probs > 0.5) as float32."""
-        soft_bits = self.forward(input_llr, message_to_var_mapping, message_types,
-                                 var_to_check_adjacency, check_to_var_adjacency)
+        """message_gnn_decoder.py:319-353: hard decision (probs > 0.5) as float32.  A hard
+        decision has no gradient, so this always takes the inference path (chunked to the
+        workspace budget), whatever the grad mode of the caller."""
+        with torch.no_grad():
+            soft_bits = self.forward(input_llr, message_to_var_mapping, message_types,
+                                     var_to_check_adjacency, check_to_var_adjacency)
         return (soft_bits > 0.5).float()
 
 
@@ -273,10 +278,19 @@ class _NativeGnnTrain(torch.autograd.Function):
         B, Nv = llr.shape
         E = dec.num_messages
         blob = torch.cat([p.detach().reshape(-1).to(dev, torch.float32) for p in params]).contiguous()
+        wsb = N.check(N.lib().ldpc_gnn_train_workspace_size(plan.handle, H, Nv, max(B, 1), L))
+        need = L * B * E * H * 4 + wsb
+        free = torch.cuda.mem_get_info(dev)[0]
+        free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)  # torch's cache
+        if need > free:
+            raise RuntimeError(
+                f"training forward for {B} frames needs {need / 2**30:.1f} GiB of device memory "
+                f"(every layer's (B, E, H) fp32 features are saved for the backward) but "
+                f"{free / 2**30:.1f} GiB are free: use a smaller batch, or decode() / torch.no_grad() "
+                f"for inference, which is chunked")
         probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
         saved = torch.empty((L, B, E, H), dtype=torch.float32, device=dev)
         if B:
-            wsb = N.check(N.lib().ldpc_gnn_train_workspace_size(plan.handle, H, Nv, B, L))
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             N.check(N.lib().ldpc_gnn_forward_train(
                 plan.handle, H, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr), Nv, B,

@@ -58,7 +58,9 @@ class _FloodDecoder:
         """llr (B, N) float32 -> (decoded_bits (B, N) float32 0/1, iterations: int).
 
         counters: optional int64[4] device tensor += [bit errors vs all-zero, frame errors,
-        frames, iteration sum] (the sweep's fused BER/FER counting)."""
+        frames, iteration sum] (the sweep's fused BER/FER counting).  With counters the call
+        never waits for the device: `iterations` is then returned as a device int32 scalar
+        (its value is also in the counters' iteration sum) instead of a Python int."""
         if self.max_iterations < 1:
             # the reference's loop never binds decoded_bits (traditional_decoders.py:109)
             raise UnboundLocalError("local variable 'decoded_bits' referenced before assignment")
@@ -80,7 +82,10 @@ class _FloodDecoder:
             g.handle, self._algo, N.ptr(x), B, int(self.max_iterations), float(self._alpha()), es,
             kind, N.ptr(bits), N.ptr(frame_iters), N.ptr(batch_iters), N.ptr(counters), N.ptr(ws),
             wsb, N.stream_ptr(dev)))
-        iterations = self.max_iterations if es == N.LDPC_ES_OFF else int(batch_iters.item())
+        if es == N.LDPC_ES_OFF:
+            iterations = self.max_iterations
+        else:  # the reference returns an int (traditional_decoders.py:107-109): one host sync
+            iterations = batch_iters[0] if counters is not None else int(batch_iters.item())
         if home != dev:
             bits = bits.to(home)
         if return_frame_iters:

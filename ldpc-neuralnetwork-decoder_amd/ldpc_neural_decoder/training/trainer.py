@@ -23,6 +23,8 @@ var_index_tensor)`` (models.decoder.LDPCNeuralDecoder), or a MessageGNNDecoder t
 its TannerToMessageGraph ``converter`` (then the index-tensor arguments are unused and may be
 None; the loss is the decoder's BCE, message_gnn_decoder.py:313-315).
 """
+import functools
+
 import torch
 
 from ldpc_neural_decoder import _native as N
@@ -30,6 +32,16 @@ from ldpc_neural_decoder.sweep import rates, run_sweep, _dist_all_reduce
 from ldpc_neural_decoder.utils.channel import awgn_llr, count_errors
 
 HISTORY_KEYS = ("train_losses", "val_losses", "ber_history", "fer_history")
+
+
+def _on_device(fn):
+    """Run a trainer method with self.device as the current HIP device, so every tensor it makes
+    (bits, LLRs, counters, losses) lands where the decoder's parameters are."""
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        with torch.cuda.device(self.device):
+            return fn(self, *args, **kwargs)
+    return wrapper
 
 
 class LDPCDecoderTrainer:
@@ -69,7 +81,7 @@ class LDPCDecoderTrainer:
         """Random (or given) bits -> LLRs on the compute device; advances the frame counter."""
         B, n = bits.shape
         llrs = awgn_llr(B, n, snr_db, seed=self.seed, frame_offset=self._frames, bits=bits,
-                        device=N.device_of(bits))
+                        device=self.device)
         self._frames += B
         return llrs
 
@@ -80,15 +92,15 @@ class LDPCDecoderTrainer:
             return self.converter.num_variables
         raise ValueError("variable_bit_length is required")
 
-    @staticmethod
-    def _random_bits(batch_size, n):
-        return torch.randint(0, 2, (batch_size, n), device=N.device_of(None)).float()
+    def _random_bits(self, batch_size, n):
+        return torch.randint(0, 2, (batch_size, n), device=self.device).float()
 
     @staticmethod
     def _to(t, dev):
         return None if t is None else torch.as_tensor(t).to(dev)
 
     # ------------------------------------------------------------------ reference API
+    @_on_device
     def train(self, num_epochs, batch_size, learning_rate, check_index_tensor, var_index_tensor,
               snr_range=None, variable_bit_length=None, validation_interval=5, momentum=0.9, weight_decay=0.0001):
         """TR:45-140."""
@@ -101,7 +113,7 @@ class LDPCDecoderTrainer:
         variable_bit_length = self._bits_per_frame(variable_bit_length)
         for epoch in range(num_epochs):
             self.decoder.train()
-            epoch_loss = torch.zeros((), dtype=torch.float64, device=N.device_of(None))
+            epoch_loss = torch.zeros((), dtype=torch.float64, device=self.device)
             num_batches = 0
             for snr_db in snr_range:
                 bits = self._random_bits(batch_size, variable_bit_length)
@@ -125,11 +137,12 @@ class LDPCDecoderTrainer:
                 print(f"Validation - Loss: {val_loss:.6f}, BER: {ber:.6f}, FER: {fer:.6f}")
         return {k: getattr(self, k) for k in HISTORY_KEYS}
 
+    @_on_device
     def validate(self, batch_size, check_index_tensor, var_index_tensor, snr_range, variable_bit_length):
         """TR:142-203 -> (avg_loss, avg_ber, avg_fer), averaged over the SNR points."""
         self.decoder.eval()
         variable_bit_length = self._bits_per_frame(variable_bit_length)
-        dev = N.device_of(None)
+        dev = self.device
         total_loss = torch.zeros((), dtype=torch.float64, device=dev)
         per_snr = torch.zeros((len(snr_range), 4), dtype=torch.int64, device=dev)
         with torch.no_grad():
@@ -143,6 +156,7 @@ class LDPCDecoderTrainer:
         ber, fer, _ = rates(per_snr, variable_bit_length)
         return float(total_loss) / n, sum(ber) / n, sum(fer) / n
 
+    @_on_device
     def evaluate_snr_range(self, snr_range, batch_size, num_trials, check_index_tensor, var_index_tensor,
                            variable_bit_length):
         """TR:205-262 -> (ber_results, fer_results).  With torch.distributed initialised the
@@ -151,7 +165,7 @@ class LDPCDecoderTrainer:
         variable_bit_length = self._bits_per_frame(variable_bit_length)
         check_index_tensor = self._to(check_index_tensor, self.device)
         var_index_tensor = self._to(var_index_tensor, self.device)
-        dev = N.device_of(None)
+        dev = self.device
         ar, rank, world = _dist_all_reduce()
         base = self._frames
 

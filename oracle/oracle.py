@@ -276,3 +276,36 @@ def philox4x32_10(ctr, key):
         k0 = k0 + W0
         k1 = k1 + W1
     return c
+
+
+def awgn_llr(batch, n, snr_db, seed, frame_offset=0, bits=None, bpsk=False):
+    """Restatement of the fused on-device channel (csrc/channel.hip) in float64 numpy: the Philox
+    stream above, Box-Muller, then the reference's float32 formulas (utils/channel.py:39 and
+    :81-86 / :137-143 for QPSK, :217-230 for BPSK AWGNChannel.transmit).  The noise generator is
+    this build's (Philox + Box-Muller instead of torch's mt19937), so this pins the kernel's
+    arithmetic, not the reference's draws.  Returns (batch, n) float64."""
+    snr = 10.0 ** (snr_db / 10.0)
+    if bpsk:
+        std = np.float32(1.0 / np.sqrt(snr))
+        denom = np.float32(float(std) ** 2)
+    else:
+        std = np.float32(np.sqrt((1.0 / snr) / 2.0))
+        denom = np.float32(1.0 / snr)
+    quads = (n + 3) // 4
+    j = np.tile(np.arange(quads, dtype=np.uint64), batch)
+    fr = np.repeat(np.arange(batch, dtype=np.uint64) + np.uint64(frame_offset), quads)
+    tag = 0xC4A77E11 ^ (1 if bpsk else 0)
+    ctr = np.stack([j.astype(np.uint32), (fr & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+                    (fr >> np.uint64(32)).astype(np.uint32), np.full(j.shape, tag, np.uint32)], 1)
+    w = philox4x32_10(ctr, [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF]).astype(np.float64)
+    u = (np.floor(w / 256.0) + 0.5) / 16777216.0          # 24 bits centred: never 0 or 1
+    r0, r1 = np.sqrt(-2 * np.log(u[:, 0])), np.sqrt(-2 * np.log(u[:, 2]))
+    t0, t1 = 2 * np.pi * u[:, 1], 2 * np.pi * u[:, 3]
+    noise = np.stack([r0 * np.cos(t0), r0 * np.sin(t0), r1 * np.cos(t1), r1 * np.sin(t1)], 1)
+    noise = noise.reshape(batch, quads * 4)[:, :n]
+    b = np.zeros((batch, n)) if bits is None else np.asarray(bits, dtype=np.float64)
+    if bpsk:
+        sym = 1.0 - 2.0 * b
+    else:
+        sym = float(np.float32(1 / np.sqrt(2))) - b * float(np.float32(np.sqrt(2)))
+    return 2.0 * (sym + noise * float(std)) / float(denom)

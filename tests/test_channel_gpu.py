@@ -85,3 +85,18 @@ def test_count_errors_and_ber_fer(cuda):
     ref = torch.ones(10, 50, dtype=torch.uint8, device=cuda)
     c2 = count_errors(dec.to(torch.uint8), ref=ref)
     assert c2.tolist()[:3] == [494, 10, 10]
+
+
+@pytest.mark.parametrize("bpsk", [False, True])
+def test_fused_channel_vs_restatement(cuda, oracle_mod, bpsk):
+    """The fused kernel's Philox -> Box-Muller -> LLR arithmetic against oracle.awgn_llr (float64
+    numpy on the same Philox words).  Tolerance (stated): the kernel uses float32 logf / sincosf /
+    sqrtf and rounds every step to float32, so |d| <= 1e-5 |llr| + 2e-5 * 2 snr."""
+    B, n, snr_db, seed, off = 7, 1666, 1.5, 0x0BAD_5EED_1234_5678, 123_456_789_012
+    bits = (torch.rand(B, n, generator=torch.Generator().manual_seed(2)) > 0.5).to(torch.uint8)
+    for tx in (None, bits):
+        got = awgn_llr(B, n, snr_db, seed=seed, frame_offset=off, bits=None if tx is None else tx.to(cuda),
+                       bpsk=bpsk, device=cuda).double().cpu().numpy()
+        want = oracle_mod.awgn_llr(B, n, snr_db, seed, off, None if tx is None else tx.numpy(), bpsk)
+        s = 10 ** (snr_db / 10)
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=2e-5 * 2 * s)

@@ -200,3 +200,41 @@ def test_large_batch_properties(cuda, H32):
     part, _ = dec.decode(low[1000:1037].contiguous(), out_dtype=torch.uint8)
     assert torch.equal(full[1000:1037], part)
     assert full.sum() > 0
+
+
+@pytest.mark.parametrize("z", [4, 32])
+def test_graph_create_qc_equals_edge_list_graph(cuda, z):
+    """ldpc_graph_create_qc (base graph + Z: load_base_matrix + expand_base_matrix, LU:97-147)
+    builds the same graph as ldpc_graph_create on the lifted H's edge list: same info, same
+    check-major edges, same decisions."""
+    import ctypes
+    base = load_base_matrix(code_path(z))
+    H = expand_base_matrix(base, z)
+    b = np.ascontiguousarray(base.numpy().astype(np.int32))
+    h = ctypes.c_void_p()
+    with torch.cuda.device(cuda):
+        N.check(N.lib().ldpc_graph_create_qc(b.ctypes.data_as(ctypes.c_void_p), b.shape[0], b.shape[1], z,
+                                             ctypes.byref(h)))
+    try:
+        dec = MinSumScaledDecoder(H, max_iterations=6, early_stopping=False)
+        g = dec.graph(cuda)
+        vals = [ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()]
+        N.check(N.lib().ldpc_graph_info(h, *[ctypes.byref(v) for v in vals]))
+        assert [v.value for v in vals] == [g.M, g.N, g.E, g.Z, g.max_dc, g.max_dv]
+        e1c, e1v = np.empty(g.E, np.int32), np.empty(g.E, np.int32)
+        e2c, e2v = np.empty(g.E, np.int32), np.empty(g.E, np.int32)
+        N.check(N.lib().ldpc_graph_edges(h, e1c.ctypes.data_as(ctypes.c_void_p), e1v.ctypes.data_as(ctypes.c_void_p)))
+        N.check(N.lib().ldpc_graph_edges(g.handle, e2c.ctypes.data_as(ctypes.c_void_p),
+                                         e2v.ctypes.data_as(ctypes.c_void_p)))
+        assert np.array_equal(e1c, e2c) and np.array_equal(e1v, e2v)
+        rows, cols = np.nonzero(H.numpy())
+        assert np.array_equal(e1c, rows) and np.array_equal(e1v, cols)  # check-major, ascending
+        llr = torch.from_numpy(golden(f"channel_z{z}.npz")["llrs"].reshape(-1, H.shape[1])).to(cuda)
+        out = [torch.empty(llr.shape, dtype=torch.uint8, device=cuda) for _ in range(2)]
+        for handle, o in zip((h, g.handle), out):
+            N.check(N.lib().ldpc_flood_decode(handle, N.LDPC_ALGO_MINSUM, N.ptr(llr), llr.shape[0], 6, 0.75,
+                                              N.LDPC_ES_OFF, N.LDPC_OUT_U8, N.ptr(o), None, None, None, None, 0,
+                                              N.stream_ptr(cuda)))
+        assert torch.equal(out[0], out[1])
+    finally:
+        N.lib().ldpc_graph_destroy(h)

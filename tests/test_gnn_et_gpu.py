@@ -51,7 +51,7 @@ def test_no_stop_is_the_full_run(cuda):
     assert torch.equal(p0, p1)
 
 
-@pytest.mark.parametrize("z,layers,B", [(4, 5, 512), (32, 4, 64)])
+@pytest.mark.parametrize("z,layers,B", [(4, 5, 512), (32, 4, 64), (32, 15, 64)])
 def test_stops_exactly_on_codeword_decisions(cuda, oracle_mod, z, layers, B):
     base, H, dec, conv = _decoder(z, layers, cuda, seed=1)
     with torch.no_grad():  # second Linear of every MLP = 0: x = 0 after every layer

@@ -190,3 +190,86 @@ def test_cli_default_example_code(cuda, tmp_path):
     assert res["snr_range"] == [0, 2] and all(0 <= x <= 1 for x in res["ber_results"] + res["fer_results"])
     cmp_ = cli.main(["--mode", "compare", "--compare_with_traditional"] + common)
     assert set(cmp_) == {"snr_range", "belief_propagation", "min_sum_scaled", "neural_decoder"}
+
+
+def _fixture_llr_fn(llrs, dev):
+    """An llr_fn for run_sweep that replays the reference's own seeded channel LLRs
+    (tests/golden/channel_z4.npz): trial t of SNR index si starts at frame (si*T + t)*B."""
+    B = llrs.shape[1]
+
+    def fn(b, n, snr, off):
+        assert b == B and off % B == 0
+        return torch.from_numpy(llrs[off // B]).to(dev)
+    return fn
+
+
+@pytest.mark.parametrize("algo,alpha,es", [("bp", None, 0), ("bp", None, 1), ("ms", 0.75, 0), ("ms", 0.75, 1),
+                                           ("ms", 0.8, 0), ("ms", 0.8, 1)])
+def test_sweep_matches_reference_ber_fer(cuda, algo, alpha, es):
+    """run_sweep + rates (the on-device harness) on the reference's fixture LLRs reproduce the
+    per-SNR BER/FER that the reference's compute_ber_fer returned (make_golden.py:110-112) and its
+    decode() iteration counts as avg_iterations (comparative_evaluation.py:146-159).  Min-sum is
+    exact (the reference's float32 mean of a 0/1 tensor of 13 312 bits is the count / 13 312 to
+    float32 rounding); BP within the BP bar (<= 0.1 % of bits; measured 0)."""
+    from golden_util import trad_key
+    from ldpc_neural_decoder.models import BeliefPropagationDecoder, MinSumScaledDecoder
+    from ldpc_neural_decoder.sweep import rates, run_sweep
+    from conftest import golden
+    ch, fx = golden("channel_z4.npz"), golden("trad_z4.npz")
+    base, H, *_ = _code(4)
+    key = trad_key(algo, alpha, es)
+    llrs, snrs = ch["llrs"], ch["snrs"].tolist()
+    B, n = llrs.shape[1:]
+    dec = (BeliefPropagationDecoder(H, 5, early_stopping=bool(es)) if algo == "bp"
+           else MinSumScaledDecoder(H, 5, alpha, early_stopping=bool(es)))
+    counts = run_sweep(lambda llr, c: dec.decode(llr, out_dtype=torch.uint8, counters=c),
+                       _fixture_llr_fn(llrs, cuda), snrs, B, 1, n, device=cuda)
+    ber, fer, avg_it = rates(counts, n)
+    ref = fx[key + "_ber_fer"]
+    assert avg_it == [float(i) for i in fx[key + "_iters"]]
+    bit_err = counts[:, 0].cpu().numpy()
+    ref_err = np.rint(ref[:, 0] * B * n)
+    if algo == "ms":
+        assert np.array_equal(bit_err, ref_err)
+        np.testing.assert_allclose(ber, ref[:, 0], rtol=1e-6, atol=0)
+        np.testing.assert_allclose(fer, ref[:, 1], rtol=0, atol=1e-7)
+    else:
+        assert np.all(np.abs(bit_err - ref_err) <= 1e-3 * B * n)
+        np.testing.assert_allclose(fer, ref[:, 1], atol=2 / B)
+
+
+def test_comparative_evaluator_vs_reference_fixtures(cuda):
+    """ComparativeEvaluator.evaluate_all end to end (comparative_evaluation.py:40-166) with its
+    channel replaced by the reference's fixture LLRs and the fixtures' 5 iterations: the results
+    dict holds the reference's BER/FER and avg_iterations for both classic decoders."""
+    from conftest import golden
+    ch, fx = golden("channel_z4.npz"), golden("trad_z4.npz")
+    base, H, *_ = _code(4)
+    ev = ComparativeEvaluator(H, device=cuda)
+    ev.bp_decoder.max_iterations = ev.ms_decoder.max_iterations = 5
+    ev._llr_fn = lambda: _fixture_llr_fn(ch["llrs"], cuda)
+    snrs = ch["snrs"].tolist()
+    res = ev.evaluate_all(snrs, batch_size=ch["llrs"].shape[1], num_trials=1)
+    for name, key in (("belief_propagation", "bp_es1"), ("min_sum_scaled", "ms_a0.75_es1")):
+        bp = name == "belief_propagation"  # BP: within the BP bar; min-sum: exact counts
+        assert res[name]["avg_iterations"] == [float(i) for i in fx[key + "_iters"]]
+        np.testing.assert_allclose(res[name]["ber"], fx[key + "_ber_fer"][:, 0], rtol=1e-6, atol=1e-3 if bp else 0)
+        np.testing.assert_allclose(res[name]["fer"], fx[key + "_ber_fer"][:, 1], atol=2 / 64 if bp else 1e-7)
+
+
+def test_trainer_keeps_data_on_its_device(cuda):
+    """Bits, LLRs and counters are made on trainer.device (not the current device), so the HIP
+    backward's gradients land next to the parameters.  With one GPU the explicit
+    device is also the current one; with several the trainer is put on the last one."""
+    base, H, cidx, vidx, _ = _code(4)
+    dev = torch.device("cuda", torch.cuda.device_count() - 1)
+    torch.manual_seed(0)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=2, hidden_dim=16, base_graph=base, Z=4)
+    tr = LDPCDecoderTrainer(dec, device=dev, converter=conv, message_types=conv.get_message_types(base, 4))
+    bits = tr._random_bits(8, H.shape[1])
+    assert bits.device == dev and tr._channel(bits, 2.0).device == dev
+    assert all(p.device == dev for p in dec.parameters())
+    with torch.cuda.device(0):
+        hist = tr.train(num_epochs=1, batch_size=8, learning_rate=0.01, check_index_tensor=None,
+                        var_index_tensor=None, snr_range=[2], validation_interval=1)
+    assert len(hist["train_losses"]) == 1 and all(p.grad is None or p.grad.device == dev for p in dec.parameters())
