@@ -96,8 +96,12 @@ def parse():
     ap.add_argument("--workload", default="minsum-z32", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="frames per GPU (0 = workload default)")
     ap.add_argument("--snr", type=float, default=None)
+    ap.add_argument("--iterations", type=int, default=0, help="override the workload's iteration count")
     ap.add_argument("--early-termination", choices=("auto", "on", "off"), default="auto",
                     help="bf16 GNN per-frame early termination (auto: on for gnn-z32-bf16 = cfg5 only)")
+    ap.add_argument("--early-stop", choices=("off", "batch", "frame"), default="off",
+                    help="min-sum / BP stopping rule: off (cfg3: every iteration), batch (the reference's "
+                         "batch-global rule, traditional_decoders.py:104-107), frame (per-frame freeze)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
                     help="target CPU work for the oracle baseline sample (0 disables)")
     ap.add_argument("--traffic-json", default=None,
@@ -230,6 +234,7 @@ def main():
     world, rank, dev = setup_dist()
     kind, z, iters, bdef, snr = WORKLOADS[a.workload]
     snr = a.snr if a.snr is not None else snr
+    iters = a.iterations or iters
     B = a.batch or bdef
 
     from ldpc_neural_decoder import _native as N
@@ -249,11 +254,14 @@ def main():
         bits = torch.empty((B, n), dtype=torch.uint8, device=dev)
         algo = N.LDPC_ALGO_MINSUM if kind == "minsum" else N.LDPC_ALGO_BP
         stream = N.stream_ptr(dev)
+        es = {"off": N.LDPC_ES_OFF, "batch": N.LDPC_ES_BATCH, "frame": N.LDPC_ES_FRAME}[a.early_stop]
+        wsb = N.check(N.lib().ldpc_flood_workspace_size(g.handle, B, iters, es))
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
 
         def step(count):
             N.check(N.lib().ldpc_flood_decode(
-                g.handle, algo, N.ptr(llr), B, iters, 0.75, N.LDPC_ES_OFF, N.LDPC_OUT_U8,
-                N.ptr(bits), None, None, N.ptr(counters) if count else None, None, 0, stream))
+                g.handle, algo, N.ptr(llr), B, iters, 0.75, es, N.LDPC_OUT_U8,
+                N.ptr(bits), None, None, N.ptr(counters) if count else None, N.ptr(ws), wsb, stream))
 
         dtype = "f32"
         per_launch_alg = flood_bytes_per_cw(g.E, g.N, iters) * B
@@ -364,7 +372,7 @@ def main():
     avg_layers = None
     if kind.startswith("gnn") and kind != "gnn-train" and getattr(gdec, "last_iterations", None) is not None:
         avg_layers = float(gdec.last_iterations.double().mean())  # this rank's last step
-    be, fe, fr, _ = tot.tolist()
+    be, fe, fr, itsum = tot.tolist()
 
     if rank == 0:
         total_frames = B * world * a.steps
@@ -406,6 +414,7 @@ def main():
                     f"(Philox seed 20251015, frame offset rank*B), resident in HBM",
             "config": {"workload": a.workload, "code": f"5G NR BG2 Z={z} (N={n})",
                        "decoder": kind, "iterations": iters, "batch_per_gpu": B,
+                       "early_stop": a.early_stop if kind in ("minsum", "bp") else None,
                        "global_batch": B * world, "snr_db": snr, "parallelism": f"dp{world}"},
             "ber": None if kind == "lay" else be / max(fr * n, 1),
             "fer": None if kind == "lay" else fe / max(fr, 1),
@@ -415,6 +424,7 @@ def main():
                          "algorithmic_per_launch": per_launch_alg},
             "roofline_notes": roofline_notes(kind, B, n, kern_ms, traffic, tjd, tj),
             "avg_layers": avg_layers,
+            "avg_iterations": itsum / max(fr, 1) if kind in ("minsum", "bp") else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -110,14 +110,22 @@ struct MinSumStats {
 // xor of the messages' bit patterns (its sign bit = the row's sign parity): v_bitop3_b32 with the
 // three-input xor table (0x96) takes two messages per instruction (the compiler keeps a chain of
 // two-input xors here)
-template <int DC>
-__device__ __forceinline__ uint32_t sign_parity(const float (&v)[DC]) {
+template <int DC, int CAP>
+__device__ __forceinline__ uint32_t sign_parity_n(const float (&v)[CAP]) {
+    static_assert(DC <= CAP, "row longer than its buffer");
     uint32_t p = __float_as_uint(v[0]);
 #pragma unroll
     for (int e = 1; e + 1 < DC; e += 2)
         asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(p) : "v"(p), "v"(v[e]), "v"(v[e + 1]));
     if constexpr (DC % 2 == 0) p ^= __float_as_uint(v[DC - 1]);
     return p;
+}
+
+// m2 = median(m1, |x|, m2) then m1 = min(m1, |x|): the two smallest magnitudes of a row with no
+// NaN (v_min / v_med3 with |x| as a source modifier; fminf would add a NaN-quieting v_max)
+__device__ __forceinline__ void two_min_step(float &m1, float &m2, float x) {
+    asm("v_med3_f32 %0, %1, |%2|, %3" : "=v"(m2) : "v"(m1), "v"(x), "v"(m2));
+    asm("v_min_f32 %0, %1, |%2|" : "=v"(m1) : "v"(m1), "v"(x));
 }
 
 struct MinSumFast {
@@ -183,6 +191,7 @@ struct Ctx {
     FloodTables T;
     char *lds;
     uint64_t *words;  // ES: Nb decision ballots + 1 invalid-lane word (in LDS)
+    uint32_t *flag;   // LDS: sticky "a v2c may be NaN" flag of the fixed kernel's fast check path
     float alpha;
     int out_dtype;
     void *bits;
@@ -195,7 +204,11 @@ __device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int co
                                              int &errs) {
     const int bit = app < 0.0f;  // NaN < 0 is false -> 0 (traditional_decoders.py:252)
     if (C.direct_bits && L.valid) {
-        put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (L.col_off(col, s4) >> 2), bit);
+        // the empty asm keeps the (final-iteration only) 64-bit output address from being
+        // hoisted out of the iteration loop, where it would hold registers for nothing
+        int64_t fr = L.frame;
+        asm volatile("" : "+v"(fr));
+        put_bit(C.bits, C.out_dtype, fr * C.T.N + (L.col_off(col, s4) >> 2), bit);
         errs += bit;
     }
     if (C.ballots) {
@@ -209,7 +222,9 @@ __device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int co
 __device__ __forceinline__ void var_decision(const Ctx &C, const Lane &L, int col, float app, int &errs) {
     const int bit = app < 0.0f;
     if (C.direct_bits && L.valid) {
-        put_bit(C.bits, C.out_dtype, L.frame * C.T.N + (int64_t)col * L.Z() + L.k, bit);
+        int64_t fr = L.frame;
+        asm volatile("" : "+v"(fr));
+        put_bit(C.bits, C.out_dtype, fr * C.T.N + (int64_t)col * L.Z() + L.k, bit);
         errs += bit;
     }
     if (C.ballots) {
@@ -241,7 +256,7 @@ __device__ __forceinline__ void check_task(const Ctx &C, const Lane &L, const in
         MinSumFast fs;
 #pragma unroll
         for (int e = 0; e < DC; ++e) fs.add(v[e]);
-        fs.par = sign_parity(v);
+        fs.par = sign_parity_n<DC>(v);
         if (!__any(fs.special)) {  // wave-uniform
             uint32_t s1, s2;
             fs.sel_words(C.alpha, s1, s2);
@@ -512,92 +527,188 @@ __device__ __forceinline__ Lane make_lane(const FloodTables &T, const float *llr
     return L;
 }
 
-}  // namespace
+// ---------------------------------------------------------------- early stop: internal modes
+// Public early_stop values are LDPC_ES_OFF / LDPC_ES_BATCH / LDPC_ES_FRAME.  The reference's
+// batch-global rule (stop at the first iteration at which EVERY frame satisfies H x = 0 and return
+// that iteration's decisions, traditional_decoders.py:104-107) runs as up to three passes, so that
+// a batch that converges after t iterations costs about t iterations, not max_iter:
+//   ES_P1     each workgroup iterates until all of ITS frames are valid at the same iteration
+//             t_wg (or max_iter), keeps that iteration's decision ballots; T = max over t_wg.
+//             No iteration before T can be valid for the whole batch.
+//   ES_P2     workgroups with t_wg == T emit their kept ballots; the others decode T iterations
+//             again and emit; a frame that is not valid at T (with T < max_iter) raises `bad`.
+//   ES_BATCH  (runs only when bad) the exhaustive search: decode max_iter iterations keeping every
+//             iteration's ballots and validity bits; batch_and / batch_emit take the first
+//             iteration at which every frame is valid.
+// es_finalize_kernel between P2 and the fallback decides, on the device, which result stands.
+constexpr int ES_P1 = 3, ES_P2 = 4;
 
-template <int ALGO, int ES>
-__global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *__restrict__ llr,
-                                                    int64_t B, int max_iter, float alpha,
-                                                    int out_dtype, void *__restrict__ bits,
-                                                    int32_t *__restrict__ iters_out,
-                                                    uint64_t *__restrict__ counters,
-                                                    int32_t *__restrict__ batch_iters,
-                                                    uint64_t *__restrict__ ws_words,
-                                                    uint32_t *__restrict__ ws_valid, int nvw) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+struct EsWs {
+    uint64_t *words;   // ES_BATCH: [nwg][max_iter][Nb] ballots
+    uint32_t *valid;   // ES_BATCH: [B][nvw] validity bit per iteration
+    int nvw;
+    uint64_t *cand;    // ES_P1: [nwg][Nb] ballots at t_wg
+    int32_t *twg;      // ES_P1: [nwg] t_wg
+    int32_t *ctl;      // [0] T = max t_wg  [1] bad  [2] fallback needed
+    uint64_t *staged;  // [4] counters of the P2 result (applied by es_finalize_kernel)
+};
+
+struct Outs {
+    int32_t *iters_out;
+    uint64_t *counters;
+    int32_t *batch_iters;
+};
+
+// The iteration loop shared by both kernels.  Body supplies the four per-wave phases:
+//   init(C, L)             v2c <- llr on every slot
+//   check(C, L, errs)      c2v of this wave's check rows, in place
+//   var(C, L, write, errs) v2c (write) and APP of this wave's columns; decisions when asked
+//   parity(C, L) -> int    1 if any of this wave's checks fails for this lane (needs ballots)
+// Every branch below depends on workgroup-uniform values only, so all waves meet the same
+// barriers even when Body is specialised per wave.
+template <int ES, class Body>
+__device__ __forceinline__ void flood_drive(Body &body, Ctx &C, const Lane &L, int64_t B, int max_iter,
+                                            const Outs &O, const EsWs &W) {
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const Lane L = make_lane(T, llr, B);
-    const int nf = (int)min<int64_t>((int64_t)T.FG, B - (int64_t)blockIdx.x * T.FG);
+    const int FG = C.T.FG, Nb = C.T.Nb, Z = C.T.Z;
+    const int nf = (int)min<int64_t>((int64_t)FG, B - (int64_t)blockIdx.x * FG);
     const uint64_t exist = nf >= 64 ? ~0ull : ((1ull << nf) - 1ull);
-
-    Ctx C;
-    C.T = T;
-    C.lds = lds;
-    C.words = reinterpret_cast<uint64_t *>(lds + (size_t)T.nslots * 256);
-    C.alpha = alpha;
-    C.out_dtype = out_dtype;
-    C.bits = bits;
-    C.direct_bits = false;
-    C.ballots = ES != LDPC_ES_OFF;
-
-    init_phase(C, L, wave);
+    int errs = 0;
+    if constexpr (ES == LDPC_ES_BATCH) {
+        if (__builtin_amdgcn_readfirstlane(W.ctl[2]) == 0) return;  // the fast passes stood
+    }
+    if constexpr (ES == ES_P2) {
+        const int T = __builtin_amdgcn_readfirstlane(W.ctl[0]);
+        if (__builtin_amdgcn_readfirstlane(W.twg[blockIdx.x]) == T) {
+            emit_from_words(C, L, W.cand + (int64_t)blockIdx.x * Nb, exist, wave, errs);
+            if (O.iters_out && L.valid && L.k == 0) O.iters_out[L.frame] = T;
+            reduce_counters(C.lds, L, errs, T, nf, Z, W.staged, nullptr);
+            return;
+        }
+        max_iter = T;
+    }
+    if (tid == 0) *C.flag = 0;
+    __syncthreads();
+    body.init(C, L);
     __syncthreads();
 
-    int errs = 0;
     int my_iters = max_iter;
     uint64_t done = 0;
     for (int it = 0; it < max_iter; ++it) {
         const bool last = it == max_iter - 1;
-        C.direct_bits = (ES == LDPC_ES_OFF) && last;
-        check_phase<ALGO>(C, L, wave, errs);
+        C.direct_bits = (ES == LDPC_ES_OFF || ES == ES_P2) && last;
+        C.ballots = ES == LDPC_ES_BATCH || ES == LDPC_ES_FRAME || ES == ES_P1 || (ES == ES_P2 && last);
+        body.check(C, L, errs);
         __syncthreads();
-        if (ES != LDPC_ES_OFF && tid == 0) C.words[T.Nb] = 0;
-        var_phase(C, L, wave, !last, errs);
+        if (C.ballots && tid == 0) C.words[Nb] = 0;
+        body.var(C, L, !last, errs);
         __syncthreads();
-        if constexpr (ES != LDPC_ES_OFF) {
+        if (C.ballots) {
             // syndrome H x = 0 per frame (traditional_decoders.py:111-134), from the ballots
-            const uint64_t m = __ballot(parity_phase(C, L, wave));
-            if (L.lane == 0 && m) atomicOr((unsigned long long *)&C.words[T.Nb], (unsigned long long)m);
+            const uint64_t m = __ballot(body.parity(C, L));
+            if (L.lane == 0 && m) atomicOr((unsigned long long *)&C.words[Nb], (unsigned long long)m);
             __syncthreads();
-            const uint64_t vmask = frame_valid_mask(C.words[T.Nb], T.Z, T.FG) & exist;
+            const uint64_t vmask = frame_valid_mask(C.words[Nb], Z, FG) & exist;
+            bool stop = false;
             if constexpr (ES == LDPC_ES_BATCH) {
                 if (L.valid && L.k == 0 && ((vmask >> L.f) & 1ull))
-                    ws_valid[L.frame * nvw + (it >> 5)] |= 1u << (it & 31);
-                uint64_t *dst = ws_words + ((int64_t)blockIdx.x * max_iter + it) * T.Nb;
-                for (int c = tid; c < T.Nb; c += blockDim.x) dst[c] = C.words[c];
-            } else {
+                    W.valid[L.frame * W.nvw + (it >> 5)] |= 1u << (it & 31);
+                uint64_t *dst = W.words + ((int64_t)blockIdx.x * max_iter + it) * Nb;
+                for (int c = tid; c < Nb; c += blockDim.x) dst[c] = C.words[c];
+            } else if constexpr (ES == LDPC_ES_FRAME) {
                 const uint64_t newly = vmask & ~done;
                 if (newly) {
                     emit_from_words(C, L, C.words, newly, wave, errs);
                     if ((newly >> L.f) & 1ull) my_iters = it + 1;
-                    if (iters_out && L.valid && L.k == 0 && ((newly >> L.f) & 1ull)) iters_out[L.frame] = it + 1;
+                    if (O.iters_out && L.valid && L.k == 0 && ((newly >> L.f) & 1ull)) O.iters_out[L.frame] = it + 1;
                     done |= newly;
                 }
+                stop = done == exist;
+            } else if constexpr (ES == ES_P1) {
+                stop = vmask == exist || last;
+                if (stop) {
+                    uint64_t *dst = W.cand + (int64_t)blockIdx.x * Nb;
+                    for (int c = tid; c < Nb; c += blockDim.x) dst[c] = C.words[c];
+                    if (tid == 0) {
+                        W.twg[blockIdx.x] = it + 1;
+                        atomicMax(&W.ctl[0], it + 1);
+                    }
+                }
+            } else if constexpr (ES == ES_P2) {
+                if (vmask != exist && tid == 0) atomicOr(&W.ctl[1], 1);
             }
             __syncthreads();
-            if (ES == LDPC_ES_FRAME && done == exist) break;
+            if (stop) break;
         }
     }
     if constexpr (ES == LDPC_ES_FRAME) {
         const uint64_t rest = exist & ~done;
         if (rest) {
             emit_from_words(C, L, C.words, rest, wave, errs);
-            if (iters_out && L.valid && L.k == 0 && ((rest >> L.f) & 1ull)) iters_out[L.frame] = max_iter;
+            if (O.iters_out && L.valid && L.k == 0 && ((rest >> L.f) & 1ull)) O.iters_out[L.frame] = max_iter;
         }
     }
-    if constexpr (ES == LDPC_ES_OFF) {
-        if (iters_out && L.valid && L.k == 0) iters_out[L.frame] = max_iter;
+    if constexpr (ES == LDPC_ES_OFF || ES == ES_P2) {
+        if (O.iters_out && L.valid && L.k == 0) O.iters_out[L.frame] = max_iter;
     }
-    if constexpr (ES != LDPC_ES_BATCH) {
-        if (counters || batch_iters) reduce_counters(lds, L, errs, my_iters, nf, T.Z, counters, batch_iters);
+    if constexpr (ES == LDPC_ES_OFF || ES == LDPC_ES_FRAME) {
+        if (O.counters || O.batch_iters) reduce_counters(C.lds, L, errs, my_iters, nf, Z, O.counters, O.batch_iters);
     }
+    if constexpr (ES == ES_P2) reduce_counters(C.lds, L, errs, max_iter, nf, Z, W.staged, nullptr);
+}
+
+template <int ALGO>
+struct GenericBody {
+    int wave;
+    __device__ __forceinline__ void init(Ctx &C, const Lane &L) { init_phase(C, L, wave); }
+    __device__ __forceinline__ void check(const Ctx &C, const Lane &L, int &errs) { check_phase<ALGO>(C, L, wave, errs); }
+    __device__ __forceinline__ void var(const Ctx &C, const Lane &L, bool write, int &errs) {
+        var_phase(C, L, wave, write, errs);
+    }
+    __device__ __forceinline__ int parity(const Ctx &C, const Lane &L) { return parity_phase(C, L, wave); }
+};
+
+__device__ __forceinline__ void init_ctx(Ctx &C, const FloodTables &T, char *lds, float alpha, int out_dtype,
+                                         void *bits) {
+    C.T = T;
+    C.lds = lds;
+    C.flag = reinterpret_cast<uint32_t *>(lds + (size_t)T.nslots * 256);
+    C.words = reinterpret_cast<uint64_t *>(lds + (size_t)T.nslots * 256 + 8);
+    C.alpha = alpha;
+    C.out_dtype = out_dtype;
+    C.bits = bits;
+    C.direct_bits = false;
+    C.ballots = false;
+}
+
+}  // namespace
+
+template <int ALGO, int ES>
+__global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *__restrict__ llr, int64_t B,
+                                                    int max_iter, float alpha, int out_dtype,
+                                                    void *__restrict__ bits, Outs O, EsWs W) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const Lane L = make_lane(T, llr, B);
+    Ctx C;
+    init_ctx(C, T, lds, alpha, out_dtype, bits);
+    GenericBody<ALGO> body{__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6)};
+    flood_drive<ES>(body, C, L, B, max_iter, O, W);
 }
 
 // ---------------------------------------------------------------- compile-time schedules
 // flood_fixed_kernel: the same algorithm for a graph whose schedule is known at compile time
-// (gen/fixed_codes.hpp: the reference's two codes).  Every slot offset, shift, degree and task
-// list is a constant: the iteration is straight-line code, LDS addresses fold into immediate
-// offsets, and no program words are decoded.  Bit-identical to flood_kernel.
+// (gen/fixed_codes.hpp: the reference's two codes), specialised per wave.  Every slot offset,
+// shift, degree and task list is a constant, and the loop-invariant per-lane data lives in
+// registers for the whole decode:
+//   ext[]   the channel LLRs of the wave's degree-1 edges (their v2c forever)
+//   cllr[]  the channel LLRs of the wave's columns
+//   rot[]   the rotated byte base f*Z + (k - s) mod Z of every shift s the wave's columns use
+// so the iteration touches no global memory and computes no addresses: a check-row message is
+// ds_read at lane4 + slot*256, a column message at rot[s] + slot*256 (immediate offsets).  Both
+// phases are software-pipelined: the next row's / column's LDS reads are issued before the
+// current one is computed (slots are disjoint between rows and between columns, so the reads
+// never depend on the writes in flight).  Bit-identical to flood_kernel.
 namespace {
 
 template <int I>
@@ -611,123 +722,271 @@ __device__ __forceinline__ void sfor(F &&f) {
     sfor_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <class G, int ALGO, int R>
-__device__ __forceinline__ void fx_check_row(const Ctx &C, const Lane &L, int &errs) {
-    constexpr int P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
-    constexpr int ZM4 = 4 * G::Z - 1;
-    float v[DC];
-    sfor<DC>([&](auto e) {
-        constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
-        constexpr int COL = G::ROW_COL[P0 + E], S4 = 4 * G::ROW_SHIFT[P0 + E];
-        if constexpr (SL >= 0)
-            v[E] = lds_rd(C.lds, SL * 256 + L.lane4);
-        else
-            v[E] = L.llr_at(COL * 4 * G::Z + ((L.k4 + S4) & ZM4));
-    });
-    auto emit = [&](auto e, float o) {
-        constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
-        if constexpr (SL >= 0) {
-            lds_wr(C.lds, SL * 256 + L.lane4, o);
-        } else {
-            if (C.direct_bits || C.ballots)
-                ext_decision(C, L, G::ROW_COL[P0 + E], 4 * G::ROW_SHIFT[P0 + E], v[E] + o, errs);
-        }
+// per-wave compile-time plan
+template <class G, int WV>
+struct FxPlan {
+    static constexpr int R0 = G::CHK_PTR[WV], NR = G::CHK_PTR[WV + 1] - R0;
+    static constexpr int C0 = G::VAR_PTR[WV], NC = G::VAR_PTR[WV + 1] - C0;
+    struct Tab {
+        int nsh = 0, next = 0, maxdc = 1, maxdv = 1;
+        int shv[64] = {};        // distinct shifts of the wave's columns
+        int shidx[64] = {};      // shift -> index into shv (or -1)
+        int ext_before[64] = {}; // ext edges in the wave's rows before row i
     };
-    if constexpr (ALGO == LDPC_ALGO_MINSUM) {
-        MinSumFast fs;
-        sfor<DC>([&](auto e) { fs.add(v[decltype(e)::value]); });
-        fs.par = sign_parity(v);
-        if (!__any(fs.special)) {  // wave-uniform
-            uint32_t s1, s2;
-            fs.sel_words(C.alpha, s1, s2);
-            sfor<DC>([&](auto e) { emit(e, fs.c2v(v[decltype(e)::value], s1, s2)); });
-        } else {
-            MinSumStats st;
-            sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
-            sfor<DC>([&](auto e) { emit(e, st.c2v(decltype(e)::value, v[decltype(e)::value], C.alpha)); });
+    static constexpr Tab make() {
+        Tab t{};
+        for (int i = 0; i < 64; ++i) t.shidx[i] = -1;
+        for (int i = 0; i < NR; ++i) {
+            const int R = G::CHK_ROWS[R0 + i];
+            t.ext_before[i] = t.next;
+            const int dc = G::ROW_PTR[R + 1] - G::ROW_PTR[R];
+            if (dc > t.maxdc) t.maxdc = dc;
+            for (int e = G::ROW_PTR[R]; e < G::ROW_PTR[R + 1]; ++e)
+                if (G::ROW_SLOT[e] < 0) ++t.next;
         }
-    } else {
-        float acc[DC];
-        float P = 1.0f;
-        sfor<DC>([&](auto jj) {
-            constexpr int J = decltype(jj)::value;
-            const float t = tanh_half(v[J]);
-            sfor<J>([&](auto e) { acc[decltype(e)::value] = acc[decltype(e)::value] * t; });
-            acc[J] = P;
-            P = P * t;
-        });
-        sfor<DC>([&](auto e) { emit(e, two_atanh(acc[decltype(e)::value])); });
+        for (int i = 0; i < NC; ++i) {
+            const int c = G::VAR_COLS[C0 + i];
+            const int dv = G::COL_PTR[c + 1] - G::COL_PTR[c];
+            if (dv > t.maxdv) t.maxdv = dv;
+            for (int j = G::COL_PTR[c]; j < G::COL_PTR[c + 1]; ++j) {
+                const int s = G::COL_SHIFT[j];
+                if (t.shidx[s] < 0) {
+                    t.shidx[s] = t.nsh;
+                    t.shv[t.nsh++] = s;
+                }
+            }
+        }
+        return t;
     }
-}
+    static constexpr Tab T = make();
+    // index into ext[] of edge e of the wave's row i (an edge without a slot)
+    static constexpr int ext_index(int i, int e) {
+        const int R = G::CHK_ROWS[R0 + i];
+        int x = T.ext_before[i];
+        for (int q = 0; q < e; ++q)
+            if (G::ROW_SLOT[G::ROW_PTR[R] + q] < 0) ++x;
+        return x;
+    }
+};
 
-template <class G, int COL>
-__device__ __forceinline__ void fx_var_col(const Ctx &C, const Lane &L, bool write, int &errs) {
-    constexpr int P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
-    constexpr int ZM4 = 4 * G::Z - 1;
-    float P = L.llr_at(COL * 4 * G::Z + L.k4);
-    if constexpr (DV > 0) {
-        // acc[e] = P_e + c_{e+1} + ... in pairs: one v_pk_add_f32 adds c to two running sums (two
-        // independent IEEE fp32 adds, the same sequence per element as the scalar form)
+#ifndef LDPC_VAR_PIPE
+#define LDPC_VAR_PIPE 24
+#endif
+// the next column's reads are issued before the current column's adds when the two columns hold
+// at most this many messages together (register budget: 4 workgroups per CU = 128 VGPRs)
+constexpr int kVarPipe = LDPC_VAR_PIPE;
+
+template <class G, int ALGO, int WV>
+struct FixedBody {
+    using P = FxPlan<G, WV>;
+    static constexpr int ZM4 = 4 * G::Z - 1;
+    static constexpr int NEXT = P::T.next > 0 ? P::T.next : 1;
+    static constexpr int NCOL = P::NC > 0 ? P::NC : 1;
+    static constexpr int NSH = P::T.nsh > 0 ? P::T.nsh : 1;
+    static constexpr int MAXDC = P::T.maxdc, MAXDV = P::T.maxdv;
+    float ext[NEXT];
+    float cllr[NCOL];
+    int rot[NSH];
+
+    __device__ __forceinline__ void init(Ctx &C, const Lane &L) {
+        bool nan = false;
+        sfor<P::NR>([&](auto i) {
+            constexpr int I = decltype(i)::value, R = G::CHK_ROWS[P::R0 + I];
+            constexpr int P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+            sfor<DC>([&](auto e) {
+                constexpr int E = decltype(e)::value;
+                if constexpr (G::ROW_SLOT[P0 + E] < 0) {
+                    constexpr int X = P::ext_index(I, E), COL = G::ROW_COL[P0 + E], S4 = 4 * G::ROW_SHIFT[P0 + E];
+                    ext[X] = L.llr_at(COL * 4 * G::Z + ((L.k4 + S4) & ZM4));
+                    nan |= ext[X] != ext[X];
+                }
+            });
+        });
+        sfor<P::T.nsh>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            rot[J] = L.fz4 + ((L.k4 + (4 * G::Z - 4 * P::T.shv[J])) & ZM4);
+        });
+        sfor<P::NC>([&](auto i) {
+            constexpr int I = decltype(i)::value, COL = G::VAR_COLS[P::C0 + I];
+            constexpr int P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
+            cllr[I] = L.llr_at(COL * 4 * G::Z + L.k4);
+            nan |= cllr[I] != cllr[I];
+            sfor<DV>([&](auto jj) {
+                constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
+                constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
+                lds_wr(C.lds + SL * 256, rot[SI], cllr[I]);
+            });
+        });
+        if (__any(nan) && L.lane == 0) *C.flag = 1;
+    }
+
+    // ---- check phase
+    template <int I>
+    __device__ __forceinline__ void load_row(const Ctx &C, const Lane &L, float (&v)[MAXDC]) const {
+        constexpr int R = G::CHK_ROWS[P::R0 + I], P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+        sfor<DC>([&](auto e) {
+            constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
+            if constexpr (SL >= 0)
+                v[E] = lds_rd(C.lds + SL * 256, L.lane4);
+            else
+                v[E] = ext[P::ext_index(I, E)];
+        });
+    }
+
+    template <int I>
+    __device__ __forceinline__ void row(const Ctx &C, const Lane &L, const float (&v)[MAXDC], bool nanflag,
+                                        int &errs) const {
+        constexpr int R = G::CHK_ROWS[P::R0 + I], P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+        auto emit = [&](auto e, float o) {
+            constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
+            if constexpr (SL >= 0) {
+                lds_wr(C.lds + SL * 256, L.lane4, o);
+            } else {
+                if (C.direct_bits || C.ballots)  // degree-1 variable: APP = llr + c2v
+                    ext_decision(C, L, G::ROW_COL[P0 + E], 4 * G::ROW_SHIFT[P0 + E], v[E] + o, errs);
+            }
+        };
+        if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+            // the two smallest magnitudes (v_med3 / v_min with |x| source modifiers)
+            float m1 = fabsf(v[0]), m2 = INFINITY;
+            sfor<DC - 1>([&](auto e) { two_min_step(m1, m2, v[decltype(e)::value + 1]); });
+            // Fast path: no zero message in the row (then m1 > 0) and no possible NaN in the
+            // workgroup (the sticky flag, see var()): torch.sign is +-1 on every message, so
+            //   c2v_e = (par ^ sign(x_e)) * (alpha * (|x_e| == m1 ? m2 : m1))
+            // bit for bit (a tie at m1 puts m1 in m2 too).  Otherwise MinSumStats (exact
+            // torch.sign(0) = 0 and NaN semantics).
+            if (!nanflag && !__any(m1 == 0.0f)) {
+                const uint32_t par = sign_parity_n<DC>(v) & 0x80000000u;
+                const uint32_t s1 = __float_as_uint(C.alpha * m1) ^ par, s2 = __float_as_uint(C.alpha * m2) ^ par;
+                bool eq[DC];
+                sfor<DC>([&](auto e) { eq[decltype(e)::value] = fabsf(v[decltype(e)::value]) == m1; });
+                sfor<DC>([&](auto e) {
+                    constexpr int E = decltype(e)::value;
+                    emit(e, __uint_as_float((__float_as_uint(v[E]) & 0x80000000u) ^ (eq[E] ? s2 : s1)));
+                });
+            } else {
+                MinSumStats st;
+                sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
+                sfor<DC>([&](auto e) { emit(e, st.c2v(decltype(e)::value, v[decltype(e)::value], C.alpha)); });
+            }
+        } else {
+            // sum-product (traditional_decoders.py:72-81): exclusive product from 1.0 ascending
+            float acc[DC];
+            float Pp = 1.0f;
+            sfor<DC>([&](auto jj) {
+                constexpr int J = decltype(jj)::value;
+                const float t = tanh_half(v[J]);
+                sfor<J>([&](auto e) { acc[decltype(e)::value] = acc[decltype(e)::value] * t; });
+                acc[J] = Pp;
+                Pp = Pp * t;
+            });
+            sfor<DC>([&](auto e) { emit(e, two_atanh(acc[decltype(e)::value])); });
+        }
+    }
+
+    __device__ __forceinline__ void check(const Ctx &C, const Lane &L, int &errs) const {
+        bool nanflag = false;
+        if constexpr (ALGO == LDPC_ALGO_MINSUM) nanflag = __builtin_amdgcn_readfirstlane(*C.flag) != 0;
+        float va[MAXDC], vb[MAXDC];
+        load_row<0>(C, L, va);
+        sfor<P::NR>([&](auto i) {
+            constexpr int I = decltype(i)::value;
+            if constexpr (I % 2 == 0) {
+                if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, vb);
+                row<I>(C, L, va, nanflag, errs);
+            } else {
+                if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, va);
+                row<I>(C, L, vb, nanflag, errs);
+            }
+        });
+    }
+
+    // ---- variable phase
+    static constexpr int dv_of(int i) { return G::COL_PTR[G::VAR_COLS[P::C0 + i] + 1] - G::COL_PTR[G::VAR_COLS[P::C0 + i]]; }
+
+    template <int I>
+    __device__ __forceinline__ void load_col(const Ctx &C, float (&c)[MAXDV]) const {
+        constexpr int COL = G::VAR_COLS[P::C0 + I], P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
+        sfor<DV>([&](auto jj) {
+            constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
+            constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
+            c[J] = lds_rd(C.lds + SL * 256, rot[SI]);
+        });
+    }
+
+    // v2c_e = llr + sum_{e' != e} c_e' in ascending check order (traditional_decoders.py:235-250):
+    // acc[e] = P_e (prefix) then + c_{e+1} + ... ; in pairs, one v_pk_add_f32 adds c to two
+    // running sums (two independent IEEE fp32 adds, the same sequence per element)
+    template <int I>
+    __device__ __forceinline__ void col(const Ctx &C, const Lane &L, const float (&c)[MAXDV], bool write,
+                                        int &errs, bool &bad) const {
+        constexpr int COL = G::VAR_COLS[P::C0 + I], P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
+        float Pp = cllr[I];
         f32x2 acc[(DV + 1) / 2];
         sfor<DV>([&](auto jj) {
             constexpr int J = decltype(jj)::value;
-            constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
-            const float c = lds_rd(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4));
-            const f32x2 cc = {c, c};
+            const f32x2 cc = {c[J], c[J]};
             sfor<J / 2>([&](auto p) { acc[decltype(p)::value] = acc[decltype(p)::value] + cc; });
             if constexpr (J % 2 == 1) {
-                acc[J / 2].x = acc[J / 2].x + c;
-                acc[J / 2].y = P;
+                acc[J / 2].x = acc[J / 2].x + c[J];
+                acc[J / 2].y = Pp;
             } else {
-                acc[J / 2].x = P;
+                acc[J / 2].x = Pp;
             }
-            P = P + c;
+            Pp = Pp + c[J];
         });
         if (write) {
             sfor<DV>([&](auto jj) {
-                constexpr int J = decltype(jj)::value;
-                constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
-                lds_wr(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4),
-                       J % 2 == 0 ? acc[J / 2].x : acc[J / 2].y);
+                constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
+                constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
+                lds_wr(C.lds + SL * 256, rot[SI], J % 2 == 0 ? acc[J / 2].x : acc[J / 2].y);
             });
         }
+        // a NaN v2c implies a NaN or infinite APP of its column (every summand of a v2c is a
+        // summand of the APP; +-inf is absorbing), so this flag bounds the fast check path
+        if constexpr (ALGO == LDPC_ALGO_MINSUM) bad |= !(fabsf(Pp) < INFINITY);
+        if (C.direct_bits || C.ballots) var_decision(C, L, COL, Pp, errs);
     }
-    if (C.direct_bits || C.ballots) var_decision(C, L, COL, P, errs);
-}
 
-template <class G, int COL>
-__device__ __forceinline__ void fx_init_col(const Ctx &C, const Lane &L) {
-    constexpr int P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
-    constexpr int ZM4 = 4 * G::Z - 1;
-    const float x = L.llr_at(COL * 4 * G::Z + L.k4);
-    sfor<DV>([&](auto jj) {
-        constexpr int J = decltype(jj)::value;
-        constexpr int SL = G::COL_SLOT[P0 + J], S4 = 4 * G::COL_SHIFT[P0 + J];
-        lds_wr(C.lds, SL * 256 + L.fz4 + ((L.k4 + (4 * G::Z - S4)) & ZM4), x);
-    });
-}
+    __device__ __forceinline__ void var(const Ctx &C, const Lane &L, bool write, int &errs) const {
+        bool bad = false;
+        if constexpr (P::NC > 0) {
+            float ca[MAXDV], cb[MAXDV];
+            load_col<0>(C, ca);
+            sfor<P::NC>([&](auto i) {
+                constexpr int I = decltype(i)::value;
+                constexpr bool ahead = I + 1 < P::NC && dv_of(I) + dv_of(I + 1) <= kVarPipe;
+                if constexpr (I % 2 == 0) {
+                    if constexpr (ahead) load_col<I + 1>(C, cb);
+                    col<I>(C, L, ca, write, errs, bad);
+                    if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, cb);
+                } else {
+                    if constexpr (ahead) load_col<I + 1>(C, ca);
+                    col<I>(C, L, cb, write, errs, bad);
+                    if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, ca);
+                }
+            });
+        }
+        if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+            if (__any(bad) && L.lane == 0) *C.flag = 1;
+        }
+    }
 
-template <class G, int R>
-__device__ __forceinline__ int fx_parity_row(const Ctx &C, const Lane &L) {
-    constexpr int P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
-    int p = 0;
-    sfor<DC>([&](auto e) {
-        constexpr int E = decltype(e)::value;
-        constexpr int COL = G::ROW_COL[P0 + E], S = G::ROW_SHIFT[P0 + E];
-        p ^= (int)((C.words[COL] >> (L.f * G::Z + ((L.k + S) & (G::Z - 1)))) & 1ull);
-    });
-    return p;
-}
+    __device__ __forceinline__ int parity(const Ctx &C, const Lane &L) const {
+        int inv = 0;
+        sfor<P::NR>([&](auto i) {
+            constexpr int R = G::CHK_ROWS[P::R0 + decltype(i)::value];
+            constexpr int P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+            sfor<DC>([&](auto e) {
+                constexpr int E = decltype(e)::value;
+                constexpr int COL = G::ROW_COL[P0 + E], S = G::ROW_SHIFT[P0 + E];
+                inv |= (int)((C.words[COL] >> (L.f * G::Z + ((L.k + S) & (G::Z - 1)))) & 1ull);
+            });
+        });
+        return inv;
+    }
+};
 
-// the four per-wave bodies, selected once per phase by the (uniform) wave index
-template <class G, int WV, class F>
-__device__ __forceinline__ void fx_rows(F &&f) {
-    sfor<G::CHK_PTR[WV + 1] - G::CHK_PTR[WV]>([&](auto i) { f(ic<G::CHK_ROWS[G::CHK_PTR[WV] + decltype(i)::value]>{}); });
-}
-template <class G, int WV, class F>
-__device__ __forceinline__ void fx_cols(F &&f) {
-    sfor<G::VAR_PTR[WV + 1] - G::VAR_PTR[WV]>([&](auto i) { f(ic<G::VAR_COLS[G::VAR_PTR[WV] + decltype(i)::value]>{}); });
-}
 template <class G, class F>
 __device__ __forceinline__ void fx_by_wave(int wave, F &&f) {
     static_assert(G::W == 4, "fixed schedules are generated for 4 waves");
@@ -743,102 +1002,43 @@ __device__ __forceinline__ void fx_by_wave(int wave, F &&f) {
 
 template <class G, int ALGO, int ES>
 __global__ __launch_bounds__(256, 4) void flood_fixed_kernel(FloodTables T, const float *__restrict__ llr,
-                                                          int64_t B, int max_iter, float alpha,
-                                                          int out_dtype, void *__restrict__ bits,
-                                                          int32_t *__restrict__ iters_out,
-                                                          uint64_t *__restrict__ counters,
-                                                          int32_t *__restrict__ batch_iters,
-                                                          uint64_t *__restrict__ ws_words,
-                                                          uint32_t *__restrict__ ws_valid, int nvw) {
+                                                          int64_t B, int max_iter, float alpha, int out_dtype,
+                                                          void *__restrict__ bits, Outs O, EsWs W) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const Lane L0 = make_lane(T, llr, B);
-    const Lane &L = L0;
-    const int nf = (int)min<int64_t>((int64_t)T.FG, B - (int64_t)blockIdx.x * T.FG);
-    const uint64_t exist = nf >= 64 ? ~0ull : ((1ull << nf) - 1ull);
-
+    const Lane L = make_lane(T, llr, B);
     Ctx C;
-    C.T = T;
-    C.lds = lds;
-    C.words = reinterpret_cast<uint64_t *>(lds + (size_t)G::NSLOTS * 256);
-    C.alpha = alpha;
-    C.out_dtype = out_dtype;
-    C.bits = bits;
-    C.direct_bits = false;
-    C.ballots = ES != LDPC_ES_OFF;
-
-    fx_by_wave<G>(wave, [&](auto wv) {
-        fx_cols<G, decltype(wv)::value>([&](auto col) { fx_init_col<G, decltype(col)::value>(C, L); });
+    init_ctx(C, T, lds, alpha, out_dtype, bits);
+    fx_by_wave<G>(__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), [&](auto wv) {
+        FixedBody<G, ALGO, decltype(wv)::value> body;
+        flood_drive<ES>(body, C, L, B, max_iter, O, W);
     });
-    __syncthreads();
-
-    int errs = 0;
-    int my_iters = max_iter;
-    uint64_t done = 0;
-    for (int it = 0; it < max_iter; ++it) {
-        const bool last = it == max_iter - 1;
-        C.direct_bits = (ES == LDPC_ES_OFF) && last;
-        // Every address below is loop-invariant; left alone the compiler hoists all of them
-        // out of the iteration loop and runs out of VGPRs.  An empty asm "redefines" the lane
-        // bases each iteration so the addresses are rebuilt next to their use.
-        Lane L = L0;
-        asm volatile("" : "+v"(L.k4), "+v"(L.fz4), "+v"(L.lane4));
-        asm volatile("" : "+v"(L.llr_row), "+v"(L.frame));
-        fx_by_wave<G>(wave, [&](auto wv) {
-            fx_rows<G, decltype(wv)::value>([&](auto r) { fx_check_row<G, ALGO, decltype(r)::value>(C, L, errs); });
-        });
-        __syncthreads();
-        if (ES != LDPC_ES_OFF && tid == 0) C.words[G::Nb] = 0;
-        fx_by_wave<G>(wave, [&](auto wv) {
-            fx_cols<G, decltype(wv)::value>([&](auto col) { fx_var_col<G, decltype(col)::value>(C, L, !last, errs); });
-        });
-        __syncthreads();
-        if constexpr (ES != LDPC_ES_OFF) {
-            int inv = 0;
-            fx_by_wave<G>(wave, [&](auto wv) {
-                fx_rows<G, decltype(wv)::value>([&](auto r) { inv |= fx_parity_row<G, decltype(r)::value>(C, L); });
-            });
-            const uint64_t m = __ballot(inv);
-            if (L.lane == 0 && m) atomicOr((unsigned long long *)&C.words[G::Nb], (unsigned long long)m);
-            __syncthreads();
-            const uint64_t vmask = frame_valid_mask(C.words[G::Nb], G::Z, T.FG) & exist;
-            if constexpr (ES == LDPC_ES_BATCH) {
-                if (L.valid && L.k == 0 && ((vmask >> L.f) & 1ull))
-                    ws_valid[L.frame * nvw + (it >> 5)] |= 1u << (it & 31);
-                uint64_t *dst = ws_words + ((int64_t)blockIdx.x * max_iter + it) * G::Nb;
-                for (int c = tid; c < G::Nb; c += blockDim.x) dst[c] = C.words[c];
-            } else {
-                const uint64_t newly = vmask & ~done;
-                if (newly) {
-                    emit_from_words(C, L, C.words, newly, wave, errs);
-                    if ((newly >> L.f) & 1ull) my_iters = it + 1;
-                    if (iters_out && L.valid && L.k == 0 && ((newly >> L.f) & 1ull)) iters_out[L.frame] = it + 1;
-                    done |= newly;
-                }
-            }
-            __syncthreads();
-            if (ES == LDPC_ES_FRAME && done == exist) break;
-        }
-    }
-    if constexpr (ES == LDPC_ES_FRAME) {
-        const uint64_t rest = exist & ~done;
-        if (rest) {
-            emit_from_words(C, L, C.words, rest, wave, errs);
-            if (iters_out && L.valid && L.k == 0 && ((rest >> L.f) & 1ull)) iters_out[L.frame] = max_iter;
-        }
-    }
-    if constexpr (ES == LDPC_ES_OFF) {
-        if (iters_out && L.valid && L.k == 0) iters_out[L.frame] = max_iter;
-    }
-    if constexpr (ES != LDPC_ES_BATCH) {
-        if (counters || batch_iters) reduce_counters(lds, L, errs, my_iters, nf, G::Z, counters, batch_iters);
-    }
 }
 
 // ---------------------------------------------------------------- batch-global early stop
+__global__ void es_init_kernel(int32_t *ctl, uint64_t *staged, uint32_t *all_words) {
+    const int t = threadIdx.x;
+    if (t < 4) ctl[t] = 0;
+    if (t < 4) staged[t] = 0;
+    if (t < 64) all_words[t] = ~0u;
+}
+
+__global__ void es_finalize_kernel(int32_t *ctl, int max_iter, const uint64_t *staged, uint64_t *counters,
+                                   int32_t *batch_iters) {
+    const int T = ctl[0];
+    const int fallback = ctl[1] != 0 && T < max_iter;
+    ctl[2] = fallback;
+    if (!fallback) {
+        if (counters)
+            for (int i = 0; i < 4; ++i) counters[i] += staged[i];
+        if (batch_iters) *batch_iters = T;
+    } else if (batch_iters) {
+        *batch_iters = 0;  // batch_emit_kernel takes the max
+    }
+}
+
 __global__ void batch_and_kernel(const uint32_t *__restrict__ ws_valid, int64_t B, int nvw,
-                                 uint32_t *__restrict__ all_words) {
+                                 uint32_t *__restrict__ all_words, const int32_t *__restrict__ ctl) {
+    if (ctl[2] == 0) return;
     __shared__ uint32_t sh[32];
     if (threadIdx.x < 32) sh[threadIdx.x] = ~0u;
     __syncthreads();
@@ -853,7 +1053,8 @@ __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const ui
                                                          const uint32_t *__restrict__ all_words, int max_iter,
                                                          int nvw, int64_t B, int out_dtype, void *bits,
                                                          int32_t *iters_out, int32_t *batch_iters,
-                                                         uint64_t *counters) {
+                                                         uint64_t *counters, const int32_t *__restrict__ ctl) {
+    if (ctl[2] == 0) return;
     __shared__ uint32_t red[2 * 512];
     int tstar = max_iter - 1;  // first iteration at which every frame was valid
     for (int w = 0; w < nvw; ++w) {
@@ -879,41 +1080,40 @@ __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const ui
 __global__ void fill_i32_kernel(int32_t *p, int32_t v) { *p = v; }
 
 // ---------------------------------------------------------------- host side
+#ifndef LDPC_FLOOD_KERNELS_ONLY  // (defined by kernel-only experiment builds)
 namespace {
 constexpr size_t kLdsMax = 160 * 1024;
 
 size_t flood_lds_bytes(const ldpc_graph *g, int es) {
-    size_t b = (size_t)g->nslots * 64 * sizeof(float);
+    size_t b = (size_t)g->nslots * 64 * sizeof(float) + 8;  // slots + the NaN flag
     if (es != LDPC_ES_OFF) b += (size_t)(g->Nb + 1) * sizeof(uint64_t);
     return std::max<size_t>(b, 2 * 64 * (size_t)g->ft.W * sizeof(uint32_t));
 }
 
-struct BatchWs {
-    uint64_t *words;
-    uint32_t *valid;
-    uint32_t *all;
-    int64_t bytes;
-    int nvw;
-};
+size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
-BatchWs batch_ws(const ldpc_graph *g, int64_t B, int max_iter, void *base) {
-    BatchWs w{};
+// workspace of the batch-global stop; base == nullptr only sizes it
+EsWs batch_ws(const ldpc_graph *g, int64_t B, int max_iter, void *base, int64_t *bytes, uint32_t **all) {
+    EsWs w{};
     const int64_t nwg = (B + g->FG - 1) / g->FG;
     w.nvw = (max_iter + 31) / 32;
     char *p = static_cast<char *>(base);
-    const int64_t words_b = nwg * max_iter * g->Nb * 8;
-    const int64_t valid_b = ((B * w.nvw * 4) + 255) / 256 * 256;
-    w.words = reinterpret_cast<uint64_t *>(p);
-    w.valid = reinterpret_cast<uint32_t *>(p + words_b);
-    w.all = reinterpret_cast<uint32_t *>(p + words_b + valid_b);
-    w.bytes = words_b + valid_b + 256;
+    size_t off = 0;
+    auto take = [&](size_t n) { char *q = p ? p + off : nullptr; off += align256(n); return q; };
+    w.words = reinterpret_cast<uint64_t *>(take((size_t)nwg * max_iter * g->Nb * 8));
+    w.valid = reinterpret_cast<uint32_t *>(take((size_t)B * w.nvw * 4));
+    *all = reinterpret_cast<uint32_t *>(take(64 * 4));
+    w.cand = reinterpret_cast<uint64_t *>(take((size_t)nwg * g->Nb * 8));
+    w.twg = reinterpret_cast<int32_t *>(take((size_t)nwg * 4));
+    w.ctl = reinterpret_cast<int32_t *>(take(64));
+    w.staged = reinterpret_cast<uint64_t *>(take(64));
+    *bytes = (int64_t)off;
     return w;
 }
 
 template <int ALGO, int ES>
-int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha,
-                 int out_dtype, void *bits, int32_t *iters, uint64_t *counters, int32_t *batch_iters,
-                 uint64_t *ws_words, uint32_t *ws_valid, int nvw, hipStream_t s) {
+int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha, int out_dtype,
+                 void *bits, const Outs &O, const EsWs &W, hipStream_t s) {
     const size_t lds = flood_lds_bytes(g, ES);
     auto kern = flood_kernel<ALGO, ES>;
     if (g->fixed_id == 1) kern = flood_fixed_kernel<fixed::BG2_Z4, ALGO, ES>;
@@ -922,20 +1122,58 @@ int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t nwg = (B + g->FG - 1) / g->FG;
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(64 * g->ft.W), lds, s, g->ft, llr, B, max_iter, alpha,
-                       out_dtype, bits, iters, counters, batch_iters, ws_words, ws_valid, nvw);
+                       out_dtype, bits, O, W);
     LDPC_CHECK_LAUNCH("flood_kernel");
     return LDPC_OK;
 }
+
+template <int ALGO>
+int run_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha, int es, int out_dtype,
+              void *bits, const Outs &O, void *work, hipStream_t s) {
+    if (es == LDPC_ES_OFF) return launch_flood<ALGO, LDPC_ES_OFF>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);
+    if (es == LDPC_ES_FRAME)
+        return launch_flood<ALGO, LDPC_ES_FRAME>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);
+    int64_t bytes = 0;
+    uint32_t *all = nullptr;
+    const EsWs W = batch_ws(g, B, max_iter, work, &bytes, &all);
+    hipLaunchKernelGGL(es_init_kernel, dim3(1), dim3(64), 0, s, W.ctl, W.staged, all);
+    LDPC_CHECK_LAUNCH("es_init_kernel");
+    LDPC_HIP(hipMemsetAsync(W.valid, 0, (size_t)B * W.nvw * 4, s));
+    const Outs none{};
+    int rc = launch_flood<ALGO, ES_P1>(g, llr, B, max_iter, alpha, out_dtype, bits, none, W, s);
+    if (rc != LDPC_OK) return rc;
+    rc = launch_flood<ALGO, ES_P2>(g, llr, B, max_iter, alpha, out_dtype, bits, Outs{O.iters_out, nullptr, nullptr}, W, s);
+    if (rc != LDPC_OK) return rc;
+    hipLaunchKernelGGL(es_finalize_kernel, dim3(1), dim3(1), 0, s, W.ctl, max_iter, W.staged, O.counters,
+                       O.batch_iters);
+    LDPC_CHECK_LAUNCH("es_finalize_kernel");
+    // fallback (runs only when es_finalize_kernel found a frame invalid at T)
+    rc = launch_flood<ALGO, LDPC_ES_BATCH>(g, llr, B, max_iter, alpha, out_dtype, bits, none, W, s);
+    if (rc != LDPC_OK) return rc;
+    hipLaunchKernelGGL(batch_and_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, W.valid, B, W.nvw, all,
+                       W.ctl);
+    LDPC_CHECK_LAUNCH("batch_and_kernel");
+    const int64_t nwg = (B + g->FG - 1) / g->FG;
+    hipLaunchKernelGGL(batch_emit_kernel, dim3((unsigned)nwg), dim3(64 * g->ft.W), 0, s, g->ft, W.words, all,
+                       max_iter, W.nvw, B, out_dtype, bits, O.iters_out, O.batch_iters, O.counters, W.ctl);
+    LDPC_CHECK_LAUNCH("batch_emit_kernel");
+    return LDPC_OK;
+}
 }  // namespace
+#endif  // LDPC_FLOOD_KERNELS_ONLY
 
 }  // namespace ldpc
 
+#ifndef LDPC_FLOOD_KERNELS_ONLY
 using namespace ldpc;
 
 extern "C" int64_t ldpc_flood_workspace_size(const ldpc_graph *g, int64_t B, int max_iter, int early_stop) {
     if (!g || B < 0 || max_iter < 0) return fail(LDPC_EINVAL, "bad arguments");
     if (early_stop != LDPC_ES_BATCH || B == 0 || max_iter == 0) return 0;
-    return batch_ws(g, B, max_iter, nullptr).bytes;
+    int64_t bytes = 0;
+    uint32_t *all = nullptr;
+    batch_ws(g, B, max_iter, nullptr, &bytes, &all);
+    return bytes;
 }
 
 extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_llr, int64_t B,
@@ -953,48 +1191,20 @@ extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_l
     if (flood_lds_bytes(g, early_stop) > kLdsMax)
         return fail(LDPC_EUNSUPPORTED, "graph too large for the LDS-resident decoder (" +
                                            std::to_string(g->nslots) + " slots)");
+    if (early_stop == LDPC_ES_BATCH) {
+        const int64_t need = ldpc_flood_workspace_size(g, B, max_iter, early_stop);
+        if (!d_work || work_bytes < need)
+            return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes");
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (d_batch_iters && early_stop != LDPC_ES_BATCH) {
         hipLaunchKernelGGL(fill_i32_kernel, dim3(1), dim3(1), 0, s, d_batch_iters,
                            early_stop == LDPC_ES_OFF ? max_iter : 0);
         LDPC_CHECK_LAUNCH("fill");
     }
-    uint64_t *wsw = nullptr;
-    uint32_t *wsv = nullptr;
-    int nvw = 0;
-    BatchWs bw{};
-    if (early_stop == LDPC_ES_BATCH) {
-        bw = batch_ws(g, B, max_iter, d_work);
-        if (!d_work || work_bytes < bw.bytes)
-            return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(bw.bytes) + " bytes");
-        LDPC_HIP(hipMemsetAsync(bw.valid, 0, (size_t)B * bw.nvw * 4, s));
-        LDPC_HIP(hipMemsetAsync(bw.all, 0xFF, 256, s));
-        wsw = bw.words;
-        wsv = bw.valid;
-        nvw = bw.nvw;
-    }
-    int rc;
-#define LAUNCH(A, E) rc = launch_flood<A, E>(g, d_llr, B, max_iter, alpha, out_dtype, d_bits, d_iters, \
-                                             d_counters, d_batch_iters, wsw, wsv, nvw, s)
-    if (algo == LDPC_ALGO_MINSUM) {
-        if (early_stop == 0) LAUNCH(0, 0); else if (early_stop == 1) LAUNCH(0, 1); else LAUNCH(0, 2);
-    } else {
-        if (early_stop == 0) LAUNCH(1, 0); else if (early_stop == 1) LAUNCH(1, 1); else LAUNCH(1, 2);
-    }
-#undef LAUNCH
-    if (rc != LDPC_OK) return rc;
-    if (early_stop == LDPC_ES_BATCH) {
-        hipLaunchKernelGGL(batch_and_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, bw.valid, B,
-                           bw.nvw, bw.all);
-        LDPC_CHECK_LAUNCH("batch_and_kernel");
-        if (d_batch_iters) {
-            hipLaunchKernelGGL(fill_i32_kernel, dim3(1), dim3(1), 0, s, d_batch_iters, 0);
-            LDPC_CHECK_LAUNCH("fill");
-        }
-        const int64_t nwg = (B + g->FG - 1) / g->FG;
-        hipLaunchKernelGGL(batch_emit_kernel, dim3((unsigned)nwg), dim3(64 * g->ft.W), 0, s, g->ft, bw.words, bw.all,
-                           max_iter, bw.nvw, B, out_dtype, d_bits, d_iters, d_batch_iters, d_counters);
-        LDPC_CHECK_LAUNCH("batch_emit_kernel");
-    }
-    return LDPC_OK;
+    const Outs O{d_iters, d_counters, d_batch_iters};
+    return algo == LDPC_ALGO_MINSUM
+               ? run_flood<LDPC_ALGO_MINSUM>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, O, d_work, s)
+               : run_flood<LDPC_ALGO_BP>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, O, d_work, s);
 }
+#endif  // LDPC_FLOOD_KERNELS_ONLY
