@@ -24,6 +24,7 @@
 // Compile with -ffp-contract=off: no a*b+c may fuse on this path.
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include <utility>
 
@@ -1023,9 +1024,9 @@ __global__ void es_init_kernel(int32_t *ctl, uint64_t *staged, uint32_t *all_wor
 }
 
 __global__ void es_finalize_kernel(int32_t *ctl, int max_iter, const uint64_t *staged, uint64_t *counters,
-                                   int32_t *batch_iters) {
+                                   int32_t *batch_iters, int force_fallback) {
     const int T = ctl[0];
-    const int fallback = ctl[1] != 0 && T < max_iter;
+    const int fallback = force_fallback || (ctl[1] != 0 && T < max_iter);
     ctl[2] = fallback;
     if (!fallback) {
         if (counters)
@@ -1144,8 +1145,10 @@ int run_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, fl
     if (rc != LDPC_OK) return rc;
     rc = launch_flood<ALGO, ES_P2>(g, llr, B, max_iter, alpha, out_dtype, bits, Outs{O.iters_out, nullptr, nullptr}, W, s);
     if (rc != LDPC_OK) return rc;
+    // LDPC_FLOOD_ES_FALLBACK=1 forces the exhaustive pass (tests: both paths must agree)
+    const char *ff = std::getenv("LDPC_FLOOD_ES_FALLBACK");
     hipLaunchKernelGGL(es_finalize_kernel, dim3(1), dim3(1), 0, s, W.ctl, max_iter, W.staged, O.counters,
-                       O.batch_iters);
+                       O.batch_iters, (ff && std::atoi(ff) != 0) ? 1 : 0);
     LDPC_CHECK_LAUNCH("es_finalize_kernel");
     // fallback (runs only when es_finalize_kernel found a frame invalid at T)
     rc = launch_flood<ALGO, LDPC_ES_BATCH>(g, llr, B, max_iter, alpha, out_dtype, bits, none, W, s);

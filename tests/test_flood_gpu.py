@@ -238,3 +238,45 @@ def test_graph_create_qc_equals_edge_list_graph(cuda, z):
         assert torch.equal(out[0], out[1])
     finally:
         N.lib().ldpc_graph_destroy(h)
+
+
+def _validity_by_iteration(oracle_mod, g, x, K):
+    val = np.zeros((x.shape[0], K), bool)
+    for t in range(1, K + 1):
+        val[:, t - 1] = oracle_mod.syndrome_valid(g, oracle_mod.flood_decode(g, x, "minsum", t, 0.75, 0)[0])
+    return val
+
+
+def test_batch_early_stop_fallback_path(cuda, oracle_mod, H4, monkeypatch):
+    """The batch-global rule (traditional_decoders.py:104-107) when the T-search passes are not
+    enough: a frame that is valid at iteration 5, invalid at 6 and valid again from 7 shares the
+    batch with a frame first valid at 6.  Every workgroup is all-valid at some t_wg (5 and 6), T = 6,
+    but the batch is first all-valid at 7, so the exhaustive fallback must run and return the
+    oracle's batch-global result.  The forced-fallback knob must not change any result."""
+    g = oracle_mod.Graph(H4.numpy())
+    rng = np.random.default_rng(1)
+    s = 10 ** 0.0
+    x = (2 * s * (1 / np.sqrt(2) + rng.normal(0, np.sqrt(1 / (2 * s)), size=(2000, g.N)))).astype(np.float32)
+    K = 12
+    val = _validity_by_iteration(oracle_mod, g, x, K)
+    flip = [i for i in range(len(x)) if val[i, 4] and not val[i, 5] and val[i, 6:].all()]
+    late = [i for i in range(len(x)) if not val[i, :5].any() and val[i, 5:].all()]
+    assert flip and late, "fixture search: no suitable frames"
+    easy = np.full((1, g.N), 8.0, np.float32)          # the all-zero codeword, valid from iteration 1
+    fg = 16                                            # frames per workgroup at Z = 4
+    batch = np.concatenate([x[flip[:1]], np.repeat(easy, fg - 1, 0), x[late[:1]], np.repeat(easy, fg - 1, 0)])
+    ref_bits, _, ref_it, _ = oracle_mod.flood_decode(g, batch, "minsum", 20, 0.75, 1)
+    assert ref_it == 7
+    dec = MinSumScaledDecoder(H4, max_iterations=20, scaling_factor=0.75, early_stopping=True)
+    llr = torch.from_numpy(batch).to(cuda)
+    bits, it, fr = dec.decode(llr, return_frame_iters=True)
+    assert it == 7 and torch.equal(fr.cpu(), torch.full((batch.shape[0],), 7, dtype=torch.int32))
+    assert np.array_equal(bits.cpu().numpy().astype(np.uint8), ref_bits)
+    # forced fallback on an ordinary batch: same decisions and iteration count as the fast passes
+    llr2 = torch.from_numpy(x[:300]).to(cuda)
+    b_fast, i_fast = dec.decode(llr2)
+    monkeypatch.setenv("LDPC_FLOOD_ES_FALLBACK", "1")
+    b_fb, i_fb = dec.decode(llr2)
+    b_fb2, i_fb2 = dec.decode(llr)
+    assert i_fast == i_fb and torch.equal(b_fast, b_fb)
+    assert i_fb2 == 7 and torch.equal(b_fb2, bits)
