@@ -37,6 +37,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 VALU instructions/s (1e9): 1024 SIMDs, 2.4 GHz, 2 cycles each
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X fp32 matrix (spec), same guide
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X bf16 dense MFMA (spec, no sparsity)
 
@@ -62,30 +63,30 @@ def flood_bytes_per_cw(E, N, iters):
     return iters * 8 * (E + N) + 5 * N
 
 
-def roofline_notes(kind, B, n, kern_ms, traffic, pmc=None, pmc_path=None):
-    """The flood decoder keeps every message in LDS, so SURVEY §8(d)'s streaming byte model
-    (algorithmic bytes) overstates what reaches HBM; report the compulsory bytes beside it, and
-    the VALU issue utilisation from the PMC pass (the kernel's real bound): a wave64 VALU
-    instruction holds its SIMD for 4 cycles, 1024 SIMDs, cycles = GRBM_GUI_ACTIVE / 8 XCDs."""
-    if kind not in ("minsum", "bp"):
-        return None
-    comp = 5 * n * B  # LLR read (4N) + uint8 decision written (N)
-    out = {"model": "SURVEY 8(d) algorithmic bytes = messages streamed through HBM every iteration; "
-                    "this decoder is LDS-resident, hence frac > 1",
-           "compulsory_bytes_per_launch": comp,
-           "compulsory_GBps": comp / (kern_ms * 1e-3) / 1e9,
-           "compulsory_frac_of_hbm_peak": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-           "traffic_over_compulsory": (traffic / comp) if traffic else None,
-           "actual_bound": "VALU issue (the reference's exact float32 order: quadratic var-node adds), "
-                           "then LDS latency and two barriers per iteration"}
+def valu_roofline(B, n, kern_ms, traffic, pmc, pmc_path, alg_bytes):
+    """The flood decoders keep every message in LDS: HBM sees the LLRs once and the decisions once,
+    so SURVEY 8(d)'s streaming byte model is not their bound.  Their bound is VALU issue: the
+    reference's exact float32 operation order (ascending, exclusive variable sums) is a fixed
+    instruction stream per frame-iteration.  achieved = VALU wave64 instructions per launch (PMC
+    SQ_INSTS_VALU of the same workload, scaled to this batch) / the live kernel time; peak = 1024
+    SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md: a SIMD issues a
+    wave64 VALU instruction over 2 cycles)."""
     c = (pmc or {}).get("counters_per_launch", {})
-    if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
-        cycles = c["GRBM_GUI_ACTIVE"] / 8
-        out["valu_busy_frac"] = c["SQ_INSTS_VALU"] * 4 / (1024 * cycles)
-        if c.get("SQ_INSTS_LDS"):
-            out["lds_insts_per_cycle_per_cu"] = c["SQ_INSTS_LDS"] / (256 * cycles)
-        out["pmc_source"] = os.path.relpath(pmc_path, ROOT) if pmc_path else None
-    return out
+    scale = B / pmc["batch"] if pmc and pmc.get("batch") else 1.0
+    insts = c.get("SQ_INSTS_VALU")
+    achieved = insts * scale / (kern_ms * 1e-3) / 1e9 if insts else None
+    comp = 5 * n * B  # LLR read (4N) + uint8 decision written (N)
+    notes = {
+        "pmc_source": os.path.relpath(pmc_path, ROOT) if pmc_path else None,
+        "valu_insts_per_launch": insts * scale if insts else None,
+        "survey_streaming_bytes_per_launch": alg_bytes,
+        "survey_streaming_GBps": alg_bytes / (kern_ms * 1e-3) / 1e9,
+        "compulsory_bytes_per_launch": comp,
+        "compulsory_frac_of_hbm_peak": comp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "traffic_over_compulsory": (traffic / comp) if traffic else None,
+    }
+    notes.update((pmc or {}).get("derived", {}))
+    return achieved, notes
 
 
 def parse():
@@ -265,8 +266,9 @@ def main():
 
         dtype = "f32"
         per_launch_alg = flood_bytes_per_cw(g.E, g.N, iters) * B
-        bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
-        dominant = "flood_kernel<minsum>" if kind == "minsum" else "flood_kernel<bp>"
+        bound, unit, peak = "valu", "Ginst/s", VALU_PEAK_GINST
+        fixed = os.environ.get("LDPC_FLOOD_FIXED", "1") != "0"
+        dominant = f"flood_fixed_kernel<BG2_Z{z}, {kind}>" if fixed else f"flood_kernel<{kind}>"
     elif kind == "lay":
         from ldpc_neural_decoder.models import CheckLayer, OutputLayer, ResidualLayer, VariableLayer
         from ldpc_neural_decoder.utils import create_LLR_mapping
@@ -377,7 +379,7 @@ def main():
     if rank == 0:
         total_frames = B * world * a.steps
         value = total_frames / elapsed
-        achieved = per_launch_alg / (kern_ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
+        achieved = None if bound == "valu" else per_launch_alg / (kern_ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
         traffic = None
         tj = a.traffic_json
         if tj is None:  # the newest PMC summary of this workload (profiles/<round>_pmc_<workload>.json)
@@ -393,6 +395,9 @@ def main():
             traffic = tjd.get("bytes_per_launch")
             if traffic is not None and tjd.get("batch") and tjd["batch"] != B:
                 traffic = traffic * B / tjd["batch"]
+        notes = None
+        if bound == "valu":
+            achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg)
         cpu = None
         if world == 1 and a.cpu_baseline_seconds > 0:
             cpu = cpu_baseline(a.workload, z, iters, a.cpu_baseline_seconds)
@@ -419,10 +424,10 @@ def main():
             "ber": None if kind == "lay" else be / max(fr * n, 1),
             "fer": None if kind == "lay" else fe / max(fr, 1),
             "roofline": {"bound": bound, "kernel": dominant, "achieved": achieved, "peak": peak,
-                         "unit": unit, "frac": achieved / peak, "traffic": traffic,
+                         "unit": unit, "frac": None if achieved is None else achieved / peak, "traffic": traffic,
                          "kernel_ms": kern_ms,
-                         "algorithmic_per_launch": per_launch_alg},
-            "roofline_notes": roofline_notes(kind, B, n, kern_ms, traffic, tjd, tj),
+                         "algorithmic_per_launch": None if bound == "valu" else per_launch_alg},
+            "roofline_notes": notes,
             "avg_layers": avg_layers,
             "avg_iterations": itsum / max(fr, 1) if kind in ("minsum", "bp") else None,
             "cpu_baseline": cpu,

@@ -84,7 +84,12 @@ int ldpc_graph_edges(const ldpc_graph *g, int32_t *h_edge_chk, int32_t *h_edge_v
  * d_counters optional uint64[4] += {bit errors vs the all-zero codeword, frame errors,
  *   frames, sum of per-frame iterations} -- the all-zero transmit of every reference harness
  *   (comparative_evaluation.py:133); counting is fused into the decoder's epilogue.
- * d_work / work_bytes: scratch, at least ldpc_flood_workspace_size(...) bytes. */
+ * d_work / work_bytes: scratch of ldpc_flood_workspace_size(...) bytes, required for
+ *   LDPC_ES_BATCH and whenever d_counters (or d_batch_iters with LDPC_ES_FRAME) is given: the
+ *   counters are reduced through per-workgroup rows, not same-address atomics.
+ * LDPC_ES_BATCH runs as passes on the stream (first all-valid iteration per workgroup, then the
+ *   batch's candidate T, then -- only if some frame is invalid at T -- the exhaustive search);
+ *   it never synchronises with the host. */
 int64_t ldpc_flood_workspace_size(const ldpc_graph *g, int64_t B, int max_iter, int early_stop);
 int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_llr, int64_t B, int max_iter,
                       float alpha, int early_stop, int out_dtype, void *d_bits, int32_t *d_iters,

@@ -64,6 +64,21 @@ struct Lane {
 };
 
 __device__ __forceinline__ float lds_rd(const char *lds, int off) { return *reinterpret_cast<const float *>(lds + off); }
+
+// ds_write_addtid_b32: LDS[M0 + OFF + 4 * lane] = v.  No address VGPR, and half the LDS cycles of a
+// ds_write_b32 (MI355X_MICROARCH.md, LDS table: 2 vs 4 per wave-instruction).  M0 must hold the
+// LDS base (addtid_begin) and the compiler must not see these stores: callers drain them with
+// addtid_end() (s_waitcnt lgkmcnt(0)) before any barrier or LDS read of the same bytes.
+__device__ __forceinline__ void addtid_begin(const char *lds) {
+    const uint32_t base = (uint32_t)(uintptr_t)lds;
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(base) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void lds_wr_tid(float v) {
+    static_assert(OFF >= 0 && OFF < 65536, "addtid offset is 16 bits");
+    asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(v), "i"(OFF) : "memory");
+}
+__device__ __forceinline__ void addtid_end() { asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory"); }
 __device__ __forceinline__ void lds_wr(char *lds, int off, float v) { *reinterpret_cast<float *>(lds + off) = v; }
 
 __device__ __forceinline__ void put_bit(void *bits, int out_dtype, int64_t idx, int bit) {
@@ -127,6 +142,19 @@ __device__ __forceinline__ uint32_t sign_parity_n(const float (&v)[CAP]) {
 __device__ __forceinline__ void two_min_step(float &m1, float &m2, float x) {
     asm("v_med3_f32 %0, %1, |%2|, %3" : "=v"(m2) : "v"(m1), "v"(x), "v"(m2));
     asm("v_min_f32 %0, %1, |%2|" : "=v"(m1) : "v"(m1), "v"(x));
+}
+
+// lane mask of |x| == m (v_cmp_eq_f32 into an SGPR pair) and a select by it; volatile so that the
+// issue order written by the caller is kept
+__device__ __forceinline__ uint64_t cmp_eq_abs(float x, float m) {
+    uint64_t k;
+    asm volatile("v_cmp_eq_f32_e64 %0, |%1|, %2" : "=s"(k) : "v"(x), "v"(m));
+    return k;
+}
+__device__ __forceinline__ uint32_t cndmask(uint32_t if0, uint32_t if1, uint64_t k) {
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(k));
+    return r;
 }
 
 struct MinSumFast {
@@ -200,6 +228,15 @@ struct Ctx {
     bool ballots;      // ES: record decisions as ballots
 };
 
+// rotate each z-bit segment of w left by s (0 <= s < z; z a power of two dividing 64), given
+// rep1 = the word with a 1 at the bottom of every segment (scalar ops: w and rep1 are uniform)
+__device__ __forceinline__ uint64_t seg_rotl(uint64_t w, int s, int z, uint64_t rep1) {
+    if (s == 0) return w;
+    if (z >= 64) return (w << s) | (w >> (64 - s));
+    const uint64_t low = ((1ull << (z - s)) - 1ull) * rep1;  // the low z - s bits of every segment
+    return ((w & low) << s) | ((w & ~low) >> (z - s));
+}
+
 // decision of variable (col, (k + s) mod Z) computed on the lane of check row k
 __device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int col, int s4, float app,
                                              int &errs) {
@@ -208,14 +245,15 @@ __device__ __forceinline__ void ext_decision(const Ctx &C, const Lane &L, int co
         // the empty asm keeps the (final-iteration only) 64-bit output address from being
         // hoisted out of the iteration loop, where it would hold registers for nothing
         int64_t fr = L.frame;
-        asm volatile("" : "+v"(fr));
-        put_bit(C.bits, C.out_dtype, fr * C.T.N + (L.col_off(col, s4) >> 2), bit);
+        int k4 = L.k4;
+        asm volatile("" : "+v"(fr), "+v"(k4));
+        put_bit(C.bits, C.out_dtype, fr * C.T.N + (col * L.z4 + ((k4 + s4) & L.zmask4)) / 4, bit);
         errs += bit;
     }
     if (C.ballots) {
-        // move the bit of variable t to lane f*Z + t before the ballot
-        const int bt = __shfl(bit, L.vrot(s4) >> 2, 64);
-        const uint64_t w = __ballot(bt);
+        // lane f*Z + k holds variable (k + s) mod Z: rotate every Z-bit segment of the ballot left
+        // by s (uniform, scalar) so that bit f*Z + t is variable t, as in var_decision
+        const uint64_t w = seg_rotl(__ballot(bit), s4 >> 2, C.T.Z, C.T.rep1);
         if (L.lane == 0) C.words[col] = w;
     }
 }
@@ -224,8 +262,9 @@ __device__ __forceinline__ void var_decision(const Ctx &C, const Lane &L, int co
     const int bit = app < 0.0f;
     if (C.direct_bits && L.valid) {
         int64_t fr = L.frame;
-        asm volatile("" : "+v"(fr));
-        put_bit(C.bits, C.out_dtype, fr * C.T.N + (int64_t)col * L.Z() + L.k, bit);
+        int k = L.k;
+        asm volatile("" : "+v"(fr), "+v"(k));
+        put_bit(C.bits, C.out_dtype, fr * C.T.N + (int64_t)col * L.Z() + k, bit);
         errs += bit;
     }
     if (C.ballots) {
@@ -471,9 +510,13 @@ __device__ __forceinline__ void emit_from_words(const Ctx &C, const Lane &L, con
     }
 }
 
-// per-workgroup reduction of the error counters: {bit errors, frame errors, frames, iter sum}
+// per-workgroup totals of the error counters, written to this workgroup's row of the partials
+// array (no global atomics: 32 768 workgroups adding into the same 4 words serialise at L2):
+//   row = {bit errors, frame errors, frames, iteration sum, max iterations}
+// counters_reduce_kernel folds the rows into the caller's counters afterwards.
+constexpr int kPartRow = 8;  // uint32 per workgroup row
 __device__ __forceinline__ void reduce_counters(void *lds, const Lane &L, int errs, int my_iters, int nf,
-                                                int Z, uint64_t *counters, int32_t *batch_iters) {
+                                                int Z, uint32_t *row) {
     uint32_t *u = reinterpret_cast<uint32_t *>(lds);
     const int nt = blockDim.x;
     __syncthreads();
@@ -482,31 +525,28 @@ __device__ __forceinline__ void reduce_counters(void *lds, const Lane &L, int er
     __syncthreads();
     if (threadIdx.x < 64) {
         const int f = threadIdx.x;
-        uint64_t be = 0, fe = 0, fr = 0, it = 0;
-        int itmax = 0;
+        uint32_t be = 0, fe = 0, fr = 0, it = 0, itmax = 0;
         if (f < nf) {
             for (int w = 0; w < nt / 64; ++w)
                 for (int k = 0; k < Z; ++k) be += u[w * 64 + f * Z + k];
             fe = be > 0;
             fr = 1;
             it = u[nt + f * Z];
-            itmax = (int)it;
+            itmax = it;
         }
         for (int off = 32; off > 0; off >>= 1) {
             be += __shfl_xor(be, off, 64);
             fe += __shfl_xor(fe, off, 64);
             fr += __shfl_xor(fr, off, 64);
             it += __shfl_xor(it, off, 64);
-            itmax = max(itmax, __shfl_xor(itmax, off, 64));
+            itmax = max(itmax, (uint32_t)__shfl_xor(itmax, off, 64));
         }
         if (f == 0) {
-            if (counters) {
-                atomicAdd((unsigned long long *)&counters[0], (unsigned long long)be);
-                atomicAdd((unsigned long long *)&counters[1], (unsigned long long)fe);
-                atomicAdd((unsigned long long *)&counters[2], (unsigned long long)fr);
-                atomicAdd((unsigned long long *)&counters[3], (unsigned long long)it);
-            }
-            if (batch_iters) atomicMax(batch_iters, itmax);
+            row[0] = be;
+            row[1] = fe;
+            row[2] = fr;
+            row[3] = it;
+            row[4] = itmax;
         }
     }
 }
@@ -544,6 +584,12 @@ __device__ __forceinline__ Lane make_lane(const FloodTables &T, const float *llr
 // es_finalize_kernel between P2 and the fallback decides, on the device, which result stands.
 constexpr int ES_P1 = 3, ES_P2 = 4;
 
+#ifdef LDPC_EXP_NOBARRIER  // timing experiment only: results are wrong without the phase barriers
+#define LDPC_ITER_SYNC() ((void)0)
+#else
+#define LDPC_ITER_SYNC() __syncthreads()
+#endif
+
 struct EsWs {
     uint64_t *words;   // ES_BATCH: [nwg][max_iter][Nb] ballots
     uint32_t *valid;   // ES_BATCH: [B][nvw] validity bit per iteration
@@ -556,8 +602,7 @@ struct EsWs {
 
 struct Outs {
     int32_t *iters_out;
-    uint64_t *counters;
-    int32_t *batch_iters;
+    uint32_t *partials;  // [nwg][kPartRow] counter rows (NULL: no counters wanted)
 };
 
 // The iteration loop shared by both kernels.  Body supplies the four per-wave phases:
@@ -584,7 +629,7 @@ __device__ __forceinline__ void flood_drive(Body &body, Ctx &C, const Lane &L, i
         if (__builtin_amdgcn_readfirstlane(W.twg[blockIdx.x]) == T) {
             emit_from_words(C, L, W.cand + (int64_t)blockIdx.x * Nb, exist, wave, errs);
             if (O.iters_out && L.valid && L.k == 0) O.iters_out[L.frame] = T;
-            reduce_counters(C.lds, L, errs, T, nf, Z, W.staged, nullptr);
+            reduce_counters(C.lds, L, errs, T, nf, Z, O.partials + (int64_t)blockIdx.x * kPartRow);
             return;
         }
         max_iter = T;
@@ -596,15 +641,26 @@ __device__ __forceinline__ void flood_drive(Body &body, Ctx &C, const Lane &L, i
 
     int my_iters = max_iter;
     uint64_t done = 0;
+    constexpr bool kEvery = ES == LDPC_ES_BATCH || ES == LDPC_ES_FRAME || ES == ES_P1;  // ballots every iteration
     for (int it = 0; it < max_iter; ++it) {
         const bool last = it == max_iter - 1;
         C.direct_bits = (ES == LDPC_ES_OFF || ES == ES_P2) && last;
         C.ballots = ES == LDPC_ES_BATCH || ES == LDPC_ES_FRAME || ES == ES_P1 || (ES == ES_P2 && last);
-        body.check(C, L, errs);
-        __syncthreads();
+        // decisions are taken only in the iterations that need them (DEC = true), so the other
+        // iterations carry no decision code at all
+        if (kEvery || last)
+            body.template check<true>(C, L, errs);
+        else
+            body.template check<false>(C, L, errs);
+        LDPC_ITER_SYNC();
         if (C.ballots && tid == 0) C.words[Nb] = 0;
-        body.var(C, L, !last, errs);
-        __syncthreads();
+        if (last)
+            body.template var<true, false>(C, L, errs);
+        else if (kEvery)
+            body.template var<true, true>(C, L, errs);
+        else
+            body.template var<false, true>(C, L, errs);
+        LDPC_ITER_SYNC();
         if (C.ballots) {
             // syndrome H x = 0 per frame (traditional_decoders.py:111-134), from the ballots
             const uint64_t m = __ballot(body.parity(C, L));
@@ -654,18 +710,20 @@ __device__ __forceinline__ void flood_drive(Body &body, Ctx &C, const Lane &L, i
         if (O.iters_out && L.valid && L.k == 0) O.iters_out[L.frame] = max_iter;
     }
     if constexpr (ES == LDPC_ES_OFF || ES == LDPC_ES_FRAME) {
-        if (O.counters || O.batch_iters) reduce_counters(C.lds, L, errs, my_iters, nf, Z, O.counters, O.batch_iters);
+        if (O.partials) reduce_counters(C.lds, L, errs, my_iters, nf, Z, O.partials + (int64_t)blockIdx.x * kPartRow);
     }
-    if constexpr (ES == ES_P2) reduce_counters(C.lds, L, errs, max_iter, nf, Z, W.staged, nullptr);
+    if constexpr (ES == ES_P2) reduce_counters(C.lds, L, errs, max_iter, nf, Z, O.partials + (int64_t)blockIdx.x * kPartRow);
 }
 
 template <int ALGO>
 struct GenericBody {
     int wave;
     __device__ __forceinline__ void init(Ctx &C, const Lane &L) { init_phase(C, L, wave); }
+    template <bool DEC>
     __device__ __forceinline__ void check(const Ctx &C, const Lane &L, int &errs) { check_phase<ALGO>(C, L, wave, errs); }
-    __device__ __forceinline__ void var(const Ctx &C, const Lane &L, bool write, int &errs) {
-        var_phase(C, L, wave, write, errs);
+    template <bool DEC, bool WRITE>
+    __device__ __forceinline__ void var(const Ctx &C, const Lane &L, int &errs) {
+        var_phase(C, L, wave, WRITE, errs);
     }
     __device__ __forceinline__ int parity(const Ctx &C, const Lane &L) { return parity_phase(C, L, wave); }
 };
@@ -773,6 +831,12 @@ struct FxPlan {
 #ifndef LDPC_VAR_PIPE
 #define LDPC_VAR_PIPE 24
 #endif
+#ifndef LDPC_SEL_ASM
+#define LDPC_SEL_ASM 1
+#endif
+#ifndef LDPC_ADDTID
+#define LDPC_ADDTID 1  // check-phase stores as ds_write_addtid_b32 (the slot entry of a row is slot[lane])
+#endif
 // the next column's reads are issued before the current column's adds when the two columns hold
 // at most this many messages together (register budget: 4 workgroups per CU = 128 VGPRs)
 constexpr int kVarPipe = LDPC_VAR_PIPE;
@@ -834,15 +898,21 @@ struct FixedBody {
         });
     }
 
-    template <int I>
+    template <int I, bool DEC>
     __device__ __forceinline__ void row(const Ctx &C, const Lane &L, const float (&v)[MAXDC], bool nanflag,
                                         int &errs) const {
         constexpr int R = G::CHK_ROWS[P::R0 + I], P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+        // an output is needed for a slot edge always, for a degree-1 edge only to take its decision
+        auto needed = [](int e) constexpr { return DEC || G::ROW_SLOT[P0 + e] >= 0; };
         auto emit = [&](auto e, float o) {
             constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
             if constexpr (SL >= 0) {
+#if LDPC_ADDTID
+                lds_wr_tid<SL * 256>(o);
+#else
                 lds_wr(C.lds + SL * 256, L.lane4, o);
-            } else {
+#endif
+            } else if constexpr (DEC) {
                 if (C.direct_bits || C.ballots)  // degree-1 variable: APP = llr + c2v
                     ext_decision(C, L, G::ROW_COL[P0 + E], 4 * G::ROW_SHIFT[P0 + E], v[E] + o, errs);
             }
@@ -859,12 +929,29 @@ struct FixedBody {
             if (!nanflag && !__any(m1 == 0.0f)) {
                 const uint32_t par = sign_parity_n<DC>(v) & 0x80000000u;
                 const uint32_t s1 = __float_as_uint(C.alpha * m1) ^ par, s2 = __float_as_uint(C.alpha * m2) ^ par;
+#if LDPC_SEL_ASM
+                // |x_e| == m1 ? s2 : s1, with each compare issued three instructions ahead of its
+                // select (a VALU-written lane mask read by a VALU needs 2 wait states on gfx950;
+                // left to the compiler, every edge paid an s_nop 1)
+                uint64_t mk[DC];
+                uint32_t sel[DC];
+                sfor<DC + 3>([&](auto q) {
+                    constexpr int Q = decltype(q)::value;
+                    if constexpr (Q < DC && needed(Q)) mk[Q] = cmp_eq_abs(v[Q], m1);
+                    if constexpr (Q >= 3 && needed(Q - 3)) sel[Q - 3] = cndmask(s1, s2, mk[Q - 3]);
+                });
+                sfor<DC>([&](auto e) {
+                    constexpr int E = decltype(e)::value;
+                    if constexpr (needed(E)) emit(e, __uint_as_float((__float_as_uint(v[E]) & 0x80000000u) ^ sel[E]));
+                });
+#else
                 bool eq[DC];
                 sfor<DC>([&](auto e) { eq[decltype(e)::value] = fabsf(v[decltype(e)::value]) == m1; });
                 sfor<DC>([&](auto e) {
                     constexpr int E = decltype(e)::value;
                     emit(e, __uint_as_float((__float_as_uint(v[E]) & 0x80000000u) ^ (eq[E] ? s2 : s1)));
                 });
+#endif
             } else {
                 MinSumStats st;
                 sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
@@ -885,21 +972,28 @@ struct FixedBody {
         }
     }
 
+    template <bool DEC>
     __device__ __forceinline__ void check(const Ctx &C, const Lane &L, int &errs) const {
         bool nanflag = false;
         if constexpr (ALGO == LDPC_ALGO_MINSUM) nanflag = __builtin_amdgcn_readfirstlane(*C.flag) != 0;
         float va[MAXDC], vb[MAXDC];
+#if LDPC_ADDTID
+        addtid_begin(C.lds);
+#endif
         load_row<0>(C, L, va);
         sfor<P::NR>([&](auto i) {
             constexpr int I = decltype(i)::value;
             if constexpr (I % 2 == 0) {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, vb);
-                row<I>(C, L, va, nanflag, errs);
+                row<I, DEC>(C, L, va, nanflag, errs);
             } else {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, va);
-                row<I>(C, L, vb, nanflag, errs);
+                row<I, DEC>(C, L, vb, nanflag, errs);
             }
         });
+#if LDPC_ADDTID
+        addtid_end();
+#endif
     }
 
     // ---- variable phase
@@ -918,9 +1012,9 @@ struct FixedBody {
     // v2c_e = llr + sum_{e' != e} c_e' in ascending check order (traditional_decoders.py:235-250):
     // acc[e] = P_e (prefix) then + c_{e+1} + ... ; in pairs, one v_pk_add_f32 adds c to two
     // running sums (two independent IEEE fp32 adds, the same sequence per element)
-    template <int I>
-    __device__ __forceinline__ void col(const Ctx &C, const Lane &L, const float (&c)[MAXDV], bool write,
-                                        int &errs, bool &bad) const {
+    template <int I, bool DEC, bool WRITE>
+    __device__ __forceinline__ void col(const Ctx &C, const Lane &L, const float (&c)[MAXDV], int &errs,
+                                        bool &bad) const {
         constexpr int COL = G::VAR_COLS[P::C0 + I], P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
         float Pp = cllr[I];
         f32x2 acc[(DV + 1) / 2];
@@ -936,7 +1030,7 @@ struct FixedBody {
             }
             Pp = Pp + c[J];
         });
-        if (write) {
+        if constexpr (WRITE) {
             sfor<DV>([&](auto jj) {
                 constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
                 constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
@@ -946,10 +1040,13 @@ struct FixedBody {
         // a NaN v2c implies a NaN or infinite APP of its column (every summand of a v2c is a
         // summand of the APP; +-inf is absorbing), so this flag bounds the fast check path
         if constexpr (ALGO == LDPC_ALGO_MINSUM) bad |= !(fabsf(Pp) < INFINITY);
-        if (C.direct_bits || C.ballots) var_decision(C, L, COL, Pp, errs);
+        if constexpr (DEC) {
+            if (C.direct_bits || C.ballots) var_decision(C, L, COL, Pp, errs);
+        }
     }
 
-    __device__ __forceinline__ void var(const Ctx &C, const Lane &L, bool write, int &errs) const {
+    template <bool DEC, bool WRITE>
+    __device__ __forceinline__ void var(const Ctx &C, const Lane &L, int &errs) const {
         bool bad = false;
         if constexpr (P::NC > 0) {
             float ca[MAXDV], cb[MAXDV];
@@ -959,11 +1056,11 @@ struct FixedBody {
                 constexpr bool ahead = I + 1 < P::NC && dv_of(I) + dv_of(I + 1) <= kVarPipe;
                 if constexpr (I % 2 == 0) {
                     if constexpr (ahead) load_col<I + 1>(C, cb);
-                    col<I>(C, L, ca, write, errs, bad);
+                    col<I, DEC, WRITE>(C, L, ca, errs, bad);
                     if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, cb);
                 } else {
                     if constexpr (ahead) load_col<I + 1>(C, ca);
-                    col<I>(C, L, cb, write, errs, bad);
+                    col<I, DEC, WRITE>(C, L, cb, errs, bad);
                     if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, ca);
                 }
             });
@@ -975,16 +1072,22 @@ struct FixedBody {
 
     __device__ __forceinline__ int parity(const Ctx &C, const Lane &L) const {
         int inv = 0;
+        // opaque copies: the per-edge bit positions are recomputed here (early-stop iterations
+        // only) instead of being hoisted out of the loop into ~50 live registers
+        int f = L.f, k = L.k;
+        asm volatile("" : "+v"(f), "+v"(k));
         sfor<P::NR>([&](auto i) {
             constexpr int R = G::CHK_ROWS[P::R0 + decltype(i)::value];
             constexpr int P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
+            int p = 0;  // parity of check r*Z + k of frame f: xor of its variables' decisions
             sfor<DC>([&](auto e) {
                 constexpr int E = decltype(e)::value;
                 constexpr int COL = G::ROW_COL[P0 + E], S = G::ROW_SHIFT[P0 + E];
-                inv |= (int)((C.words[COL] >> (L.f * G::Z + ((L.k + S) & (G::Z - 1)))) & 1ull);
+                p ^= (int)(C.words[COL] >> (f * G::Z + ((k + S) & (G::Z - 1))));
             });
+            inv |= p;
         });
-        return inv;
+        return inv & 1;
     }
 };
 
@@ -1001,8 +1104,10 @@ __device__ __forceinline__ void fx_by_wave(int wave, F &&f) {
 
 }  // namespace
 
+// 4 workgroups per CU without early stop (LDS: 159 slots x 256 B + 8 B each); the early-stop
+// modes also keep Nb + 1 ballot words in LDS, which leaves room for 3, so they may use 168 VGPRs
 template <class G, int ALGO, int ES>
-__global__ __launch_bounds__(256, 4) void flood_fixed_kernel(FloodTables T, const float *__restrict__ llr,
+__global__ __launch_bounds__(256, ES == LDPC_ES_OFF ? 4 : 3) void flood_fixed_kernel(FloodTables T, const float *__restrict__ llr,
                                                           int64_t B, int max_iter, float alpha, int out_dtype,
                                                           void *__restrict__ bits, Outs O, EsWs W) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -1021,6 +1126,43 @@ __global__ void es_init_kernel(int32_t *ctl, uint64_t *staged, uint32_t *all_wor
     if (t < 4) ctl[t] = 0;
     if (t < 4) staged[t] = 0;
     if (t < 64) all_words[t] = ~0u;
+}
+
+// fold the per-workgroup counter rows: counters[0..3] += column sums, *batch_iters = max(it) when
+// set_iters (ES_FRAME: the largest per-frame count; the fallback: tstar + 1).  gate: run only
+// when *gate != 0 (NULL: always).  One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void counters_reduce_kernel(const uint32_t *__restrict__ partials, int64_t nwg,
+                                                               uint64_t *counters, int32_t *batch_iters,
+                                                               const int32_t *gate) {
+    if (gate && *gate == 0) return;
+    uint64_t acc[4] = {0, 0, 0, 0};
+    uint32_t mx = 0;
+    for (int64_t r = threadIdx.x; r < nwg; r += blockDim.x) {
+        const uint32_t *row = partials + r * kPartRow;
+        for (int i = 0; i < 4; ++i) acc[i] += row[i];
+        mx = max(mx, row[4]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        for (int i = 0; i < 4; ++i) acc[i] += __shfl_xor(acc[i], off, 64);
+        mx = max(mx, (uint32_t)__shfl_xor(mx, off, 64));
+    }
+    __shared__ uint64_t sh[16][5];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        for (int i = 0; i < 4; ++i) sh[w][i] = acc[i];
+        sh[w][4] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t[5] = {0, 0, 0, 0, 0};
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
+            for (int i = 0; i < 4; ++i) t[i] += sh[q][i];
+            t[4] = max(t[4], sh[q][4]);
+        }
+        if (counters)
+            for (int i = 0; i < 4; ++i) counters[i] += t[i];
+        if (batch_iters) *batch_iters = (int32_t)t[4];
+    }
 }
 
 __global__ void es_finalize_kernel(int32_t *ctl, int max_iter, const uint64_t *staged, uint64_t *counters,
@@ -1053,8 +1195,8 @@ __global__ void batch_and_kernel(const uint32_t *__restrict__ ws_valid, int64_t 
 __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const uint64_t *__restrict__ ws_words,
                                                          const uint32_t *__restrict__ all_words, int max_iter,
                                                          int nvw, int64_t B, int out_dtype, void *bits,
-                                                         int32_t *iters_out, int32_t *batch_iters,
-                                                         uint64_t *counters, const int32_t *__restrict__ ctl) {
+                                                         int32_t *iters_out, uint32_t *partials,
+                                                         const int32_t *__restrict__ ctl) {
     if (ctl[2] == 0) return;
     __shared__ uint32_t red[2 * 512];
     int tstar = max_iter - 1;  // first iteration at which every frame was valid
@@ -1075,7 +1217,7 @@ __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const ui
     emit_from_words(C, L, ws_words + ((int64_t)blockIdx.x * max_iter + tstar) * T.Nb, ~0ull, wave, errs);
     if (iters_out && L.valid && L.k == 0) iters_out[L.frame] = tstar + 1;
     const int nf = (int)min<int64_t>((int64_t)T.FG, B - (int64_t)blockIdx.x * T.FG);
-    if (counters || batch_iters) reduce_counters(red, L, errs, tstar + 1, nf, T.Z, counters, batch_iters);
+    if (partials) reduce_counters(red, L, errs, tstar + 1, nf, T.Z, partials + (int64_t)blockIdx.x * kPartRow);
 }
 
 __global__ void fill_i32_kernel(int32_t *p, int32_t v) { *p = v; }
@@ -1093,22 +1235,34 @@ size_t flood_lds_bytes(const ldpc_graph *g, int es) {
 
 size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
-// workspace of the batch-global stop; base == nullptr only sizes it
-EsWs batch_ws(const ldpc_graph *g, int64_t B, int max_iter, void *base, int64_t *bytes, uint32_t **all) {
-    EsWs w{};
+// Workspace: [counter rows: nwg x kPartRow uint32] then, for LDPC_ES_BATCH, the EsWs arrays.
+// base == nullptr only sizes it.
+struct FloodWs {
+    uint32_t *partials;
+    EsWs es;
+    uint32_t *all;
+    int64_t bytes;
+};
+
+FloodWs flood_ws(const ldpc_graph *g, int64_t B, int max_iter, int early_stop, void *base) {
+    FloodWs w{};
     const int64_t nwg = (B + g->FG - 1) / g->FG;
-    w.nvw = (max_iter + 31) / 32;
     char *p = static_cast<char *>(base);
     size_t off = 0;
     auto take = [&](size_t n) { char *q = p ? p + off : nullptr; off += align256(n); return q; };
-    w.words = reinterpret_cast<uint64_t *>(take((size_t)nwg * max_iter * g->Nb * 8));
-    w.valid = reinterpret_cast<uint32_t *>(take((size_t)B * w.nvw * 4));
-    *all = reinterpret_cast<uint32_t *>(take(64 * 4));
-    w.cand = reinterpret_cast<uint64_t *>(take((size_t)nwg * g->Nb * 8));
-    w.twg = reinterpret_cast<int32_t *>(take((size_t)nwg * 4));
-    w.ctl = reinterpret_cast<int32_t *>(take(64));
-    w.staged = reinterpret_cast<uint64_t *>(take(64));
-    *bytes = (int64_t)off;
+    w.partials = reinterpret_cast<uint32_t *>(take((size_t)nwg * kPartRow * 4));
+    if (early_stop == LDPC_ES_BATCH) {
+        EsWs &e = w.es;
+        e.nvw = (max_iter + 31) / 32;
+        e.words = reinterpret_cast<uint64_t *>(take((size_t)nwg * max_iter * g->Nb * 8));
+        e.valid = reinterpret_cast<uint32_t *>(take((size_t)B * e.nvw * 4));
+        w.all = reinterpret_cast<uint32_t *>(take(64 * 4));
+        e.cand = reinterpret_cast<uint64_t *>(take((size_t)nwg * g->Nb * 8));
+        e.twg = reinterpret_cast<int32_t *>(take((size_t)nwg * 4));
+        e.ctl = reinterpret_cast<int32_t *>(take(64));
+        e.staged = reinterpret_cast<uint64_t *>(take(64));
+    }
+    w.bytes = (int64_t)off;
     return w;
 }
 
@@ -1128,39 +1282,57 @@ int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter,
     return LDPC_OK;
 }
 
+int reduce_rows(const ldpc_graph *g, int64_t B, const uint32_t *partials, uint64_t *counters, int32_t *batch_iters,
+                const int32_t *gate, hipStream_t s) {
+    if (!counters && !batch_iters) return LDPC_OK;
+    const int64_t nwg = (B + g->FG - 1) / g->FG;
+    hipLaunchKernelGGL(counters_reduce_kernel, dim3(1), dim3(1024), 0, s, partials, nwg, counters, batch_iters, gate);
+    LDPC_CHECK_LAUNCH("counters_reduce_kernel");
+    return LDPC_OK;
+}
+
 template <int ALGO>
 int run_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha, int es, int out_dtype,
-              void *bits, const Outs &O, void *work, hipStream_t s) {
-    if (es == LDPC_ES_OFF) return launch_flood<ALGO, LDPC_ES_OFF>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);
-    if (es == LDPC_ES_FRAME)
-        return launch_flood<ALGO, LDPC_ES_FRAME>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);
-    int64_t bytes = 0;
-    uint32_t *all = nullptr;
-    const EsWs W = batch_ws(g, B, max_iter, work, &bytes, &all);
-    hipLaunchKernelGGL(es_init_kernel, dim3(1), dim3(64), 0, s, W.ctl, W.staged, all);
+              void *bits, int32_t *iters_out, uint64_t *counters, int32_t *batch_iters, void *work, hipStream_t s) {
+    const FloodWs ws = flood_ws(g, B, max_iter, es, work);
+    const bool want = counters || batch_iters;
+    const Outs O{iters_out, want ? ws.partials : nullptr};
+    if (es == LDPC_ES_OFF) {
+        int rc = launch_flood<ALGO, LDPC_ES_OFF>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);
+        // ES off: every frame ran max_iter (batch_iters was set before the launch)
+        return rc != LDPC_OK ? rc : reduce_rows(g, B, ws.partials, counters, nullptr, nullptr, s);
+    }
+    if (es == LDPC_ES_FRAME) {
+        int rc = launch_flood<ALGO, LDPC_ES_FRAME>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);
+        return rc != LDPC_OK ? rc : reduce_rows(g, B, ws.partials, counters, batch_iters, nullptr, s);
+    }
+    const EsWs &W = ws.es;
+    hipLaunchKernelGGL(es_init_kernel, dim3(1), dim3(64), 0, s, W.ctl, W.staged, ws.all);
     LDPC_CHECK_LAUNCH("es_init_kernel");
     LDPC_HIP(hipMemsetAsync(W.valid, 0, (size_t)B * W.nvw * 4, s));
-    const Outs none{};
-    int rc = launch_flood<ALGO, ES_P1>(g, llr, B, max_iter, alpha, out_dtype, bits, none, W, s);
+    int rc = launch_flood<ALGO, ES_P1>(g, llr, B, max_iter, alpha, out_dtype, bits, Outs{}, W, s);
     if (rc != LDPC_OK) return rc;
-    rc = launch_flood<ALGO, ES_P2>(g, llr, B, max_iter, alpha, out_dtype, bits, Outs{O.iters_out, nullptr, nullptr}, W, s);
+    // P2 always writes its counter rows: they become `staged`, applied by es_finalize_kernel
+    rc = launch_flood<ALGO, ES_P2>(g, llr, B, max_iter, alpha, out_dtype, bits, Outs{iters_out, ws.partials}, W, s);
+    if (rc != LDPC_OK) return rc;
+    rc = reduce_rows(g, B, ws.partials, W.staged, nullptr, nullptr, s);
     if (rc != LDPC_OK) return rc;
     // LDPC_FLOOD_ES_FALLBACK=1 forces the exhaustive pass (tests: both paths must agree)
     const char *ff = std::getenv("LDPC_FLOOD_ES_FALLBACK");
-    hipLaunchKernelGGL(es_finalize_kernel, dim3(1), dim3(1), 0, s, W.ctl, max_iter, W.staged, O.counters,
-                       O.batch_iters, (ff && std::atoi(ff) != 0) ? 1 : 0);
+    hipLaunchKernelGGL(es_finalize_kernel, dim3(1), dim3(1), 0, s, W.ctl, max_iter, W.staged, counters,
+                       batch_iters, (ff && std::atoi(ff) != 0) ? 1 : 0);
     LDPC_CHECK_LAUNCH("es_finalize_kernel");
     // fallback (runs only when es_finalize_kernel found a frame invalid at T)
-    rc = launch_flood<ALGO, LDPC_ES_BATCH>(g, llr, B, max_iter, alpha, out_dtype, bits, none, W, s);
+    rc = launch_flood<ALGO, LDPC_ES_BATCH>(g, llr, B, max_iter, alpha, out_dtype, bits, Outs{}, W, s);
     if (rc != LDPC_OK) return rc;
-    hipLaunchKernelGGL(batch_and_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, W.valid, B, W.nvw, all,
+    hipLaunchKernelGGL(batch_and_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, W.valid, B, W.nvw, ws.all,
                        W.ctl);
     LDPC_CHECK_LAUNCH("batch_and_kernel");
     const int64_t nwg = (B + g->FG - 1) / g->FG;
-    hipLaunchKernelGGL(batch_emit_kernel, dim3((unsigned)nwg), dim3(64 * g->ft.W), 0, s, g->ft, W.words, all,
-                       max_iter, W.nvw, B, out_dtype, bits, O.iters_out, O.batch_iters, O.counters, W.ctl);
+    hipLaunchKernelGGL(batch_emit_kernel, dim3((unsigned)nwg), dim3(64 * g->ft.W), 0, s, g->ft, W.words, ws.all,
+                       max_iter, W.nvw, B, out_dtype, bits, iters_out, want ? ws.partials : nullptr, W.ctl);
     LDPC_CHECK_LAUNCH("batch_emit_kernel");
-    return LDPC_OK;
+    return reduce_rows(g, B, ws.partials, counters, batch_iters, W.ctl + 2, s);
 }
 }  // namespace
 #endif  // LDPC_FLOOD_KERNELS_ONLY
@@ -1172,11 +1344,8 @@ using namespace ldpc;
 
 extern "C" int64_t ldpc_flood_workspace_size(const ldpc_graph *g, int64_t B, int max_iter, int early_stop) {
     if (!g || B < 0 || max_iter < 0) return fail(LDPC_EINVAL, "bad arguments");
-    if (early_stop != LDPC_ES_BATCH || B == 0 || max_iter == 0) return 0;
-    int64_t bytes = 0;
-    uint32_t *all = nullptr;
-    batch_ws(g, B, max_iter, nullptr, &bytes, &all);
-    return bytes;
+    if (B == 0 || max_iter == 0) return 0;
+    return flood_ws(g, B, max_iter, early_stop, nullptr).bytes;
 }
 
 extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_llr, int64_t B,
@@ -1194,20 +1363,21 @@ extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_l
     if (flood_lds_bytes(g, early_stop) > kLdsMax)
         return fail(LDPC_EUNSUPPORTED, "graph too large for the LDS-resident decoder (" +
                                            std::to_string(g->nslots) + " slots)");
-    if (early_stop == LDPC_ES_BATCH) {
+    // scratch is needed for the batch-global stop and for any counter / batch-iteration output
+    if (early_stop == LDPC_ES_BATCH || d_counters || (d_batch_iters && early_stop == LDPC_ES_FRAME)) {
         const int64_t need = ldpc_flood_workspace_size(g, B, max_iter, early_stop);
         if (!d_work || work_bytes < need)
             return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes");
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (d_batch_iters && early_stop != LDPC_ES_BATCH) {
-        hipLaunchKernelGGL(fill_i32_kernel, dim3(1), dim3(1), 0, s, d_batch_iters,
-                           early_stop == LDPC_ES_OFF ? max_iter : 0);
+    if (d_batch_iters && early_stop == LDPC_ES_OFF) {
+        hipLaunchKernelGGL(fill_i32_kernel, dim3(1), dim3(1), 0, s, d_batch_iters, max_iter);
         LDPC_CHECK_LAUNCH("fill");
     }
-    const Outs O{d_iters, d_counters, d_batch_iters};
     return algo == LDPC_ALGO_MINSUM
-               ? run_flood<LDPC_ALGO_MINSUM>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, O, d_work, s)
-               : run_flood<LDPC_ALGO_BP>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, O, d_work, s);
+               ? run_flood<LDPC_ALGO_MINSUM>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, d_iters,
+                                             d_counters, d_batch_iters, d_work, s)
+               : run_flood<LDPC_ALGO_BP>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, d_iters,
+                                         d_counters, d_batch_iters, d_work, s);
 }
 #endif  // LDPC_FLOOD_KERNELS_ONLY

@@ -184,6 +184,8 @@ int build(ldpc_graph *g) {
     t.N = N;
     t.nslots = nslots;
     t.W = W;
+    t.rep1 = 0;
+    for (int b = 0; b < 64; b += g->Z) t.rep1 |= 1ull << b;
 
     // compile-time schedule available for this exact graph (and the default 4 waves)?
     auto matches = [&](auto tag) {

@@ -36,6 +36,7 @@ struct FloodTables {
     const int32_t *chk_prog, *var_prog, *par_prog, *bw_task, *prog_ptr;
     int Z, FG, Mb, Nb, N, nslots;
     int W;  // waves per workgroup
+    uint64_t rep1;  // a 1 at the bottom of every Z-bit segment of a 64-bit ballot
 };
 constexpr int32_t kExtFlag = (int32_t)0x80000000u;
 constexpr int kShiftBit = 18;

@@ -13,4 +13,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc2 -o run -- python3 $R/bench.py --workload $W --steps 2 --warmup 1 --cpu-baseline-seconds 0 $EXTRA > $OUT/pmc2.log 2>&1; ok $?; echo "pmc2 rc=$rc"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc3 -o run -- python3 $R/bench.py --workload $W --steps 2 --warmup 1 --cpu-baseline-seconds 0 $EXTRA > $OUT/pmc3.log 2>&1; ok $?; echo "pmc3 rc=$rc"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc4 -o run -- python3 $R/bench.py --workload $W --steps 2 --warmup 1 --cpu-baseline-seconds 0 $EXTRA > $OUT/pmc4.log 2>&1; ok $?; echo "pmc4 rc=$rc"
+timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc5 -o run -- python3 $R/bench.py --workload $W --steps 2 --warmup 1 --cpu-baseline-seconds 0 $EXTRA > $OUT/pmc5.log 2>&1; ok $?; echo "pmc5 rc=$rc"
 ls -R $OUT | head -50
