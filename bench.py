@@ -17,6 +17,9 @@ Workloads (BASELINE.json configs):
   gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate),
               per-frame early-termination syndrome check after every layer (avg_layers reported)
   gnn-z32-bf16-i10  cfg4 shape (10 layers) on the bf16 path: the north-star "10 iterations" GNN line
+  gnn-z32-sweep  cfg4 as BASELINE states it: the on-device SNR sweep 0..6 dB step 1 (sweep.py
+              evaluate_message_gnn = run_comparison_all.py:245-295), fp32, B frames per GPU per SNR;
+              one step = one whole sweep (channel + decode + counters, RCCL all-reduce at the end)
   lay-z32     the index-gather layers (models/layers.py): 10 iterations of CheckLayer ->
               VariableLayer -> ResidualLayer(depth 2) + OutputLayer on the var-major edge vector
   gnn-train-z32 / gnn-train-z4  one training step (fp32 forward saving features, BCE, HIP backward,
@@ -51,6 +54,7 @@ WORKLOADS = {
     "gnn-z32-bf16": ("gnn-bf16", 32, 15, 32768, 2.0),
     "gnn-z4-bf16": ("gnn-bf16", 4, 5, 4096, 2.0),
     "gnn-z32-bf16-i10": ("gnn-bf16", 32, 10, 32768, 2.0),
+    "gnn-z32-sweep": ("gnn-sweep", 32, 10, 32768, None),
     "gnn-train-z32": ("gnn-train", 32, 10, 256, 2.0),
     "lay-z32": ("lay", 32, 10, 4096, 2.0),
     "gnn-train-z4": ("gnn-train", 4, 5, 4096, 2.0),
@@ -154,6 +158,7 @@ def cpu_baseline(workload, z, iters, target_s):
         return (2 * s * (1 / np.sqrt(2) + noise)).astype(np.float32)
 
     if kind.startswith("gnn"):
+        snr = 2.0 if snr is None else snr
         from ldpc_neural_decoder.models import create_message_gnn_decoder
         torch.manual_seed(7)
         dec, conv = create_message_gnn_decoder(torch.from_numpy(H), num_iterations=iters,
@@ -235,6 +240,8 @@ def main():
     world, rank, dev = setup_dist()
     kind, z, iters, bdef, snr = WORKLOADS[a.workload]
     snr = a.snr if a.snr is not None else snr
+    sweep = snr is None  # gnn-z32-sweep: every step sweeps 0..6 dB
+    snr = 0.0 if sweep else snr
     iters = a.iterations or iters
     B = a.batch or bdef
 
@@ -310,8 +317,16 @@ def main():
         probs = torch.empty((B, n), dtype=torch.float32, device=dev)
         vg, cg = conv.var_groups, conv.check_groups
         g_m, g_n = H.shape
+        sweep_snrs = [float(x) for x in range(0, 7)]
+        sweep_out = {}
 
-        if kind == "gnn-train":
+        if kind == "gnn-sweep":
+            from ldpc_neural_decoder.sweep import evaluate_message_gnn
+
+            def step(count):  # trial t of each SNR -> rank t: every rank decodes B frames per SNR
+                sweep_out["ber_fer"] = evaluate_message_gnn(gdec, conv, sweep_snrs, B, world, dev, seed=20251015,
+                                                            message_types=types)
+        elif kind == "gnn-train":
             opt = torch.optim.SGD(gdec.parameters(), lr=1e-3, momentum=0.9, weight_decay=1e-4)
             gt = torch.zeros((B, n), dtype=torch.float32, device=dev)
             Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
@@ -333,7 +348,10 @@ def main():
 
         dtype = "bf16" if kind == "gnn-bf16" else "f32"
         E = len(conv.messages)
-        if kind == "gnn-bf16":
+        if kind == "gnn-sweep":
+            per_launch_alg = 12 * 64 * 64 * E * B * iters * len(sweep_snrs)  # MLP FLOPs per sweep
+            bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
+        elif kind == "gnn-bf16":
             # HBM-bound; per frame-layer 3 passes over the bf16 features
             # (group-mean read, MLP read + write) + the fp32-sized group-mean rows written + read
             per_launch_alg = iters * (3 * E * 64 * 2 + 2 * (g_n + g_m) * 64 * 4) * B
@@ -346,7 +364,8 @@ def main():
         else:
             per_launch_alg = 12 * 64 * 64 * E * B * iters  # useful MLP FLOPs per forward
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
-        dominant = "gnn training step" if kind == "gnn-train" else "gnn forward (all layers)"
+        dominant = {"gnn-train": "gnn training step", "gnn-sweep": "SNR sweep (7 x channel + gnn forward + count)"}.get(
+            kind, "gnn forward (all layers)")
 
     for _ in range(a.warmup):
         step(False)
@@ -377,7 +396,7 @@ def main():
     be, fe, fr, itsum = tot.tolist()
 
     if rank == 0:
-        total_frames = B * world * a.steps
+        total_frames = B * world * a.steps * (7 if kind == "gnn-sweep" else 1)
         value = total_frames / elapsed
         achieved = None if bound == "valu" else per_launch_alg / (kern_ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
         traffic = None
@@ -415,14 +434,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": f"synthetic: all-zero codeword through the on-device QPSK/AWGN channel at {snr} dB "
+            "data": f"synthetic: all-zero codeword through the on-device QPSK/AWGN channel at "
+                    f"{'0..6 (step 1)' if sweep else snr} dB "
                     f"(Philox seed 20251015, frame offset rank*B), resident in HBM",
             "config": {"workload": a.workload, "code": f"5G NR BG2 Z={z} (N={n})",
                        "decoder": kind, "iterations": iters, "batch_per_gpu": B,
                        "early_stop": a.early_stop if kind in ("minsum", "bp") else None,
-                       "global_batch": B * world, "snr_db": snr, "parallelism": f"dp{world}"},
-            "ber": None if kind == "lay" else be / max(fr * n, 1),
-            "fer": None if kind == "lay" else fe / max(fr, 1),
+                       "global_batch": B * world, "snr_db": "0..6" if sweep else snr,
+                       "parallelism": f"dp{world}"},
+            "ber": None if kind == "lay" else (sweep_out["ber_fer"][0] if kind == "gnn-sweep"
+                                               else be / max(fr * n, 1)),
+            "fer": None if kind == "lay" else (sweep_out["ber_fer"][1] if kind == "gnn-sweep" else fe / max(fr, 1)),
             "roofline": {"bound": bound, "kernel": dominant, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": None if achieved is None else achieved / peak, "traffic": traffic,
                          "kernel_ms": kern_ms,

@@ -56,9 +56,20 @@ def rates(counts, n):
 
 
 def _dist_all_reduce():
+    """(all_reduce fn, rank, world) of the initialised process group.  RCCL ("nccl") reduces the
+    device tensor in place over xGMI; gloo (CPU tests, multi-rank rehearsals sharing one card)
+    reduces a host copy."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        return lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM), dist.get_rank(), dist.get_world_size()
+        if dist.get_backend() == "gloo":
+            def ar(t):
+                h = t.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.SUM)
+                t.copy_(h)
+        else:
+            def ar(t):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return ar, dist.get_rank(), dist.get_world_size()
     return None, 0, 1
 
 
@@ -162,6 +173,7 @@ class ComparativeEvaluator:
         ax.legend()
         if save_path:
             fig.savefig(save_path)
+            plt.close(fig)  # saved: do not keep it in pyplot's figure list
         return fig
 
     def plot_ber_comparison(self, save_path=None):
