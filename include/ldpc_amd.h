@@ -145,6 +145,14 @@ typedef struct ldpc_gnn_plan ldpc_gnn_plan;
 #define LDPC_GNN_EARLY_STOP 1 /* cfg5 per-frame early termination (bf16 path; see below) */
 int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_vgroup, int n_cgroups,
                          const int32_t *h_cgroup, ldpc_gnn_plan **out);
+/* General adjacencies: the reference runs a dense bmm with whatever (E x E) matrices it is given
+ * (message_gnn_decoder.py:106-118), after zero-padding / cropping them to E (:93-104).  A CSR plan
+ * takes each side as a CSR matrix (row m: the columns j with A[m][j] != 0, ascending, and the
+ * values; h_*_ptr has E + 1 entries): every message then aggregates sum_j A[m][j] c[j] over its
+ * own row.  fp32 forward only (precision 0); the bf16 path and training need a group plan. */
+int ldpc_gnn_plan_create_csr(int64_t E, const int32_t *h_v_ptr, const int32_t *h_v_col, const float *h_v_val,
+                             const int32_t *h_c_ptr, const int32_t *h_c_col, const float *h_c_val,
+                             ldpc_gnn_plan **out);
 int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p);
 int64_t ldpc_gnn_weights_size(int hidden, int types, int layers);
 int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers,

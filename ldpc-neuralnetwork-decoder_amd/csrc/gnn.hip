@@ -79,6 +79,7 @@ struct GnnLayer {
     // plan
     const int32_t *vgroup, *cgroup, *vg_ptr, *vg_mem, *cg_ptr, *cg_mem;
     const float *inv_v, *inv_c;
+    const float *vg_w, *cg_w;  // weighted plan: member weights (NULL for group plans)
     int Gv, Gc;
     int64_t E, B;
     // group means
@@ -110,13 +111,18 @@ __global__ __launch_bounds__(256) void gnn_group_mean_kernel(GnnLayer P, int H) 
     const int32_t *ptr = isv ? P.vg_ptr : P.cg_ptr;
     const int32_t *mem = isv ? P.vg_mem : P.cg_mem;
     const float inv = isv ? P.inv_v[gg] : P.inv_c[gg];
+    const float *wts = isv ? P.vg_w : P.cg_w;
     float *dst = (isv ? P.Mv + (b * P.Gv + gg) * H : P.Mc + (b * P.Gc + gg) * H);
     const int p0 = ptr[gg], p1 = ptr[gg + 1];
     for (int u = lane; u < H; u += 64) {
         float s = 0.0f;
         for (int p = p0; p < p1; ++p) {
             const int m = mem[p];
-            s += x_feat(P, b, m, u, H) + P.emb[P.msg_type[m] * H + u];
+            const float c = x_feat(P, b, m, u, H) + P.emb[P.msg_type[m] * H + u];
+            if (wts)  // general adjacency (message_gnn_decoder.py:108/118: bmm(A, c)), nonzeros ascending
+                s += wts[p] * c;
+            else
+                s += c;
         }
         dst[u] = s * inv;
     }
@@ -668,10 +674,73 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     return LDPC_OK;
 }
 
+// General adjacencies (message_gnn_decoder.py:93-118: any (E x E) matrix after the reference's
+// zero-pad / crop) as two CSR matrices: row m lists the messages j with A[m, j] != 0, ascending, and
+// their values.  Every message reads aggregation row m of each side, so the MLP kernels run
+// unchanged on rows that are bmm(A, c) instead of group means.
+extern "C" int ldpc_gnn_plan_create_csr(int64_t E, const int32_t *h_v_ptr, const int32_t *h_v_col, const float *h_v_val,
+                                        const int32_t *h_c_ptr, const int32_t *h_c_col, const float *h_c_val,
+                                        ldpc_gnn_plan **out) {
+    if (!out) return fail(LDPC_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (E <= 0 || E > (1 << 30) || !h_v_ptr || !h_c_ptr) return fail(LDPC_EINVAL, "bad GNN CSR plan arguments");
+    const int64_t nv = h_v_ptr[E], nc = h_c_ptr[E];
+    if (h_v_ptr[0] != 0 || h_c_ptr[0] != 0 || nv < 0 || nc < 0 || (nv && (!h_v_col || !h_v_val)) ||
+        (nc && (!h_c_col || !h_c_val)))
+        return fail(LDPC_EINVAL, "bad CSR arrays");
+    for (int64_t m = 0; m < E; ++m)
+        if (h_v_ptr[m + 1] < h_v_ptr[m] || h_c_ptr[m + 1] < h_c_ptr[m]) return fail(LDPC_EINVAL, "CSR row pointers must ascend");
+    for (int64_t i = 0; i < nv; ++i)
+        if (h_v_col[i] < 0 || h_v_col[i] >= E) return fail(LDPC_EINVAL, "CSR column out of range");
+    for (int64_t i = 0; i < nc; ++i)
+        if (h_c_col[i] < 0 || h_c_col[i] >= E) return fail(LDPC_EINVAL, "CSR column out of range");
+    std::vector<int32_t> blob;
+    blob.reserve(2 * E + 2 * (E + 1) + nv + nc);
+    for (int64_t m = 0; m < E; ++m) blob.push_back((int32_t)m);  // vgroup: own row
+    for (int64_t m = 0; m < E; ++m) blob.push_back((int32_t)m);  // cgroup: own row
+    blob.insert(blob.end(), h_v_ptr, h_v_ptr + E + 1);
+    blob.insert(blob.end(), h_v_col, h_v_col + nv);
+    blob.insert(blob.end(), h_c_ptr, h_c_ptr + E + 1);
+    blob.insert(blob.end(), h_c_col, h_c_col + nc);
+    std::vector<float> inv(2 * E, 1.0f), wts;
+    wts.insert(wts.end(), h_v_val, h_v_val + nv);
+    wts.insert(wts.end(), h_c_val, h_c_val + nc);
+    wts.push_back(0.0f);
+    auto *p = new ldpc_gnn_plan();
+    p->E = E;
+    p->Gv = (int)E;
+    p->Gc = (int)E;
+    p->weighted = true;
+    if (hipGetDevice(&p->device) != hipSuccess || hipMalloc(&p->d_tab, blob.size() * 4) != hipSuccess ||
+        hipMalloc(&p->d_inv, inv.size() * 4) != hipSuccess || hipMalloc(&p->d_w, wts.size() * 4) != hipSuccess) {
+        ldpc_gnn_plan_destroy(p);
+        return fail(LDPC_EHIP, "GNN plan allocation failed");
+    }
+    if (hipMemcpy(p->d_tab, blob.data(), blob.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_inv, inv.data(), inv.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_w, wts.data(), wts.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        ldpc_gnn_plan_destroy(p);
+        return fail(LDPC_EHIP, "GNN plan upload failed");
+    }
+    p->vgroup = p->d_tab;
+    p->cgroup = p->vgroup + E;
+    p->vg_ptr = p->cgroup + E;
+    p->vg_mem = p->vg_ptr + E + 1;
+    p->cg_ptr = p->vg_mem + nv;
+    p->cg_mem = p->cg_ptr + E + 1;
+    p->inv_v = p->d_inv;
+    p->inv_c = p->d_inv + E;
+    p->vg_w = p->d_w;
+    p->cg_w = p->d_w + nv;
+    *out = p;
+    return LDPC_OK;
+}
+
 extern "C" int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p) {
     if (!p) return LDPC_OK;
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_inv) (void)hipFree(p->d_inv);
+    if (p->d_w) (void)hipFree(p->d_w);
     if (p->d_gt) (void)hipFree(p->d_gt);
     delete p;
     return LDPC_OK;
@@ -713,6 +782,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     L.vgroup = p->vgroup; L.cgroup = p->cgroup;
     L.vg_ptr = p->vg_ptr; L.vg_mem = p->vg_mem; L.cg_ptr = p->cg_ptr; L.cg_mem = p->cg_mem;
     L.inv_v = p->inv_v; L.inv_c = p->inv_c;
+    L.vg_w = p->vg_w; L.cg_w = p->cg_w;
     L.Gv = p->Gv; L.Gc = p->Gc;
     L.E = p->E; L.B = B;
     L.Mv = w.Mv; L.Mc = w.Mc;
@@ -744,8 +814,10 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H : L.last ? nullptr : (l % 2 == 0) ? w.xa : w.xb;
         L.msg_out = w.msg_out;
         const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
-        L.d1 = H == 64 && gm_tiles() && d1_skip();
-        if (H == 64 && gm_tiles()) {
+        L.d1 = H == 64 && gm_tiles() && d1_skip() && !p->weighted;
+        if (p->weighted)  // general adjacency: weighted rows, one wave per (frame, message row)
+            hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);
+        else if (H == 64 && gm_tiles()) {
             const GtTiles G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles, L.d1 ? p->n_gtiles_v1 : 0};
             const int64_t twaves = B * (int64_t)(G.n_tiles - G.first);
             hipLaunchKernelGGL(gnn_group_mean_tile_kernel, dim3((unsigned)((twaves + 3) / 4)), dim3(256), 0, s, L, G);
@@ -790,6 +862,8 @@ extern "C" int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types
         return fail(LDPC_EUNSUPPORTED, "early termination is implemented on the bf16 path (precision 1)");
     if (B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
+    if (precision == 1 && p->weighted)
+        return fail(LDPC_EUNSUPPORTED, "the bf16 path needs a group plan (clique adjacencies); use precision 0");
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (precision == 1)
         return gnn_bf16_forward(p, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, flags, d_probs,

@@ -11,6 +11,12 @@ struct ldpc_gnn_plan {
     float *d_inv = nullptr;    // 1/|group|: inv_v[Gv] inv_c[Gc]
     const int32_t *vgroup, *cgroup, *vg_ptr, *vg_mem, *cg_ptr, *cg_mem;
     const float *inv_v, *inv_c;
+    // weighted plan (ldpc_gnn_plan_create_csr): aggregation row m of each side is row m of a
+    // general (E x E) adjacency in CSR form, vg_w / cg_w hold the member weights (inv = 1, every
+    // message reads its own row).  Group plans leave these NULL.
+    bool weighted = false;
+    float *d_w = nullptr;
+    const float *vg_w = nullptr, *cg_w = nullptr;
     // bf16 path: "group tiles" of 8 groups of one degree each (var groups first, then check
     // groups, each side sorted by degree), so one wave sums 8 groups with no divergence.
     //   gt_meta[t] = {degree, offset into gt_mem}, gt_grp[8 t + q] = group id (check groups

@@ -837,6 +837,7 @@ extern "C" int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int ty
                                       const float *d_llr, int N, int64_t B, float *d_probs, float *d_saved,
                                       void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     if (hidden <= 0 || hidden > kMaxH || types <= 0 || layers <= 0 || N <= 0 || B < 0)
         return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 64)");
     if (B == 0) return LDPC_OK;
@@ -851,6 +852,7 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
                                  int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
                                  float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     const int H = hidden, T = types, L = layers;
     if (H <= 0 || H > kMaxH || T <= 0 || L <= 0 || N <= 0 || B < 0)
         return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 64)");

@@ -39,6 +39,7 @@ SIGNATURES = {
     "ldpc_philox_raw": (ctypes.c_int, [_U64, ctypes.c_uint32, ctypes.c_uint32, _I64, _P, _P]),
     "ldpc_count_errors": (ctypes.c_int, [_P, ctypes.c_int, _P, _I64, ctypes.c_int, _P, _P]),
     "ldpc_gnn_plan_create": (ctypes.c_int, [_I64, ctypes.c_int, _P, ctypes.c_int, _P, _P]),
+    "ldpc_gnn_plan_create_csr": (ctypes.c_int, [_I64, _P, _P, _P, _P, _P, _P, _P]),
     "ldpc_gnn_plan_destroy": (ctypes.c_int, [_P]),
     "ldpc_gnn_weights_size": (_I64, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "ldpc_gnn_workspace_size": (_I64, [_P, ctypes.c_int, ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int]),
@@ -152,7 +153,11 @@ class NativeGraph:
 
 
 class NativeGnnPlan:
-    """An ldpc_gnn_plan* (variable / check groupings of the E messages) on one device."""
+    """An ldpc_gnn_plan* on one device: the variable / check groupings of the E messages (group
+    means), or -- ``NativeGnnPlan.csr`` -- two general (E, E) adjacencies in CSR form (weighted
+    rows, fp32 forward only)."""
+
+    weighted = False
 
     def __init__(self, vgroup, n_v, cgroup, n_c, device):
         import numpy as np
@@ -163,6 +168,22 @@ class NativeGnnPlan:
         with torch.cuda.device(device):
             check(lib().ldpc_gnn_plan_create(self.E, self.n_v, vg.ctypes.data_as(_P), self.n_c,
                                              cg.ctypes.data_as(_P), ctypes.byref(self._h)))
+
+    @classmethod
+    def csr(cls, E, v_csr, c_csr, device):
+        """v_csr / c_csr = (ptr (E+1,), col (nnz,), val (nnz,)) numpy arrays."""
+        import numpy as np
+        self = cls.__new__(cls)
+        self.E, self.n_v, self.n_c, self.device, self.weighted = int(E), int(E), int(E), device, True
+        arrs = []
+        for ptr, col, val in (v_csr, c_csr):
+            arrs += [np.ascontiguousarray(ptr, dtype=np.int32), np.ascontiguousarray(col, dtype=np.int32),
+                     np.ascontiguousarray(val, dtype=np.float32)]
+        self._keep = arrs
+        self._h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            check(lib().ldpc_gnn_plan_create_csr(self.E, *[a.ctypes.data_as(_P) for a in arrs], ctypes.byref(self._h)))
+        return self
 
     @property
     def handle(self):

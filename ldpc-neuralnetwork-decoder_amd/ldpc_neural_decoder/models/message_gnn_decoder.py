@@ -13,9 +13,10 @@ Compatibility notes (each mirrors the reference line cited):
   * ``message_types`` None -> all zeros (:240-241); shorter/longer -> zero-pad/truncate (:68-78);
     values clamped to [0, T-1] (:81).
   * ``var_to_check_adjacency`` / ``check_to_var_adjacency`` are required (None fails like the
-    reference, :93).  They must be message adjacencies of the kind TannerToMessageGraph builds
-    (normalized cliques of messages sharing a variable / a check, :410-469); the groups are read
-    off the matrix once and verified by probing (A @ r == group-mean(r)).
+    reference, :93).  A mis-sized pair is zero-padded / cropped as :92-104 does.  The
+    normalized cliques TannerToMessageGraph builds (:410-469) are recognised (groups read off the
+    matrix once, verified by probing A @ r == group-mean(r)) and aggregated as group means; any
+    other matrix runs as a general sparse bmm(A, c) over its nonzeros (fp32 forward only).
   * the unused ``output_layer`` (:188) is kept so state_dicts round-trip.
   * with grad enabled and trainable parameters, forward() runs the fp32 training path (every
     layer's features saved for the HIP backward, csrc/gnn_train.hip); otherwise the inference
@@ -92,24 +93,18 @@ def _io_mapping(mapping, E, N_vars, device):
     return m.to(torch.int32).contiguous()
 
 
-def _groups_from_adjacency(A, E):
+def _clique_groups(A, E):
     """Read the message groups off a normalized clique adjacency (message_gnn_decoder.py:410-469).
 
-    Returns (labels (E,) int64 numpy, number of groups).  The labels are the first nonzero column
-    of every row, renumbered densely; the matrix is then probed with random vectors to check that
-    A @ r equals the group mean of r (the only property the decoder relies on)."""
-    tagged = getattr(A, "_ldpc_groups", None)
-    if tagged is not None:
-        return tagged
-    if A is None:
-        raise AttributeError("'NoneType' object has no attribute 'size'")
-    if A.dim() != 2 or A.shape[0] != E or A.shape[1] != E:
-        raise NotImplementedError(
-            f"adjacency of shape {tuple(A.shape)} for {E} messages: the reference's pad/crop "
-            "resize (message_gnn_decoder.py:93-104) is not supported")
+    Returns (labels (E,) int64 numpy, number of groups), or None when A is not such a matrix.  The
+    labels are the first nonzero column of every row, renumbered densely; the matrix is then
+    probed with random vectors to check that A @ r equals the group mean of r (the only property
+    the group-mean kernels rely on)."""
     dev = A.device  # setup-time structure probe, on whichever device holds the matrix
     Ad = A.to(torch.float32)
     nz = Ad != 0
+    if not bool(nz.any(dim=1).all()):
+        return None  # an all-zero row (e.g. after the reference's zero-pad) is no clique
     first = torch.argmax(nz.to(torch.int8), dim=1)
     uniq, labels = torch.unique(first, return_inverse=True)
     n = int(uniq.numel())
@@ -121,15 +116,76 @@ def _groups_from_adjacency(A, E):
         want = (sums / cnt)[labels]
         got = Ad @ r
         if not torch.allclose(got, want, rtol=1e-4, atol=1e-5):
-            raise NotImplementedError(
-                "adjacency is not a normalized clique adjacency of message groups; only the "
-                "TannerToMessageGraph construction (message_gnn_decoder.py:410-469) is supported")
-    out = (labels.cpu().numpy().astype(np.int64), n)
+            return None
+    return labels.cpu().numpy().astype(np.int64), n
+
+
+def _csr_of(A):
+    """(ptr (E+1,), col, val) of a dense matrix: row m lists its nonzero columns ascending."""
+    Ad = A.detach().to("cpu", torch.float32)
+    rows, cols = torch.nonzero(Ad, as_tuple=True)  # row-major: rows ascending, cols ascending in a row
+    ptr = torch.zeros(Ad.shape[0] + 1, dtype=torch.int64)
+    ptr[1:] = torch.cumsum(torch.bincount(rows, minlength=Ad.shape[0]), 0)
+    return ptr.numpy(), cols.numpy(), Ad[rows, cols].numpy()
+
+
+def _resize_like_reference(Av, Ac, E):
+    """message_gnn_decoder.py:92-104: when the var adjacency is not (E, E), both matrices are
+    replaced by (E, E) zeros holding the top-left min(rows of A_v, E) block of each (the check
+    matrix is resized by the var matrix's size, exactly as the reference does)."""
+    if Av.size(0) == E and Av.size(1) == E:
+        return Av, Ac
+    new_v = torch.zeros((E, E), device=Av.device)
+    new_c = torch.zeros((E, E), device=Av.device)
+    k = min(Av.size(0), E)
+    new_v[:k, :k] = Av[:k, :k]
+    new_c[:k, :k] = Ac[:k, :k]
+    return new_v, new_c
+
+
+def _aggregation_specs(Av, Ac, E):
+    """The two aggregation specs the native plan is built from, per side either
+    ("groups", labels, n) -- a normalized clique adjacency, aggregated as group means -- or
+    ("csr", ptr, col, val) -- any other matrix, aggregated as bmm(A, c) over its nonzeros.
+    Cached on the caller's tensors (the reference rebuilds nothing per call either)."""
+    if Av is None or Ac is None:
+        raise AttributeError("'NoneType' object has no attribute 'size'")  # as MGD:93 fails
+    cached = getattr(Av, "_ldpc_specs", None)
+    if cached is not None and cached[0] == E and cached[1] is Ac:
+        return cached[2]
+    tagged = getattr(Av, "_ldpc_groups", None), getattr(Ac, "_ldpc_groups", None)
+    if tagged[0] is not None and tagged[1] is not None and Av.shape == (E, E) and Ac.shape == (E, E):
+        specs = (("groups",) + tuple(tagged[0]), ("groups",) + tuple(tagged[1]))
+    else:
+        v, c = _resize_like_reference(Av, Ac, E)
+        if c.dim() != 2 or c.shape[0] != E or c.shape[1] != E:
+            raise RuntimeError(f"check_to_var_adjacency of shape {tuple(c.shape)} cannot multiply {E} messages")
+        out = []
+        for A in (v, c):
+            g = _clique_groups(A, E)
+            out.append(("groups",) + g if g is not None else ("csr",) + _csr_of(A))
+        specs = tuple(out)
+        if specs[0][0] != specs[1][0]:  # a mixed pair runs as two CSR matrices
+            specs = tuple(s_ if s_[0] == "csr" else ("csr",) + _csr_of(A) for s_, A in zip(specs, (v, c)))
     try:
-        A._ldpc_groups = out
+        Av._ldpc_specs = (E, Ac, specs)
     except Exception:
         pass
-    return out
+    return specs
+
+
+def _groups_from_adjacency(A, E):
+    """The (labels, count) groups of a normalized clique adjacency of E messages (see
+    _clique_groups); NotImplementedError for any other matrix."""
+    tagged = getattr(A, "_ldpc_groups", None)
+    if tagged is not None:
+        return tagged
+    if A is None:
+        raise AttributeError("'NoneType' object has no attribute 'size'")
+    g = _clique_groups(A, E) if A.dim() == 2 and A.shape == (E, E) else None
+    if g is None:
+        raise NotImplementedError("not a normalized clique adjacency of message groups")
+    return g
 
 
 class MessageGNNDecoder(nn.Module):
@@ -182,21 +238,30 @@ class MessageGNNDecoder(nn.Module):
             self._blob, self._blob_key = blob, key
         return self._blob
 
-    def _plan(self, vlab, n_v, clab, n_c, device):
-        key = (str(device), vlab.tobytes(), clab.tobytes())
+    def _plan(self, vspec, cspec, device):
+        """vspec / cspec: (labels, count) or ("groups", labels, count) or ("csr", ptr, col, val)."""
+        norm = lambda sp: sp if isinstance(sp[0], str) else ("groups",) + tuple(sp)
+        vspec, cspec = norm(vspec), norm(cspec)
+        key = (str(device), vspec[0]) + tuple(np.asarray(a).tobytes() for a in vspec[1:] + cspec[1:])
         plan = self._plans.get(key)
         if plan is None:
-            plan = N.NativeGnnPlan(vlab, n_v, clab, n_c, device)
+            if vspec[0] == "groups" and cspec[0] == "groups":
+                plan = N.NativeGnnPlan(vspec[1], vspec[2], cspec[1], cspec[2], device)
+            else:
+                plan = N.NativeGnnPlan.csr(self.num_messages, vspec[1:], cspec[1:], device)
             self._plans = {key: plan}  # keep one plan; graphs rarely change
         return plan
 
     def native_forward(self, llr, io_map, types, vgroups, cgroups, chunk=None):
-        """llr (B, N) on a HIP device; io_map/types (E,) int32; groups = (labels, count)."""
+        """llr (B, N) on a HIP device; io_map/types (E,) int32; vgroups / cgroups = (labels, count)
+        group specs, or ("csr", ptr, col, val) general adjacencies (fp32 only)."""
         dev = llr.device
         B, Nv = llr.shape
         T = self.gnn_layers[0].message_type_embeddings.shape[0]
         L = len(self.gnn_layers)
-        plan = self._plan(vgroups[0], vgroups[1], cgroups[0], cgroups[1], dev)
+        plan = self._plan(vgroups, cgroups, dev)
+        if plan.weighted and self.precision != "fp32":
+            raise NotImplementedError("a general (non-clique) adjacency runs on the fp32 path only")
         blob = self._weights_blob(dev)
         prec = 1 if self.precision == "bf16" else 0
         flags = N.LDPC_GNN_EARLY_STOP if self.early_termination else 0
@@ -230,8 +295,7 @@ class MessageGNNDecoder(nn.Module):
         home = input_llr.device
         dev = N.device_of(input_llr)
         E = self.num_messages
-        vg = _groups_from_adjacency(var_to_check_adjacency, E)
-        cg = _groups_from_adjacency(check_to_var_adjacency, E)
+        vg, cg = _aggregation_specs(var_to_check_adjacency, check_to_var_adjacency, E)
         llr = input_llr.to(dev, torch.float32).contiguous()
         io_map = _io_mapping(message_to_var_mapping, E, llr.shape[1], dev)
         T = self.gnn_layers[0].message_type_embeddings.shape[0]
@@ -240,7 +304,10 @@ class MessageGNNDecoder(nn.Module):
         if self.precision == "fp32" and torch.is_grad_enabled() and any(p.requires_grad for p in params):
             # training: fp32 forward that saves every layer's features + the HIP backward
             # (precision="bf16" is an inference setting: it always takes the no-grad path)
-            plan = self._plan(vg[0], vg[1], cg[0], cg[1], dev)
+            plan = self._plan(vg, cg, dev)
+            if plan.weighted:
+                raise NotImplementedError("training through a general (non-clique) adjacency is not supported; "
+                                          "use the TannerToMessageGraph adjacencies")
             probs = _NativeGnnTrain.apply(self, llr, io_map, types, plan, *params)
         else:
             with torch.no_grad():

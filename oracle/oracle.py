@@ -168,6 +168,46 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
     return probs
 
 
+def gnn_forward_dense(sd, llr, msg_var_io, num_vars, Av, Ac, types=None):
+    """MessageGNNDecoder.forward restated with the reference's own aggregation: dense
+    bmm(A, x + emb) with whatever adjacencies are given, zero-padded / cropped to E as
+    message_gnn_decoder.py:92-104 does (MessageGNNLayer.forward :51-129, decoder :190-317).  Used
+    to pin the general-adjacency path; gnn_forward above is the segment-mean form of the same math
+    for the TannerToMessageGraph cliques."""
+    import torch
+
+    llr = torch.as_tensor(llr, dtype=torch.float32)
+    mv = torch.as_tensor(msg_var_io, dtype=torch.long)
+    B, E = llr.shape[0], mv.numel()
+    n_layers = len({k.split(".")[1] for k in sd if k.startswith("gnn_layers.")})
+    x = llr[:, mv].unsqueeze(-1) * sd["input_embedding.weight"][:, 0] + sd["input_embedding.bias"]
+    t = torch.zeros(E, dtype=torch.long) if types is None else torch.as_tensor(types).long()
+    Av, Ac = torch.as_tensor(Av, dtype=torch.float32), torch.as_tensor(Ac, dtype=torch.float32)
+    if Av.size(0) != E or Av.size(1) != E:  # :92-104
+        nv, nc = torch.zeros(E, E), torch.zeros(E, E)
+        k = min(Av.size(0), E)
+        nv[:k, :k] = Av[:k, :k]
+        nc[:k, :k] = Ac[:k, :k]
+        Av, Ac = nv, nc
+
+    def mlp(p, z):
+        h = torch.relu(z @ sd[p + ".0.weight"].T + sd[p + ".0.bias"])
+        return h @ sd[p + ".2.weight"].T + sd[p + ".2.bias"]
+
+    for i in range(n_layers):
+        p = f"gnn_layers.{i}."
+        emb = sd[p + "message_type_embeddings"]
+        c = x + emb[t.clamp(0, emb.shape[0] - 1)]
+        a = torch.bmm(Av.unsqueeze(0).expand(B, -1, -1), c)
+        b = torch.bmm(Ac.unsqueeze(0).expand(B, -1, -1), c)
+        y = mlp(p + "var_to_check_update", torch.cat([c, a], 2)) + mlp(p + "check_to_var_update", torch.cat([c, b], 2))
+        x = y + x if i > 0 else y
+    last = f"gnn_layers.{n_layers - 1}.output_projection."
+    out = (x @ sd[last + "weight"][0]) + sd[last + "bias"][0]
+    var_llrs = torch.zeros(B, num_vars).index_add_(1, mv, out)
+    return torch.sigmoid(var_llrs + llr)
+
+
 # --------------------------------------------------------------------------- index-gather layers
 # Restatement of models/layers.py:5-208 and utils/ldpc_utils.py:5-95 (var-major edge mapping),
 # in torch ops so that autograd gives the reference gradients (test infrastructure only).

@@ -121,3 +121,20 @@ def test_oracle_per_frame_mode_is_consistent(oracle_mod):
         assert np.array_equal(bits[b], ref[0])
         if iters[b] < 8:
             assert oracle_mod.syndrome_valid(g, bits[b:b + 1])[0]
+
+
+def test_dense_gnn_oracle_matches_reference():
+    """oracle.gnn_forward_dense (the reference's dense-bmm aggregation, used to pin the general-
+    adjacency path) on the normalized clique adjacencies reproduces the reference's probs."""
+    import oracle as oracle_py
+    from ldpc_neural_decoder.models.message_gnn_decoder import TannerToMessageGraph
+    from ldpc_neural_decoder.utils import expand_base_matrix, load_base_matrix
+    from conftest import code_path
+    c, f = golden("codes_z4.npz"), golden("gnn_z4.npz")
+    sd = {k[3:]: torch.from_numpy(f[k]) for k in f.files if k.startswith("w__")}
+    H = expand_base_matrix(load_base_matrix(code_path(4)), 4)
+    conv = TannerToMessageGraph(H)
+    ev = c["messages"][:, 0]
+    p = oracle_py.gnn_forward_dense(sd, f["llr"], ev, int(c["H_shape"][1]), conv.var_to_check_adjacency,
+                                    conv.check_to_var_adjacency, c["message_types"]).numpy()
+    np.testing.assert_allclose(p, f["probs"], atol=2e-6)
