@@ -221,18 +221,30 @@ def cpu_baseline(workload, z, iters, target_s):
                 "sample": f"{b} frames, BG2 Z={z} (E={E} edge LLRs), {iters} iterations of the index-gather "
                           f"layers, oracle (torch CPU) on {cpu} with {torch.get_num_threads()} threads, {dt:.1f} s"}
     algo = "minsum" if kind == "minsum" else "bp"
-    b = 16
-    t0 = time.perf_counter()
-    oracle.flood_decode(g, sample(b), algo, iters, 0.75, 0)
-    dt = max(time.perf_counter() - t0, 1e-6)
-    b = int(min(1 << 16, max(16, b * target_s / dt)))
-    x = sample(b)
-    t0 = time.perf_counter()
-    oracle.flood_decode(g, x, algo, iters, 0.75, 0)
-    dt = time.perf_counter() - t0
-    return {"value": b / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
-            "sample": f"{b} frames, BG2 Z={z}, {algo} {iters} it, {snr} dB, oracle/ldpc_oracle.c "
-                      f"single-threaded on {cpu} (os.cpu_count()={os.cpu_count()}), {dt:.1f} s"}
+
+    def timed(threads, seconds):
+        oracle.set_threads(threads)
+        b = 16 * threads
+        t0 = time.perf_counter()
+        oracle.flood_decode(g, sample(b), algo, iters, 0.75, 0)
+        dt = max(time.perf_counter() - t0, 1e-6)
+        b = int(min(1 << 18, max(16 * threads, b * seconds / dt)))
+        x = sample(b)
+        t0 = time.perf_counter()
+        oracle.flood_decode(g, x, algo, iters, 0.75, 0)
+        return b, time.perf_counter() - t0
+
+    # all cores of this process's share (OMP_NUM_THREADS: 16 per GPU on the bench boxes, whose
+    # os.cpu_count() counts the whole machine) and one core, the literal loop order in C both times
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1
+    b1, dt1 = timed(1, target_s / 3)
+    bn, dtn = timed(threads, target_s)
+    oracle.set_threads(1)
+    return {"value": bn / dtn, "unit": "codewords/s", "cores": threads, "kind": "port",
+            "value_1core": b1 / dt1,
+            "sample": f"{bn} frames, BG2 Z={z}, {algo} {iters} it, {snr} dB, oracle/ldpc_oracle.c (the "
+                      f"reference's loop order) with an OpenMP frame loop on {threads} threads of {cpu} "
+                      f"(os.cpu_count()={os.cpu_count()}), {dtn:.1f} s; 1 thread: {b1} frames in {dt1:.1f} s"}
 
 
 def main():

@@ -44,7 +44,15 @@ def lib():
         _lib.ldpc_oracle_expand.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         _lib.ldpc_oracle_syndrome.argtypes = [ctypes.c_int, P, P, ctypes.c_int, P,
                                               ctypes.c_int64, P]
+        _lib.ldpc_oracle_set_threads.argtypes = [ctypes.c_int]
+        _lib.ldpc_oracle_set_threads.restype = ctypes.c_int
     return _lib
+
+
+def set_threads(n):
+    """Host threads of flood_decode's frame loop (OpenMP); returns the count in use.  Only the
+    timed CPU baseline (bench.py) uses more than 1."""
+    return lib().ldpc_oracle_set_threads(int(n))
 
 
 def _p(a):
