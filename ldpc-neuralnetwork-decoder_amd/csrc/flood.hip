@@ -1222,6 +1222,212 @@ __global__ __launch_bounds__(512) void batch_emit_kernel(FloodTables T, const ui
 
 __global__ void fill_i32_kernel(int32_t *p, int32_t v) { *p = v; }
 
+// ---------------------------------------------------------------- streaming decoder (any graph)
+// For graphs whose messages do not fit a CU's LDS (lifting sizes that do not divide 64 leave the
+// QC detection at Z = 1; large Z; big non-QC codes): the same flooding iteration with every
+// message in HBM, laid out edge-major and frame-fastest (msg[e][b]), so that the 64 lanes of a
+// wave -- 64 consecutive frames of one row / column -- load and store 256 contiguous bytes.  One
+// launch per phase; each thread owns one (check, frame) or (variable, frame).  The float32
+// operation sequences are the LDS kernels' (= the reference's), so results are bit-identical
+// (min-sum) / identical (BP) across the two paths.  Early stop keeps the reference's rules with
+// device flags: a finished batch (LDPC_ES_BATCH) or frame (LDPC_ES_FRAME) skips the later launches.
+struct StreamArgs {
+    const int32_t *chk_ptr, *ev, *var_ptr, *var_edge;
+    int M, N;
+    int64_t E, B;
+    float *msg;        // [E][B] v2c / c2v in place
+    float *llrT;       // [N][B]
+    uint8_t *bitsT;    // [N][B] hard decisions of the latest iteration
+    uint8_t *done;     // [B] LDPC_ES_FRAME: frame frozen
+    int32_t *iters;    // [B] LDPC_ES_FRAME: iterations of a frozen frame
+    int32_t *ctl;      // [0] batch stopped  [1] batch iterations
+    int32_t *invalid;  // [max_iter] LDPC_ES_BATCH: frames failing H x = 0 after each iteration
+    float alpha;
+    int es;
+};
+
+__device__ __forceinline__ bool stream_skip(const StreamArgs &S, int64_t b) {
+    if (S.es == LDPC_ES_BATCH) return S.ctl[0] != 0;
+    if (S.es == LDPC_ES_FRAME) return S.done[b] != 0;
+    return false;
+}
+
+// (B, N) -> (N, B) through 64 x 64 LDS tiles
+__global__ __launch_bounds__(256) void stream_transpose_llr_kernel(const float *__restrict__ llr, int64_t B, int N,
+                                                                   float *__restrict__ llrT) {
+    __shared__ float t[64][65];
+    const int64_t b0 = (int64_t)blockIdx.x * 64;
+    const int v0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4)
+        if (b0 + r < B && v0 + tx < N) t[r][tx] = llr[(b0 + r) * N + v0 + tx];
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4)
+        if (v0 + r < N && b0 + tx < B) llrT[(int64_t)(v0 + r) * B + b0 + tx] = t[tx][r];
+}
+
+__global__ __launch_bounds__(256) void stream_init_kernel(StreamArgs S) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= S.E * S.B) return;
+    const int64_t e = t / S.B, b = t - e * S.B;
+    S.msg[t] = S.llrT[(int64_t)S.ev[e] * S.B + b];  // v2c <- llr (traditional_decoders.py:199-202)
+}
+
+template <int ALGO>
+__global__ __launch_bounds__(256) void stream_check_kernel(StreamArgs S) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)S.M * S.B) return;
+    const int64_t i = t / S.B, b = t - i * S.B;
+    if (stream_skip(S, b)) return;
+    const int e0 = S.chk_ptr[i], e1 = S.chk_ptr[i + 1];
+    float *m = S.msg + b;
+    if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+        MinSumStats st;  // exact torch.sign / NaN semantics (traditional_decoders.py:207-232)
+        for (int e = e0; e < e1; ++e) st.add(e - e0, m[(int64_t)e * S.B]);
+        for (int e = e0; e < e1; ++e) {
+            float *q = m + (int64_t)e * S.B;
+            *q = st.c2v(e - e0, *q, S.alpha);
+        }
+    } else {
+        // c2v_e = 2 atanh(prod_{f != e} tanh(v_f / 2)), product from 1.0 ascending (:72-81).
+        // In place: edge e's output is written after the products of edges <= e were formed, and
+        // edges > e still need v_e, so keep the row's tanh values in a small register window and
+        // write outputs one edge behind: out_e only after every product that reads v_e is done,
+        // i.e. after the whole row -- rows longer than kStreamDc fall back to a second pass that
+        // recomputes from the untouched inputs (the outputs go to the row's tail buffer first).
+        constexpr int kStreamDc = 32;
+        const int dc = e1 - e0;
+        if (dc <= kStreamDc) {
+            float th[kStreamDc], out[kStreamDc];
+            for (int e = 0; e < dc; ++e) th[e] = tanh_half(m[(int64_t)(e0 + e) * S.B]);
+            for (int e = 0; e < dc; ++e) {
+                float prod = 1.0f;
+                for (int f = 0; f < dc; ++f)
+                    if (f != e) prod = prod * th[f];
+                out[e] = two_atanh(prod);
+            }
+            for (int e = 0; e < dc; ++e) m[(int64_t)(e0 + e) * S.B] = out[e];
+        }  // longer rows are refused on the host (ldpc_flood_decode: LDPC_EUNSUPPORTED)
+    }
+}
+
+// v2c_e = llr + sum_{e' != e} c_e' in ascending check order; APP = llr + all (traditional_decoders.py:235-252)
+__global__ __launch_bounds__(256) void stream_var_kernel(StreamArgs S, int write) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)S.N * S.B) return;
+    const int64_t j = t / S.B, b = t - j * S.B;
+    if (stream_skip(S, b)) return;
+    const int p0 = S.var_ptr[j], p1 = S.var_ptr[j + 1];
+    const float l = S.llrT[t];
+    float *m = S.msg + b;
+    constexpr int kWin = 32;  // c2v values held in registers (in-place update needs them all first)
+    const int dv = p1 - p0;
+    float app = l;
+    if (dv <= kWin) {
+        float c[kWin];
+        for (int p = 0; p < dv; ++p) c[p] = m[(int64_t)S.var_edge[p0 + p] * S.B];
+        if (write) {
+            float P = l;  // prefix P_p = llr + c_0 + ... + c_{p-1}, then the tail adds
+            for (int p = 0; p < dv; ++p) {
+                float acc = P;
+                for (int q = p + 1; q < dv; ++q) acc = acc + c[q];
+                m[(int64_t)S.var_edge[p0 + p] * S.B] = acc;
+                P = P + c[p];
+            }
+            app = P;
+        } else {
+            for (int p = 0; p < dv; ++p) app = app + c[p];
+        }
+    }  // longer columns are refused on the host (ldpc_flood_decode: LDPC_EUNSUPPORTED)
+    S.bitsT[t] = app < 0.0f;  // NaN < 0 is false -> 0
+}
+
+// per-frame syndrome after an iteration: LDPC_ES_FRAME freezes valid frames, LDPC_ES_BATCH
+// counts the invalid ones for stream_batch_step_kernel
+__global__ __launch_bounds__(256) void stream_syndrome_kernel(StreamArgs S, int it) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int bad = 0;
+    if (b < S.B && !stream_skip(S, b)) {
+        for (int i = 0; i < S.M && !bad; ++i) {
+            int p = 0;
+            for (int e = S.chk_ptr[i]; e < S.chk_ptr[i + 1]; ++e) p ^= S.bitsT[(int64_t)S.ev[e] * S.B + b];
+            bad = p;
+        }
+        if (S.es == LDPC_ES_FRAME && !bad) {
+            S.done[b] = 1;
+            S.iters[b] = it + 1;
+        }
+    } else {
+        bad = 0;
+    }
+    if (S.es == LDPC_ES_BATCH) {
+        const uint64_t m = __ballot(bad);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&S.invalid[it], (int)__popcll(m));
+    }
+}
+
+__global__ void stream_batch_step_kernel(StreamArgs S, int it) {
+    if (S.ctl[0] == 0 && S.invalid[it] == 0) {  // every frame valid: the reference returns (:104-107)
+        S.ctl[0] = 1;
+        S.ctl[1] = it + 1;
+    }
+}
+
+// (N, B) decisions -> (B, N) output bits, per-frame iteration counts and counter rows
+__global__ __launch_bounds__(256) void stream_emit_kernel(StreamArgs S, int max_iter, int out_dtype, void *bits,
+                                                          int32_t *iters_out, uint32_t *partials) {
+    __shared__ uint8_t tile[64][65];
+    __shared__ uint32_t errs[64];
+    const int64_t b0 = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    if (threadIdx.x < 64) errs[threadIdx.x] = 0;
+    for (int v0 = 0; v0 < S.N; v0 += 64) {
+        __syncthreads();
+        for (int r = ty; r < 64; r += 4)
+            tile[r][tx] = (v0 + r < S.N && b0 + tx < S.B) ? S.bitsT[(int64_t)(v0 + r) * S.B + b0 + tx] : 0;
+        __syncthreads();
+        for (int r = ty; r < 64; r += 4) {
+            const int64_t b = b0 + r;
+            if (b < S.B && v0 + tx < S.N) {
+                const int bit = tile[tx][r];
+                put_bit(bits, out_dtype, b * S.N + v0 + tx, bit);
+                if (bit) atomicAdd(&errs[r], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int64_t b = b0 + threadIdx.x;
+        uint32_t be = 0, fe = 0, fr = 0, it = 0;
+        if (b < S.B) {
+            int n = max_iter;
+            if (S.es == LDPC_ES_BATCH && S.ctl[0]) n = S.ctl[1];
+            if (S.es == LDPC_ES_FRAME && S.done[b]) n = S.iters[b];
+            if (iters_out) iters_out[b] = n;
+            be = errs[threadIdx.x];
+            fe = be > 0;
+            fr = 1;
+            it = (uint32_t)n;
+        }
+        uint32_t mx = it;
+        for (int off = 32; off > 0; off >>= 1) {
+            be += __shfl_xor(be, off, 64);
+            fe += __shfl_xor(fe, off, 64);
+            fr += __shfl_xor(fr, off, 64);
+            it += __shfl_xor(it, off, 64);
+            mx = max(mx, (uint32_t)__shfl_xor(mx, off, 64));
+        }
+        if (threadIdx.x == 0 && partials) {
+            uint32_t *row = partials + (int64_t)blockIdx.x * kPartRow;
+            row[0] = be;
+            row[1] = fe;
+            row[2] = fr;
+            row[3] = it;
+            row[4] = mx;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- host side
 #ifndef LDPC_FLOOD_KERNELS_ONLY  // (defined by kernel-only experiment builds)
 namespace {
@@ -1264,6 +1470,74 @@ FloodWs flood_ws(const ldpc_graph *g, int64_t B, int max_iter, int early_stop, v
     }
     w.bytes = (int64_t)off;
     return w;
+}
+
+constexpr int kStreamMaxDeg = 32;  // register windows of stream_check_kernel (BP) / stream_var_kernel
+
+bool use_stream(const ldpc_graph *g, int es) {
+    if (!g->lds_ok || flood_lds_bytes(g, es) > kLdsMax) return true;
+    const char *e = std::getenv("LDPC_FLOOD_STREAM");  // force the streaming kernels (tests, A/B)
+    return e && std::atoi(e) != 0;
+}
+
+struct StreamWs {
+    float *msg, *llrT;
+    uint8_t *bitsT, *done;
+    int32_t *iters, *ctl, *invalid;
+    uint32_t *partials;
+    int64_t bytes;
+};
+
+StreamWs stream_ws(const ldpc_graph *g, int64_t B, int max_iter, void *base) {
+    StreamWs w{};
+    char *p = static_cast<char *>(base);
+    size_t off = 0;
+    auto take = [&](size_t n) { char *q = p ? p + off : nullptr; off += align256(n); return q; };
+    w.msg = reinterpret_cast<float *>(take((size_t)g->E * B * 4));
+    w.llrT = reinterpret_cast<float *>(take((size_t)g->N * B * 4));
+    w.bitsT = reinterpret_cast<uint8_t *>(take((size_t)g->N * B));
+    w.done = reinterpret_cast<uint8_t *>(take((size_t)B));
+    w.iters = reinterpret_cast<int32_t *>(take((size_t)B * 4));
+    w.ctl = reinterpret_cast<int32_t *>(take(64));
+    w.invalid = reinterpret_cast<int32_t *>(take((size_t)max_iter * 4));
+    w.partials = reinterpret_cast<uint32_t *>(take((size_t)((B + 63) / 64) * kPartRow * 4));
+    w.bytes = (int64_t)off;
+    return w;
+}
+
+template <int ALGO>
+int run_stream(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha, int es, int out_dtype,
+               void *bits, int32_t *iters_out, uint64_t *counters, int32_t *batch_iters, void *work, hipStream_t s) {
+    const StreamWs w = stream_ws(g, B, max_iter, work);
+    StreamArgs S{g->chk_ptr, g->ev, g->var_ptr, g->var_edge, g->M, g->N, g->E, B, w.msg, w.llrT, w.bitsT, w.done,
+                 w.iters, w.ctl, w.invalid, alpha, es};
+    LDPC_HIP(hipMemsetAsync(w.done, 0, (size_t)B, s));
+    LDPC_HIP(hipMemsetAsync(w.ctl, 0, 64, s));
+    LDPC_HIP(hipMemsetAsync(w.invalid, 0, (size_t)max_iter * 4, s));
+    const dim3 tgrid((unsigned)((B + 63) / 64), (unsigned)((g->N + 63) / 64));
+    hipLaunchKernelGGL(stream_transpose_llr_kernel, tgrid, dim3(256), 0, s, llr, B, g->N, w.llrT);
+    auto blocks = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    hipLaunchKernelGGL(stream_init_kernel, blocks(g->E * B), dim3(256), 0, s, S);
+    LDPC_CHECK_LAUNCH("stream init");
+    for (int it = 0; it < max_iter; ++it) {
+        hipLaunchKernelGGL(stream_check_kernel<ALGO>, blocks((int64_t)g->M * B), dim3(256), 0, s, S);
+        hipLaunchKernelGGL(stream_var_kernel, blocks((int64_t)g->N * B), dim3(256), 0, s, S, it < max_iter - 1 ? 1 : 0);
+        if (es != LDPC_ES_OFF) {
+            hipLaunchKernelGGL(stream_syndrome_kernel, blocks(B), dim3(256), 0, s, S, it);
+            if (es == LDPC_ES_BATCH) hipLaunchKernelGGL(stream_batch_step_kernel, dim3(1), dim3(1), 0, s, S, it);
+        }
+        LDPC_CHECK_LAUNCH("stream iteration");
+    }
+    const bool want = counters || batch_iters;
+    hipLaunchKernelGGL(stream_emit_kernel, dim3((unsigned)((B + 63) / 64)), dim3(256), 0, s, S, max_iter, out_dtype,
+                       bits, iters_out, want ? w.partials : nullptr);
+    LDPC_CHECK_LAUNCH("stream emit");
+    if (!want) return LDPC_OK;
+    // batch_iters: ES off was set before the launch; otherwise the largest per-frame count
+    hipLaunchKernelGGL(counters_reduce_kernel, dim3(1), dim3(1024), 0, s, w.partials, (B + 63) / 64, counters,
+                       es == LDPC_ES_OFF ? nullptr : batch_iters, nullptr);
+    LDPC_CHECK_LAUNCH("counters_reduce_kernel");
+    return LDPC_OK;
 }
 
 template <int ALGO, int ES>
@@ -1345,6 +1619,7 @@ using namespace ldpc;
 extern "C" int64_t ldpc_flood_workspace_size(const ldpc_graph *g, int64_t B, int max_iter, int early_stop) {
     if (!g || B < 0 || max_iter < 0) return fail(LDPC_EINVAL, "bad arguments");
     if (B == 0 || max_iter == 0) return 0;
+    if (use_stream(g, early_stop)) return stream_ws(g, B, max_iter, nullptr).bytes;
     return flood_ws(g, B, max_iter, early_stop, nullptr).bytes;
 }
 
@@ -1360,11 +1635,11 @@ extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_l
     if (max_iter < 1 || max_iter > 1024) return fail(LDPC_EINVAL, "max_iter must be in [1, 1024]");
     if (B == 0) return LDPC_OK;
     if (!d_llr || !d_bits) return fail(LDPC_EINVAL, "llr / bits is NULL");
-    if (flood_lds_bytes(g, early_stop) > kLdsMax)
-        return fail(LDPC_EUNSUPPORTED, "graph too large for the LDS-resident decoder (" +
-                                           std::to_string(g->nslots) + " slots)");
-    // scratch is needed for the batch-global stop and for any counter / batch-iteration output
-    if (early_stop == LDPC_ES_BATCH || d_counters || (d_batch_iters && early_stop == LDPC_ES_FRAME)) {
+    const bool streaming = use_stream(g, early_stop);
+    if (streaming && (g->max_dv > kStreamMaxDeg || (algo == LDPC_ALGO_BP && g->max_dc > kStreamMaxDeg)))
+        return fail(LDPC_EUNSUPPORTED, "streaming decoder: node degree above " + std::to_string(kStreamMaxDeg));
+    // scratch is needed by the streaming decoder, the batch-global stop and any counter output
+    if (streaming || early_stop == LDPC_ES_BATCH || d_counters || (d_batch_iters && early_stop == LDPC_ES_FRAME)) {
         const int64_t need = ldpc_flood_workspace_size(g, B, max_iter, early_stop);
         if (!d_work || work_bytes < need)
             return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes");
@@ -1374,6 +1649,12 @@ extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_l
         hipLaunchKernelGGL(fill_i32_kernel, dim3(1), dim3(1), 0, s, d_batch_iters, max_iter);
         LDPC_CHECK_LAUNCH("fill");
     }
+    if (streaming)
+        return algo == LDPC_ALGO_MINSUM
+                   ? run_stream<LDPC_ALGO_MINSUM>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, d_iters,
+                                                  d_counters, d_batch_iters, d_work, s)
+                   : run_stream<LDPC_ALGO_BP>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, d_iters,
+                                              d_counters, d_batch_iters, d_work, s);
     return algo == LDPC_ALGO_MINSUM
                ? run_flood<LDPC_ALGO_MINSUM>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, d_iters,
                                              d_counters, d_batch_iters, d_work, s)

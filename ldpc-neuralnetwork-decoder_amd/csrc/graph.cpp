@@ -74,8 +74,34 @@ void schedule(const std::vector<int> &tasks, const std::vector<double> &cost, in
     }
 }
 
+// Device CSR tables of the streaming decoder: checks' edges (check-major = edge order) and, for
+// every variable, its edge ids in ascending check order (traditional_decoders.py:26-40).
+int build_csr(ldpc_graph *g) {
+    const int M = g->M, N = g->N;
+    const int64_t E = g->E;
+    std::vector<int32_t> blob((size_t)(M + 1) + E + (N + 1) + E, 0);
+    int32_t *cp = blob.data(), *ev = cp + M + 1, *vp = ev + E, *ve = vp + N + 1;
+    for (int64_t e = 0; e < E; ++e) {
+        ++cp[g->edge_chk[e] + 1];
+        ev[e] = g->edge_var[e];
+        ++vp[g->edge_var[e] + 1];
+    }
+    for (int i = 0; i < M; ++i) cp[i + 1] += cp[i];
+    for (int j = 0; j < N; ++j) vp[j + 1] += vp[j];
+    std::vector<int32_t> fill(vp, vp + N);
+    for (int64_t e = 0; e < E; ++e) ve[fill[g->edge_var[e]]++] = (int32_t)e;  // edges ascend = checks ascend
+    LDPC_HIP(hipMalloc(&g->d_csr, blob.size() * sizeof(int32_t)));
+    LDPC_HIP(hipMemcpy(g->d_csr, blob.data(), blob.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    g->chk_ptr = g->d_csr;
+    g->ev = g->chk_ptr + M + 1;
+    g->var_ptr = g->ev + E;
+    g->var_edge = g->var_ptr + N + 1;
+    return LDPC_OK;
+}
+
 int build(ldpc_graph *g) {
     const int M = g->M, N = g->N;
+    if (int rc = build_csr(g)) return rc;
     // choose the lifting: the largest z dividing 64 that H is block-circulant for, so that a
     // wave's 64 lanes are exactly FG = 64/z frames x z rows (every lane owns a position; no
     // lane predicates on the hot path).  z = 1 (one frame per lane) always works.
@@ -156,8 +182,12 @@ int build(ldpc_graph *g) {
         prog_ptr[(W + 1) + w + 1] = (int32_t)var.size();
         prog_ptr[3 * (W + 1) + w + 1] = bw_ptr[w + 1];
     }
-    if ((int64_t)nslots * 256 >= (1 << kShiftBit) || Nb >= (1 << kShiftBit) || g->max_dv >= 256)
-        return fail(LDPC_EUNSUPPORTED, "graph too large for the flood schedule encoding");
+    if ((int64_t)nslots * 256 >= (1 << kShiftBit) || Nb >= (1 << kShiftBit) || g->max_dv >= 256) {
+        // far beyond the LDS of a CU anyway: this graph decodes on the streaming kernels only
+        g->lds_ok = false;
+        LDPC_HIP(hipDeviceSynchronize());
+        return LDPC_OK;
+    }
 
     // one int32 blob on the device
     std::vector<int32_t> blob;
@@ -263,6 +293,7 @@ extern "C" int ldpc_graph_create_qc(const int32_t *h_base, int mb, int nb, int z
 extern "C" int ldpc_graph_destroy(ldpc_graph *g) {
     if (!g) return LDPC_OK;
     if (g->d_tab) (void)hipFree(g->d_tab);
+    if (g->d_csr) (void)hipFree(g->d_csr);
     delete g;
     return LDPC_OK;
 }

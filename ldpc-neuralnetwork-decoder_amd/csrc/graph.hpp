@@ -59,4 +59,8 @@ struct ldpc_graph {
     ldpc::FloodTables ft{};
     int fixed_id = 0;      // 0: table-driven kernel; 1/2: compile-time schedule BG2_Z4 / BG2_Z32
     int fixed_match = 0;   // what the graph matched (kept when the variant is forced off)
+    bool lds_ok = true;    // the LDS-resident schedule exists (its encoding fits); else stream only
+    // streaming decoder (flood.hip, any graph): check-major CSR + per-variable edge lists
+    int32_t *d_csr = nullptr;  // chk_ptr[M+1] edge_var[E] var_ptr[N+1] var_edge[E]
+    const int32_t *chk_ptr = nullptr, *ev = nullptr, *var_ptr = nullptr, *var_edge = nullptr;
 };
