@@ -11,6 +11,9 @@ are reduced over ranks once at the end.  Rank 0 prints ONE JSON line.
 
 Workloads (BASELINE.json configs):
   minsum-z32  cfg3 (default): BG2 Z=32, scaled min-sum alpha 0.75, 10 iterations, B=65536/GPU
+  minsum-z32-stream  cfg3 on the streaming kernels (messages in HBM; the path of graphs that do
+              not fit LDS), for the HBM roofline of SURVEY 8(d)'s byte model
+  minsum-z384 BG2 lifted to Z=384 (5G's largest; the NR_2_0_32 shifts taken mod 384), streaming
   bp-z4       cfg1 sizes on the GPU: BG2 Z=4, BP, 5 iterations, B=64 (x --batch)
   gnn-z4      cfg2: BG2 Z=4, MessageGNN 5 layers, H=64, T=4, B=4096, fp32
   gnn-z32     cfg4 per GPU: BG2 Z=32, MessageGNN 10 layers, H=64, T=32, B=32768/GPU, fp32
@@ -47,6 +50,8 @@ BF16_MFMA_PEAK_TFS = 2500.0  # MI355X bf16 dense MFMA (spec, no sparsity)
 WORKLOADS = {
     # name: (decoder, Z, iterations, default batch per GPU, SNR dB)
     "minsum-z32": ("minsum", 32, 10, 65536, 2.0),
+    "minsum-z32-stream": ("minsum", 32, 10, 65536, 2.0),
+    "minsum-z384": ("minsum", 384, 10, 8192, 2.0),
     "bp-z4": ("bp", 4, 5, 64, 2.0),
     "bp-z32": ("bp", 32, 10, 65536, 2.0),
     "gnn-z4": ("gnn", 4, 5, 4096, 2.0),
@@ -146,7 +151,7 @@ def cpu_baseline(workload, z, iters, target_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     kind, _, _, _, snr = WORKLOADS[workload]
-    base = oracle.load_base(os.path.join(ROOT, "codes", f"NR_2_0_{z}.txt"))
+    base = oracle.load_base(os.path.join(ROOT, "codes", f"NR_2_0_{z if z in (4, 32) else 32}.txt"))
     H = oracle.expand(base, z)
     g = oracle.Graph(H)
     rng = np.random.default_rng(0)
@@ -260,7 +265,9 @@ def main():
     from ldpc_neural_decoder import _native as N
     from ldpc_neural_decoder.utils import awgn_llr, expand_base_matrix, load_base_matrix
 
-    base = load_base_matrix(os.path.join(ROOT, "codes", f"NR_2_0_{z}.txt"))
+    if a.workload.endswith("-stream"):
+        os.environ["LDPC_FLOOD_STREAM"] = "1"
+    base = load_base_matrix(os.path.join(ROOT, "codes", f"NR_2_0_{z if z in (4, 32) else 32}.txt"))
     H = expand_base_matrix(base, z)
     n = H.shape[1]
     llr = awgn_llr(B, n, snr, seed=20251015, frame_offset=rank * B, device=dev)
@@ -285,9 +292,14 @@ def main():
 
         dtype = "f32"
         per_launch_alg = flood_bytes_per_cw(g.E, g.N, iters) * B
-        bound, unit, peak = "valu", "Ginst/s", VALU_PEAK_GINST
-        fixed = os.environ.get("LDPC_FLOOD_FIXED", "1") != "0"
-        dominant = f"flood_fixed_kernel<BG2_Z{z}, {kind}>" if fixed else f"flood_kernel<{kind}>"
+        streaming = a.workload.endswith("-stream") or z not in (4, 32)
+        if streaming:  # messages stream through HBM every iteration: SURVEY 8(d)'s byte model is the bound
+            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+            dominant = f"stream_check_kernel<{kind}> + stream_var_kernel (all iterations)"
+        else:
+            bound, unit, peak = "valu", "Ginst/s", VALU_PEAK_GINST
+            fixed = os.environ.get("LDPC_FLOOD_FIXED", "1") != "0"
+            dominant = f"flood_fixed_kernel<BG2_Z{z}, {kind}>" if fixed else f"flood_kernel<{kind}>"
     elif kind == "lay":
         from ldpc_neural_decoder.models import CheckLayer, OutputLayer, ResidualLayer, VariableLayer
         from ldpc_neural_decoder.utils import create_LLR_mapping

@@ -9,7 +9,9 @@
 // The float32 operation sequence is the reference's (each torch op rounds to float32, scalars are
 // cast to float32 first), so the only difference from the reference is the normal generator:
 // Philox-4x32-10 + Box-Muller here, torch's CPU mt19937 there (parity is statistical; see
-// tests/test_channel.py).  Compile with -ffp-contract=off so s + n*std does not fuse.
+// tests/test_channel_gpu.py; the fused arithmetic is pinned against oracle.awgn_llr there, and the
+// reference-API functions against the reference's own seeded outputs in tests/test_channel_host.py).
+// Compile with -ffp-contract=off so s + n*std does not fuse.
 #include <cmath>
 #include <cstdint>
 

@@ -1273,72 +1273,124 @@ __global__ __launch_bounds__(256) void stream_init_kernel(StreamArgs S) {
     S.msg[t] = S.llrT[(int64_t)S.ev[e] * S.B + b];  // v2c <- llr (traditional_decoders.py:199-202)
 }
 
+// one (check, frame): the row's DC messages in registers (DC is the row's degree, uniform over a
+// wave of 64 consecutive frames of one row)
+template <int ALGO, int DC>
+__device__ __forceinline__ void stream_row(const StreamArgs &S, float *m, int e0) {
+    float v[DC];
+#pragma unroll
+    for (int e = 0; e < DC; ++e) v[e] = m[(int64_t)(e0 + e) * S.B];
+    float out[DC];
+    if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+        // the LDS kernels' fast path (two minima by v_min / v_med3, sign parity by xor) when the
+        // row has no zero and no NaN message; else MinSumStats (exact torch.sign semantics)
+        float m1 = fabsf(v[0]), m2 = INFINITY;
+        bool special = is_zero_sign(v[0]);
+#pragma unroll
+        for (int e = 1; e < DC; ++e) {
+            two_min_step(m1, m2, v[e]);
+            special |= is_zero_sign(v[e]);
+        }
+        if (!special) {
+            const uint32_t par = sign_parity_n<DC>(v) & 0x80000000u;
+            const uint32_t s1 = __float_as_uint(S.alpha * m1) ^ par, s2 = __float_as_uint(S.alpha * m2) ^ par;
+#pragma unroll
+            for (int e = 0; e < DC; ++e)
+                out[e] = __uint_as_float((__float_as_uint(v[e]) & 0x80000000u) ^ (fabsf(v[e]) == m1 ? s2 : s1));
+        } else {
+            MinSumStats st;
+#pragma unroll
+            for (int e = 0; e < DC; ++e) st.add(e, v[e]);
+#pragma unroll
+            for (int e = 0; e < DC; ++e) out[e] = st.c2v(e, v[e], S.alpha);
+        }
+    } else {
+        // c2v_e = 2 atanh(prod_{f != e} tanh(v_f / 2)), product from 1.0 ascending (:72-81):
+        // acc[e] = P_e * t_{e+1} * ... built column by column, as the LDS kernels do
+        float acc[DC];
+        float P = 1.0f;
+#pragma unroll
+        for (int j = 0; j < DC; ++j) {
+            const float t = tanh_half(v[j]);
+#pragma unroll
+            for (int e = 0; e < j; ++e) acc[e] = acc[e] * t;
+            acc[j] = P;
+            P = P * t;
+        }
+#pragma unroll
+        for (int e = 0; e < DC; ++e) out[e] = two_atanh(acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < DC; ++e) m[(int64_t)(e0 + e) * S.B] = out[e];
+}
+
+#define LDPC_STREAM_DEG_CASES(X)                                                                       \
+    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) \
+    X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+
 template <int ALGO>
 __global__ __launch_bounds__(256) void stream_check_kernel(StreamArgs S) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)S.M * S.B) return;
     const int64_t i = t / S.B, b = t - i * S.B;
     if (stream_skip(S, b)) return;
-    const int e0 = S.chk_ptr[i], e1 = S.chk_ptr[i + 1];
+    const int e0 = S.chk_ptr[i], dc = S.chk_ptr[i + 1] - e0;
     float *m = S.msg + b;
-    if constexpr (ALGO == LDPC_ALGO_MINSUM) {
-        MinSumStats st;  // exact torch.sign / NaN semantics (traditional_decoders.py:207-232)
-        for (int e = e0; e < e1; ++e) st.add(e - e0, m[(int64_t)e * S.B]);
-        for (int e = e0; e < e1; ++e) {
-            float *q = m + (int64_t)e * S.B;
-            *q = st.c2v(e - e0, *q, S.alpha);
-        }
-    } else {
-        // c2v_e = 2 atanh(prod_{f != e} tanh(v_f / 2)), product from 1.0 ascending (:72-81).
-        // In place: edge e's output is written after the products of edges <= e were formed, and
-        // edges > e still need v_e, so keep the row's tanh values in a small register window and
-        // write outputs one edge behind: out_e only after every product that reads v_e is done,
-        // i.e. after the whole row -- rows longer than kStreamDc fall back to a second pass that
-        // recomputes from the untouched inputs (the outputs go to the row's tail buffer first).
-        constexpr int kStreamDc = 32;
-        const int dc = e1 - e0;
-        if (dc <= kStreamDc) {
-            float th[kStreamDc], out[kStreamDc];
-            for (int e = 0; e < dc; ++e) th[e] = tanh_half(m[(int64_t)(e0 + e) * S.B]);
-            for (int e = 0; e < dc; ++e) {
-                float prod = 1.0f;
-                for (int f = 0; f < dc; ++f)
-                    if (f != e) prod = prod * th[f];
-                out[e] = two_atanh(prod);
-            }
-            for (int e = 0; e < dc; ++e) m[(int64_t)(e0 + e) * S.B] = out[e];
-        }  // longer rows are refused on the host (ldpc_flood_decode: LDPC_EUNSUPPORTED)
+    switch (dc) {  // degrees above 32 are refused on the host
+#define X(n) case n: stream_row<ALGO, n>(S, m, e0); break;
+        LDPC_STREAM_DEG_CASES(X)
+#undef X
+        default: break;
     }
 }
 
-// v2c_e = llr + sum_{e' != e} c_e' in ascending check order; APP = llr + all (traditional_decoders.py:235-252)
+// one (variable, frame): v2c_e = llr + sum_{e' != e} c_e' in ascending check order as the prefix
+// P_e followed by the tail adds (traditional_decoders.py:235-250); APP = P_DV -> decision
+template <int DV>
+__device__ __forceinline__ float stream_col(const StreamArgs &S, float *m, const int32_t *edges, float l, bool write) {
+    float c[DV];
+    int64_t off[DV];
+#pragma unroll
+    for (int p = 0; p < DV; ++p) {
+        off[p] = (int64_t)edges[p] * S.B;
+        c[p] = m[off[p]];
+    }
+    f32x2 acc[(DV + 1) / 2];
+    float P = l;
+#pragma unroll
+    for (int j = 0; j < DV; ++j) {
+        const f32x2 cc = {c[j], c[j]};
+#pragma unroll
+        for (int p = 0; p < j / 2; ++p) acc[p] = acc[p] + cc;
+        if (j % 2 == 1) {
+            acc[j / 2].x = acc[j / 2].x + c[j];
+            acc[j / 2].y = P;
+        } else {
+            acc[j / 2].x = P;
+        }
+        P = P + c[j];
+    }
+    if (write) {
+#pragma unroll
+        for (int p = 0; p < DV; ++p) m[off[p]] = p % 2 == 0 ? acc[p / 2].x : acc[p / 2].y;
+    }
+    return P;
+}
+
 __global__ __launch_bounds__(256) void stream_var_kernel(StreamArgs S, int write) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)S.N * S.B) return;
     const int64_t j = t / S.B, b = t - j * S.B;
     if (stream_skip(S, b)) return;
-    const int p0 = S.var_ptr[j], p1 = S.var_ptr[j + 1];
+    const int p0 = S.var_ptr[j], dv = S.var_ptr[j + 1] - p0;
     const float l = S.llrT[t];
-    float *m = S.msg + b;
-    constexpr int kWin = 32;  // c2v values held in registers (in-place update needs them all first)
-    const int dv = p1 - p0;
     float app = l;
-    if (dv <= kWin) {
-        float c[kWin];
-        for (int p = 0; p < dv; ++p) c[p] = m[(int64_t)S.var_edge[p0 + p] * S.B];
-        if (write) {
-            float P = l;  // prefix P_p = llr + c_0 + ... + c_{p-1}, then the tail adds
-            for (int p = 0; p < dv; ++p) {
-                float acc = P;
-                for (int q = p + 1; q < dv; ++q) acc = acc + c[q];
-                m[(int64_t)S.var_edge[p0 + p] * S.B] = acc;
-                P = P + c[p];
-            }
-            app = P;
-        } else {
-            for (int p = 0; p < dv; ++p) app = app + c[p];
-        }
-    }  // longer columns are refused on the host (ldpc_flood_decode: LDPC_EUNSUPPORTED)
+    switch (dv) {  // degrees above 32 are refused on the host
+#define X(n) case n: app = stream_col<n>(S, S.msg + b, S.var_edge + p0, l, write != 0); break;
+        LDPC_STREAM_DEG_CASES(X)
+#undef X
+        default: break;
+    }
     S.bitsT[t] = app < 0.0f;  // NaN < 0 is false -> 0
 }
 
@@ -1472,7 +1524,7 @@ FloodWs flood_ws(const ldpc_graph *g, int64_t B, int max_iter, int early_stop, v
     return w;
 }
 
-constexpr int kStreamMaxDeg = 32;  // register windows of stream_check_kernel (BP) / stream_var_kernel
+constexpr int kStreamMaxDeg = 32;  // register windows of stream_check_kernel / stream_var_kernel
 
 bool use_stream(const ldpc_graph *g, int es) {
     if (!g->lds_ok || flood_lds_bytes(g, es) > kLdsMax) return true;
@@ -1636,7 +1688,7 @@ extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_l
     if (B == 0) return LDPC_OK;
     if (!d_llr || !d_bits) return fail(LDPC_EINVAL, "llr / bits is NULL");
     const bool streaming = use_stream(g, early_stop);
-    if (streaming && (g->max_dv > kStreamMaxDeg || (algo == LDPC_ALGO_BP && g->max_dc > kStreamMaxDeg)))
+    if (streaming && (g->max_dv > kStreamMaxDeg || g->max_dc > kStreamMaxDeg))
         return fail(LDPC_EUNSUPPORTED, "streaming decoder: node degree above " + std::to_string(kStreamMaxDeg));
     // scratch is needed by the streaming decoder, the batch-global stop and any counter output
     if (streaming || early_stop == LDPC_ES_BATCH || d_counters || (d_batch_iters && early_stop == LDPC_ES_FRAME)) {
