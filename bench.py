@@ -372,8 +372,13 @@ def main():
 
         dtype = "bf16" if kind == "gnn-bf16" else "f32"
         E = len(conv.messages)
+        # fp32 forward FLOPs per frame-layer as executed: the reference's MLPs cost 12 H^2 per message
+        # (two sides x (W1 over [c; g]: 4 H^2 + W2: 2 H^2)); W1's group half is applied once per group
+        # (gnn.hip, gnn_group_proj_kernel), so 8 H^2 per message + 2 H^2 per var / check group
+        fwd_flops = 8 * 64 * 64 * E + 2 * 64 * 64 * (g_n + g_m)
+        nominal_flops = 12 * 64 * 64 * E
         if kind == "gnn-sweep":
-            per_launch_alg = 12 * 64 * 64 * E * B * iters * len(sweep_snrs)  # MLP FLOPs per sweep
+            per_launch_alg = fwd_flops * B * iters * len(sweep_snrs)  # MLP FLOPs per sweep
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         elif kind == "gnn-bf16":
             # HBM-bound; per frame-layer 3 passes over the bf16 features
@@ -386,7 +391,7 @@ def main():
             per_launch_alg = 36 * 64 * 64 * E * B * iters
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         else:
-            per_launch_alg = 12 * 64 * 64 * E * B * iters  # useful MLP FLOPs per forward
+            per_launch_alg = fwd_flops * B * iters  # MLP FLOPs per forward, as executed
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         dominant = {"gnn-train": "gnn training step", "gnn-sweep": "SNR sweep (7 x channel + gnn forward + count)"}.get(
             kind, "gnn forward (all layers)")
@@ -439,6 +444,11 @@ def main():
             if traffic is not None and tjd.get("batch") and tjd["batch"] != B:
                 traffic = traffic * B / tjd["batch"]
         notes = None
+        if kind in ("gnn", "gnn-sweep"):
+            notes = {"flop_model": "executed fp32 MFMA FLOPs: 8 H^2 E + 2 H^2 (N + M) per frame-layer "
+                                   "(W1's group half applied per group); the per-message [c; g] form is 12 H^2 E",
+                     "nominal_12H2E_per_launch": nominal_flops * B * iters * (len(sweep_snrs) if kind == "gnn-sweep" else 1),
+                     "nominal_frac": nominal_flops / fwd_flops * achieved / peak}
         if bound == "valu":
             achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg)
         cpu = None

@@ -14,7 +14,13 @@
 //                           H lanes, 256-B coalesced rows.  Layer 0 builds c from the LLRs.
 //                           H = 64 runs gnn_group_mean_tile_kernel instead: one wave per 8 groups
 //                           of one degree (the plan's group tiles), 8 lanes x 32 B per row.
-//   gnn_mlp_mfma_kernel     H = 64.  Persistent, one 512-thread workgroup per CU holding the
+//   gnn_group_proj_kernel   H = 64, group plans (default): the group mean AND its product with
+//                           the group half of each side's first Linear (+ b1), one row per group,
+//                           so the per-message GEMM1 runs over c only (see the kernel).
+//   gnn_mlp2_kernel         H = 64, group plans (default): the MLP over c started from those rows.
+//                           The two frame halves of a call run on two streams.
+//   gnn_mlp_mfma_kernel     H = 64, general (CSR) adjacencies and LDPC_GNN_PROJ=0: the
+//                           per-message [c; g] form.  Persistent, one 512-thread workgroup per CU holding the
 //                           layer's four weight matrices (100 KB fp32, rows padded so one
 //                           ds_read_b128 feeds four MFMA k-steps) in LDS; every wave owns a
 //                           32-message tile and runs the four GEMMs on v_mfma_f32_32x32x2_f32 in
@@ -41,6 +47,18 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMfmaH = 64;
+#ifndef LDPC_MLP2_WPS
+#define LDPC_MLP2_WPS 3
+#endif
+#ifndef LDPC_MLP2_NT
+#define LDPC_MLP2_NT 768
+#endif
+#ifndef LDPC_PROJ_WPS
+#define LDPC_PROJ_WPS 2
+#endif
+#ifndef LDPC_PROJ_NT
+#define LDPC_PROJ_NT 768
+#endif
 int mlp_threads() {
     static int t = [] {
         const char *e = std::getenv("LDPC_GNN_MLP_THREADS");
@@ -251,7 +269,9 @@ constexpr int kEmbStride = 68;
 __device__ __forceinline__ int crow(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
 template <int kMlpThreads>
-__global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_kernel(GnnLayer P) {
+// both variants cap registers at 2 waves per SIMD: the 256-thread one then leaves half of every
+// SIMD's register file to the group-mean waves of the other stream
+__global__ __launch_bounds__(kMlpThreads, 2) void gnn_mlp_mfma_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int H = kMfmaH;
     const int tid = threadIdx.x;
@@ -411,6 +431,316 @@ __global__ __launch_bounds__(kMlpThreads, kMlpThreads / 256) void gnn_mlp_mfma_k
     }
 }
 
+// ------------------------------------------------------------------------ projected groups, H = 64
+// The first Linear of each side takes [c; g] with g the mean of c over the message's group
+// (message_gnn_decoder.py:106-118), so  W1 [c; g] + b1 = W1_left c + (W1_right g + b1).  The
+// bracket is one row per GROUP: gnn_group_proj_kernel computes it once per group (1664 + 1344 rows
+// per BG2 Z = 32 frame instead of 2 x 6304 per-message products) and the MLP starts its GEMM1
+// accumulator from it, so GEMM1 runs over the 64 units of c only: 2/3 of the per-message MFMA work.
+// A degree-1 var group's row is W1_right c of its own message, so no message needs a special case.
+//
+// gnn_group_proj_kernel: one wave per (frame, 32-group tile of one side): lane (j, half) sums units
+// half*32 .. +31 of c over group j's members (ascending, as the group-mean kernels), scales by
+// 1/|group| -- exactly the B operand of v_mfma_f32_32x32x2_f32 for K = 64 -- then 2 x 32 MFMAs
+// against W1_right (LDS) and + b1.  Rows go to Mv / Mc (same shape as the group means).
+// LDS (floats): W1vR [64][68], W1cR [64][68], b1v, b1c, w_in, b_in [64 each], emb [T][68].
+constexpr int kPS = 68;
+constexpr int kPOffW1c = 64 * kPS, kPOffB = 2 * 64 * kPS, kPOffEmb = kPOffB + 4 * 64;
+inline size_t proj_lds_bytes(int T, int waves) { return (size_t)(kPOffEmb + T * kPS + waves * 32 * kPS) * 4; }  // + 32 group means per wave
+
+struct ProjTiles {
+    const int4 *meta;
+    const int32_t *grp, *deg, *mem;
+    int n_tiles;
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group_proj_kernel(GnnLayer P, ProjTiles T) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 64 * 64; i += NT) {
+        const int o = i >> 6, k = i & 63;
+        lds[o * kPS + k] = P.w1v[o * 128 + 64 + k];
+        lds[kPOffW1c + o * kPS + k] = P.w1c[o * 128 + 64 + k];
+    }
+    if (tid < 64) {
+        lds[kPOffB + tid] = P.b1v[tid];
+        lds[kPOffB + 64 + tid] = P.b1c[tid];
+        lds[kPOffB + 128 + tid] = P.w_in[tid];
+        lds[kPOffB + 192 + tid] = P.b_in[tid];
+    }
+    for (int i = tid; i < P.T * 64; i += NT) lds[kPOffEmb + (i >> 6) * kPS + (i & 63)] = P.emb[i];
+    __syncthreads();
+    const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
+    // this wave's 32 group means, [32][68] after the shared image
+    float *gm = lds + kPOffEmb + P.T * kPS + wave * 32 * kPS;
+    const int c4 = 4 * (lane & 15), r4 = lane >> 4;
+    const int64_t ntiles = P.B * T.n_tiles;
+    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
+    for (int64_t tt = tw.first; tt < tw.end; tt += tw.stride) {
+        const int64_t b = tt / T.n_tiles;
+        const int t = (int)(tt - b * T.n_tiles);
+        const int4 md = T.meta[t];
+        // group means, 16 lanes x 16 B per 256-B row: lane (r, c) owns units 4c .. 4c+3 of the tile's
+        // groups 4p + r, p < 8, all eight summed side by side so that every lane keeps eight rows in
+        // flight.  Per unit the members are summed in ascending order (x + emb first), x 1/|group|.
+        int dg[8];
+        float4 acc[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            dg[p] = T.deg[32 * t + 4 * p + r4];
+            acc[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+        const int32_t *mem = T.mem + md.z + r4;
+        if (P.x_in) {
+            const float *xb = P.x_in + (int64_t)b * P.E * 64 + c4;
+            const float *eb = lds + kPOffEmb + c4;
+            int mi[8], mj[8];
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                mi[p] = mem[4 * p];
+                mj[p] = mem[32 + 4 * p];  // the table holds maxdeg + 1 rows (last one padding)
+            }
+            auto accum = [&](const float4 (&x)[8], const int (&ty)[8], int i) {
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    if (i < dg[p]) {
+                        const float4 e = *reinterpret_cast<const float4 *>(eb + ty[p] * kPS);
+                        acc[p].x += x[p].x + e.x; acc[p].y += x[p].y + e.y;
+                        acc[p].z += x[p].z + e.z; acc[p].w += x[p].w + e.w;
+                    }
+                }
+            };
+            for (int i = 0; i < md.y; i += 2) {  // two members of all eight groups in flight
+                float4 x[8], y[8];
+                int tx[8], tyy[8];
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    x[p] = *reinterpret_cast<const float4 *>(xb + (int64_t)mi[p] * 64);
+                    y[p] = *reinterpret_cast<const float4 *>(xb + (int64_t)mj[p] * 64);
+                    tx[p] = P.msg_type[mi[p]];
+                    tyy[p] = P.msg_type[mj[p]];
+                }
+                if (i + 2 < md.y) {
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        mi[p] = mem[32 * (i + 2) + 4 * p];
+                        mj[p] = mem[32 * (i + 3) + 4 * p];
+                    }
+                }
+                accum(x, tx, i);
+                accum(y, tyy, i + 1);
+            }
+        } else {
+            const float4 w = *reinterpret_cast<const float4 *>(lds + kPOffB + 128 + c4);
+            const float4 bi = *reinterpret_cast<const float4 *>(lds + kPOffB + 192 + c4);
+            for (int i = 0; i < md.y; ++i) {
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    if (i < dg[p]) {
+                        const int m = mem[32 * i + 4 * p];
+                        const float l = P.llr[(int64_t)b * P.N + P.msg_var[m]];
+                        const float4 e = *reinterpret_cast<const float4 *>(lds + kPOffEmb + P.msg_type[m] * kPS + c4);
+                        acc[p].x += (l * w.x + bi.x) + e.x; acc[p].y += (l * w.y + bi.y) + e.y;  // Linear(1, H) + emb
+                        acc[p].z += (l * w.z + bi.z) + e.z; acc[p].w += (l * w.w + bi.w) + e.w;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int slot = 4 * p + r4, g = T.grp[32 * t + slot];
+            const float inv = g >= 0 ? (md.x ? P.inv_c : P.inv_v)[g] : 0.0f;
+            *reinterpret_cast<float4 *>(gm + slot * kPS + c4) =
+                make_float4(acc[p].x * inv, acc[p].y * inv, acc[p].z * inv, acc[p].w * inv);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // B operand: lane (j, half) <- group j's units 8 q + 4 half + i (q < 8)
+        float g32[32];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float4 v = *reinterpret_cast<const float4 *>(gm + j * kPS + 8 * q + 4 * half);
+            g32[4 * q] = v.x; g32[4 * q + 1] = v.y; g32[4 * q + 2] = v.z; g32[4 * q + 3] = v.w;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const float *W = lds + (md.x ? kPOffW1c : 0);
+        int wl = j * kPS + 4 * half;  // step kk + i pairs unit 8 (kk/4) + i (half 0) with + 4 (half 1)
+        asm volatile("" : "+v"(wl));
+        f32x16 h0 = {}, h1 = {};
+#pragma unroll
+        for (int kk = 0; kk < 32; kk += 4) {
+            const float4 wa = *reinterpret_cast<const float4 *>(W + wl + 2 * kk);
+            const float4 wb = *reinterpret_cast<const float4 *>(W + wl + 32 * kPS + 2 * kk);
+            const float a4[4] = {wa.x, wa.y, wa.z, wa.w}, b4[4] = {wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                h0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i], g32[kk + i], h0, 0, 0, 0);
+                h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b4[i], g32[kk + i], h1, 0, 0, 0);
+            }
+        }
+        const int g = T.grp[32 * t + j];
+        if (g < 0) continue;
+        const float *b1 = lds + kPOffB + 64 * md.x;
+        float *dst = md.x ? P.Mc + ((int64_t)b * P.Gc + g) * 64 : P.Mv + ((int64_t)b * P.Gv + g) * 64;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int u = 8 * q + 4 * half;  // registers 4q .. 4q+3 hold units crow(4q + i, half) = u + i
+            *reinterpret_cast<float4 *>(dst + u) =
+                make_float4(h0[4 * q] + b1[u], h0[4 * q + 1] + b1[u + 1], h0[4 * q + 2] + b1[u + 2], h0[4 * q + 3] + b1[u + 3]);
+            *reinterpret_cast<float4 *>(dst + 32 + u) =
+                make_float4(h1[4 * q] + b1[32 + u], h1[4 * q + 1] + b1[33 + u], h1[4 * q + 2] + b1[34 + u],
+                            h1[4 * q + 3] + b1[35 + u]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------ MLP over projected groups
+// As gnn_mlp_mfma_kernel, but GEMM1 is W1_left c (K = 64: lane half h carries units 32 h .. +31 of
+// c, one k of each half per MFMA step) started from the message's projected group rows (above),
+// and nothing else changes: ReLU, GEMM2 of both sides into one accumulator, b2v + b2c, residual,
+// output projection.  Per 32-message tile 2 x (64 + 64) MFMAs instead of 2 x (128 + 64).
+// LDS (floats): W1vL [64][68], W1cL, W2v [64][68], W2c, then b2v, b2c, wo [64 each], emb [T][68].
+constexpr int kM2OffW1c = 64 * kPS, kM2OffW2v = 2 * 64 * kPS, kM2OffW2c = 3 * 64 * kPS;
+constexpr int kM2OffB = 4 * 64 * kPS, kM2OffEmb = kM2OffB + 3 * 64;
+inline size_t mlp2_lds_bytes(int T) { return (size_t)(kM2OffEmb + T * kPS) * 4; }
+
+template <int NT, int WPS>
+__global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 64 * 64; i += NT) {
+        const int o = i >> 6, k = i & 63;
+        lds[o * kPS + k] = P.w1v[o * 128 + k];
+        lds[kM2OffW1c + o * kPS + k] = P.w1c[o * 128 + k];
+        lds[kM2OffW2v + o * kPS + k] = P.w2v[i];
+        lds[kM2OffW2c + o * kPS + k] = P.w2c[i];
+    }
+    if (tid < 64) {
+        lds[kM2OffB + tid] = P.b2v[tid];
+        lds[kM2OffB + 64 + tid] = P.b2c[tid];
+        lds[kM2OffB + 128 + tid] = P.last ? P.wo[tid] : 0.0f;
+    }
+    for (int i = tid; i < P.T * 64; i += NT) lds[kM2OffEmb + (i >> 6) * kPS + (i & 63)] = P.emb[i];
+    __syncthreads();
+
+    const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
+    const int64_t R = P.B * P.E;
+    const int64_t ntiles = (R + 31) / 32;
+    const float bo = P.last ? P.bo[0] : 0.0f;
+    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
+    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+        const int64_t row = t * 32 + j;
+        const bool ok = row < R;
+        const int64_t rr = ok ? row : R - 1;
+        const int64_t b = rr / P.E, m = rr - b * P.E;
+        float in[32];
+        {
+            // lane half h carries units 8 q + 4 h + i (float4 chunk 2 q + h of the row)
+            const float *e = lds + kM2OffEmb + P.msg_type[m] * kPS + 4 * half;
+            if (P.x_in) {
+                const float *xr = P.x_in + rr * 64 + 4 * half;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float4 v = *reinterpret_cast<const float4 *>(xr + 8 * q);
+                    in[4 * q + 0] = v.x + e[8 * q + 0];
+                    in[4 * q + 1] = v.y + e[8 * q + 1];
+                    in[4 * q + 2] = v.z + e[8 * q + 2];
+                    in[4 * q + 3] = v.w + e[8 * q + 3];
+                }
+            } else {
+                const float l = P.llr[b * P.N + P.msg_var[m]];
+#pragma unroll
+                for (int k = 0; k < 32; ++k) {
+                    const int u = 8 * (k >> 2) + 4 * half + (k & 3);
+                    in[k] = (l * P.w_in[u] + P.b_in[u]) + e[8 * (k >> 2) + (k & 3)];
+                }
+            }
+        }
+        const float *pv = P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
+        const float *pc = P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
+        f32x16 y0 = {}, y1 = {};
+        int w1lane = j * kPS + 4 * half, w2lane = j * kPS + 4 * half;
+        asm volatile("" : "+v"(w1lane), "+v"(w2lane));
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const float *pr = side == 0 ? pv : pc;
+            f32x16 h0, h1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // registers 4q .. 4q+3 <-> units 8q + 4 half + i (+ 32 for h1)
+                const float4 a = *reinterpret_cast<const float4 *>(pr + 8 * q);
+                const float4 c = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q);
+                h0[4 * q] = a.x; h0[4 * q + 1] = a.y; h0[4 * q + 2] = a.z; h0[4 * q + 3] = a.w;
+                h1[4 * q] = c.x; h1[4 * q + 1] = c.y; h1[4 * q + 2] = c.z; h1[4 * q + 3] = c.w;
+            }
+            const float *W1 = lds + (side == 0 ? 0 : kM2OffW1c);
+            const float *W2 = lds + (side == 0 ? kM2OffW2v : kM2OffW2c);
+#pragma unroll
+            for (int kk = 0; kk < 32; kk += 4) {
+                const float4 wa = *reinterpret_cast<const float4 *>(W1 + w1lane + 2 * kk);
+                const float4 wb = *reinterpret_cast<const float4 *>(W1 + w1lane + 32 * kPS + 2 * kk);
+                const float a4[4] = {wa.x, wa.y, wa.z, wa.w}, b4[4] = {wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    h0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i], in[kk + i], h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b4[i], in[kk + i], h1, 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                h0[r] = fmaxf(h0[r], 0.0f);
+                h1[r] = fmaxf(h1[r], 0.0f);
+            }
+#pragma unroll
+            for (int rq = 0; rq < 4; ++rq) {
+                const float *w = W2 + w2lane + 8 * rq;
+                const float4 a0 = *reinterpret_cast<const float4 *>(w);
+                const float4 a1 = *reinterpret_cast<const float4 *>(w + 32 * kPS);
+                const float4 c0 = *reinterpret_cast<const float4 *>(w + 32);
+                const float4 c1 = *reinterpret_cast<const float4 *>(w + 32 * kPS + 32);
+                const float A0[4] = {a0.x, a0.y, a0.z, a0.w}, A1[4] = {a1.x, a1.y, a1.z, a1.w};
+                const float C0[4] = {c0.x, c0.y, c0.z, c0.w}, C1[4] = {c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 4 * rq + i;
+                    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[i], h0[r], y0, 0, 0, 0);
+                    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[i], h0[r], y1, 0, 0, 0);
+                    y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(C0[i], h1[r], y0, 0, 0, 0);
+                    y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(C1[i], h1[r], y1, 0, 0, 0);
+                }
+            }
+        }
+        const float *b2v = lds + kM2OffB, *b2c = lds + kM2OffB + 64, *wo = lds + kM2OffB + 128;
+        float part = 0.0f;
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int o0 = 32 * ot + 8 * q + 4 * half;
+                float4 v;
+                float *vv = reinterpret_cast<float *>(&v);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float acc = ot == 0 ? y0[4 * q + i] : y1[4 * q + i];
+                    vv[i] = (acc + b2v[o0 + i]) + b2c[o0 + i];
+                }
+                if (P.residual) {
+                    const float4 xr = *reinterpret_cast<const float4 *>(P.x_in + rr * 64 + o0);
+                    v.x += xr.x; v.y += xr.y; v.z += xr.z; v.w += xr.w;
+                }
+                if (P.last) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) part += vv[i] * wo[o0 + i];
+                }
+                if (ok && P.x_out) *reinterpret_cast<float4 *>(P.x_out + row * 64 + o0) = v;
+            }
+        }
+        if (P.last) {
+            part += __shfl_xor(part, 32, 64);
+            if (ok && half == 0) P.msg_out[b * P.E + m] = part + bo;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------ fused MLP, any H
 // one wave per message, lanes = output units (H <= 64 per pass); VALU fp32.
 __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H) {
@@ -546,8 +876,49 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
 
 int g_num_cus = 0;
 
+constexpr int kMlp2Wps = LDPC_MLP2_WPS, kMlp2Nt = LDPC_MLP2_NT;
+// LDPC_GNN_PROJ=0 keeps the per-message [c; g] GEMM1 (gnn_mlp_mfma_kernel) for A/B runs
+bool proj_path() {
+    static bool t = [] {
+        const char *e = std::getenv("LDPC_GNN_PROJ");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return t;
+}
+
+// LDPC_GNN_STREAMS=1 runs the fp32 forward as one frame range on the caller's stream (A/B runs);
+// default 2: two frame halves on two streams, so one half's HBM-bound group-mean launch runs in
+// the register/wave slots the other half's MFMA-bound MLP leaves free on every CU.
+int gnn_streams() {
+    static int t = [] {
+        const char *e = std::getenv("LDPC_GNN_STREAMS");
+        return (e && std::atoi(e) == 1) ? 1 : 2;
+    }();
+    return t;
+}
+
 }  // namespace
 }  // namespace ldpc
+
+// One non-blocking side stream and a fork/join event pair per device, created on first use and kept
+// for the process (the forward is issued from the caller's thread; the events only order launches).
+int ldpc::gnn_side_stream(hipStream_t *side, hipEvent_t *fork, hipEvent_t *join) {
+    constexpr int kMaxDev = 64;
+    static hipStream_t streams[kMaxDev];
+    static hipEvent_t forks[kMaxDev], joins[kMaxDev];
+    int dev = 0;
+    LDPC_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDev) return fail(LDPC_EUNSUPPORTED, "device index out of range");
+    if (!streams[dev]) {
+        LDPC_HIP(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
+        LDPC_HIP(hipEventCreateWithFlags(&forks[dev], hipEventDisableTiming));
+        LDPC_HIP(hipEventCreateWithFlags(&joins[dev], hipEventDisableTiming));
+    }
+    *side = streams[dev];
+    *fork = forks[dev];
+    *join = joins[dev];
+    return LDPC_OK;
+}
 
 using namespace ldpc;
 
@@ -628,6 +999,37 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     int n_v1 = 0;  // var tiles come first, sorted by degree: the degree-1 ones lead
     while (2 * n_v1 < (int)gt_meta.size() && gt_meta[2 * n_v1] == 1) ++n_v1;
     add_tiles(cptr, cmem, n_cgroups, n_vgroups);
+    // fp32 path: projection tiles of 32 groups of one side (gnn.hpp), each side sorted by degree
+    std::vector<int32_t> pt;  // meta [4 n] | grp [32 n] | deg [32 n] | mem
+    std::vector<int32_t> pt_meta, pt_grp, pt_deg, pt_mem;
+    auto add_ptiles = [&](const std::vector<int32_t> &ptr, const std::vector<int32_t> &mem, int ngroups, int side) {
+        std::vector<int32_t> order;
+        for (int g = 0; g < ngroups; ++g)
+            if (ptr[g + 1] > ptr[g]) order.push_back(g);
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int a, int b) { return ptr[a + 1] - ptr[a] < ptr[b + 1] - ptr[b]; });
+        for (size_t i = 0; i < order.size(); i += 32) {
+            const size_t n = std::min<size_t>(32, order.size() - i);
+            int dmax = 0;
+            for (size_t q = 0; q < n; ++q) dmax = std::max(dmax, ptr[order[i + q] + 1] - ptr[order[i + q]]);
+            pt_meta.insert(pt_meta.end(), {side, dmax, (int32_t)pt_mem.size(), 0});
+            for (int k = 0; k <= dmax; ++k)  // one padding row: the kernel reads members in pairs
+                for (size_t q = 0; q < 32; ++q) {
+                    const int g = q < n ? order[i + q] : -1;
+                    pt_mem.push_back(g >= 0 && k < ptr[g + 1] - ptr[g] ? mem[ptr[g] + k] : 0);
+                }
+            for (size_t q = 0; q < 32; ++q) {
+                pt_grp.push_back(q < n ? order[i + q] : -1);
+                pt_deg.push_back(q < n ? ptr[order[i + q] + 1] - ptr[order[i + q]] : 0);
+            }
+        }
+    };
+    add_ptiles(vptr, vmem, n_vgroups, 0);
+    add_ptiles(cptr, cmem, n_cgroups, 1);
+    pt.insert(pt.end(), pt_meta.begin(), pt_meta.end());
+    pt.insert(pt.end(), pt_grp.begin(), pt_grp.end());
+    pt.insert(pt.end(), pt_deg.begin(), pt_deg.end());
+    pt.insert(pt.end(), pt_mem.begin(), pt_mem.end());
     std::vector<int32_t> blob;
     blob.insert(blob.end(), h_vgroup, h_vgroup + E);
     blob.insert(blob.end(), h_cgroup, h_cgroup + E);
@@ -646,7 +1048,8 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     hipError_t e2 = hipMalloc(&p->d_tab, blob.size() * 4);
     hipError_t e3 = hipMalloc(&p->d_inv, inv.size() * 4);
     hipError_t e4 = hipMalloc(&p->d_gt, gt_words * 4);
-    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess) {
+    hipError_t e5 = hipMalloc(&p->d_pt, pt.size() * 4);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan allocation failed");
     }
@@ -655,10 +1058,16 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         hipMemcpy(p->d_gt, gt_meta.data(), gt_meta.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_gt + gt_meta.size(), gt_grp.data(), gt_grp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_gt + gt_meta.size() + gt_grp.size(), gt_mem.data(), gt_mem.size() * 4,
-                  hipMemcpyHostToDevice) != hipSuccess) {
+                  hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_pt, pt.data(), pt.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan upload failed");
     }
+    p->n_ptiles = (int)(pt_meta.size() / 4);
+    p->pt_meta = reinterpret_cast<const int4 *>(p->d_pt);
+    p->pt_grp = p->d_pt + pt_meta.size();
+    p->pt_deg = p->pt_grp + pt_grp.size();
+    p->pt_mem = p->pt_deg + pt_deg.size();
     p->vgroup = p->d_tab;
     p->cgroup = p->vgroup + E;
     p->vg_ptr = p->cgroup + E;
@@ -742,6 +1151,7 @@ extern "C" int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p) {
     if (p->d_inv) (void)hipFree(p->d_inv);
     if (p->d_w) (void)hipFree(p->d_w);
     if (p->d_gt) (void)hipFree(p->d_gt);
+    if (p->d_pt) (void)hipFree(p->d_pt);
     delete p;
     return LDPC_OK;
 }
@@ -794,6 +1204,35 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     const void *mfma_fn = mt == 512 ? reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<512>)
                                     : reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<256>);
     if (mfma) LDPC_HIP(hipFuncSetAttribute(mfma_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mfma_lds));
+    // projected-group path (H = 64, group plans; LDPC_GNN_PROJ=0 selects the per-message [c; g]
+    // kernels for A/B runs)
+    const bool proj = mfma && !p->weighted && p->n_ptiles > 0 && proj_path();
+    // projection workgroups of 12 waves (one LDS weight image for 12 waves' gathers) when the
+    // type table leaves room, else 4
+    const int proj_nt = LDPC_PROJ_NT == 768 && proj_lds_bytes(types, 12) <= 160 * 1024 ? 768 : 256;
+    const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64), mlp2_lds = mlp2_lds_bytes(types);
+    const void *proj_fn = proj_nt == 768 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<768>)
+                                         : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
+    int mlp2_per_cu = 1, proj_per_cu = 1;
+    if (proj) {
+        if (mlp2_lds > 160 * 1024 || proj_lds > 160 * 1024)
+            return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
+        proj_per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
+        // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
+        mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
+        LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
+    }
+    // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
+    const GnnLayer L0 = L;
+    auto run_range = [&](int64_t b0, int64_t nb, hipStream_t st) -> int {
+    GnnLayer L = L0;
+    L.B = nb;
+    L.llr = d_llr + b0 * N;
+    L.Mv = w.Mv + b0 * p->Gv * H;
+    L.Mc = w.Mc + b0 * p->Gc * H;
+    const int64_t xoff = b0 * p->E * H;
     const float *x_in = nullptr;
     for (int l = 0; l < layers; ++l) {
         const float *lw = d_weights + 2 * H + (int64_t)l * layer_floats(H, types);
@@ -811,40 +1250,76 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.x_in = x_in;
         L.residual = l > 0;
         L.last = l == layers - 1;
-        L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H : L.last ? nullptr : (l % 2 == 0) ? w.xa : w.xb;
-        L.msg_out = w.msg_out;
-        const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
+        L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H + xoff
+                          : L.last ? nullptr : ((l % 2 == 0) ? w.xa : w.xb) + xoff;
+        L.msg_out = w.msg_out + b0 * p->E;
+        const int64_t waves = nb * (int64_t)(p->Gv + p->Gc);
         L.d1 = H == 64 && gm_tiles() && d1_skip() && !p->weighted;
+        if (proj) {
+            L.d1 = 0;
+            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles};
+            const int64_t ptiles = nb * (int64_t)p->n_ptiles;
+            const int pw = proj_nt / 64;
+            const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
+            if (proj_nt == 768)
+                hipLaunchKernelGGL(gnn_group_proj_kernel<768>, dim3(pgrid), dim3(768), proj_lds, st, L, T);
+            else
+                hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds, st, L, T);
+            LDPC_CHECK_LAUNCH("gnn_group_proj_kernel");
+            const int64_t tiles = (nb * p->E + 31) / 32;
+            constexpr int wpb = kMlp2Nt / 64;
+            const unsigned grid = (unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu);
+            hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>), dim3(grid), dim3(kMlp2Nt), mlp2_lds, st, L);
+            LDPC_CHECK_LAUNCH("gnn_mlp2_kernel");
+            x_in = L.x_out;
+            continue;
+        }
         if (p->weighted)  // general adjacency: weighted rows, one wave per (frame, message row)
-            hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);
+            hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, L, H);
         else if (H == 64 && gm_tiles()) {
             const GtTiles G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles, L.d1 ? p->n_gtiles_v1 : 0};
-            const int64_t twaves = B * (int64_t)(G.n_tiles - G.first);
-            hipLaunchKernelGGL(gnn_group_mean_tile_kernel, dim3((unsigned)((twaves + 3) / 4)), dim3(256), 0, s, L, G);
+            const int64_t twaves = nb * (int64_t)(G.n_tiles - G.first);
+            hipLaunchKernelGGL(gnn_group_mean_tile_kernel, dim3((unsigned)((twaves + 3) / 4)), dim3(256), 0, st, L, G);
         } else if (H == 64)
-            hipLaunchKernelGGL(gnn_group_mean_h64_kernel, dim3((unsigned)((waves + 15) / 16)), dim3(256), 0, s, L);
+            hipLaunchKernelGGL(gnn_group_mean_h64_kernel, dim3((unsigned)((waves + 15) / 16)), dim3(256), 0, st, L);
         else
-            hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);
+            hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, L, H);
         LDPC_CHECK_LAUNCH("gnn_group_mean_kernel");
         if (mfma) {
-            const int64_t tiles = (B * p->E + 31) / 32;
+            const int64_t tiles = (nb * p->E + 31) / 32;
             const int64_t want = (tiles + mt / 64 - 1) / (mt / 64);
             const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus);
             if (mt == 512)
-                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<512>, dim3(grid), dim3(512), mfma_lds, s, L);
+                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<512>, dim3(grid), dim3(512), mfma_lds, st, L);
             else
-                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<256>, dim3(grid), dim3(256), mfma_lds, s, L);
+                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<256>, dim3(grid), dim3(256), mfma_lds, st, L);
             LDPC_CHECK_LAUNCH("gnn_mlp_mfma_kernel");
         } else {
-            const int64_t want = (B * p->E + 3) / 4;
+            const int64_t want = (nb * p->E + 3) / 4;
             const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus * 8);
-            hipLaunchKernelGGL(gnn_mlp_generic_kernel, dim3(grid), dim3(256), (size_t)16 * H * 4, s, L, H);
+            hipLaunchKernelGGL(gnn_mlp_generic_kernel, dim3(grid), dim3(256), (size_t)16 * H * 4, st, L, H);
             LDPC_CHECK_LAUNCH("gnn_mlp_generic_kernel");
         }
         x_in = L.x_out;
     }
-    const int64_t n = B * N;
-    (void)n;
+    return LDPC_OK;
+    };
+    // Two frame halves on two streams (fork / join through events on the caller's stream): every
+    // frame's layers stay in order on its stream, and the halves share no data.
+    if (gnn_streams() == 2 && B >= 2 * 64) {
+        hipStream_t s2;
+        hipEvent_t fork, join;
+        if (int rc = gnn_side_stream(&s2, &fork, &join)) return rc;
+        const int64_t b1 = B / 2;
+        LDPC_HIP(hipEventRecord(fork, s));
+        LDPC_HIP(hipStreamWaitEvent(s2, fork, 0));
+        if (int rc = run_range(0, b1, s)) return rc;
+        if (int rc = run_range(b1, B - b1, s2)) return rc;
+        LDPC_HIP(hipEventRecord(join, s2));
+        LDPC_HIP(hipStreamWaitEvent(s, join, 0));
+    } else if (int rc = run_range(0, B, s)) {
+        return rc;
+    }
     if (int rc = gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, nullptr, d_probs, s)) return rc;
     return LDPC_OK;
 }

@@ -26,6 +26,15 @@ struct ldpc_gnn_plan {
     int32_t *d_gt = nullptr;
     const int2 *gt_meta = nullptr;
     const int32_t *gt_grp = nullptr, *gt_mem = nullptr;
+    // fp32 projection tiles (gnn.hip, gnn_group_proj_kernel): 32 groups of one side per tile,
+    // each side sorted by degree.  pt_meta[t] = {side (0 var, 1 check), max degree, offset into
+    // pt_mem, 0}; pt_grp[32 t + j] = group id within its side (-1 = padding), pt_deg[32 t + j]
+    // its degree (0 for padding); pt_mem[off + 32 i + j] = i-th member message of lane j's group
+    // (message 0 past its degree; max degree + 1 rows per tile).
+    int n_ptiles = 0;
+    int32_t *d_pt = nullptr;
+    const int4 *pt_meta = nullptr;
+    const int32_t *pt_grp = nullptr, *pt_deg = nullptr, *pt_mem = nullptr;
 };
 
 namespace ldpc {
@@ -47,6 +56,9 @@ __device__ __forceinline__ const int32_t *csr_mem(const int32_t *ints, int N) { 
 int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
                      const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
                      float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s);
+
+// The per-device side stream and fork/join events the forwards split their frames over.
+int gnn_side_stream(hipStream_t *side, hipEvent_t *fork, hipEvent_t *join);
 
 // bf16 forward (precision 1, H = 64); same arguments as ldpc_gnn_forward.
 // The workspace is sized for the largest type count the LDS image admits (kBf16MaxTypes).

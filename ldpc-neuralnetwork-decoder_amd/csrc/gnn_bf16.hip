@@ -590,6 +590,16 @@ int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, 
     }
 }
 
+// LDPC_GNN_STREAMS=1: one frame range on the caller's stream; default two halves on two streams
+// (gnn.hip), so one half's group means and syndrome checks overlap the other half's MLP.
+int gnn_streams_bf16() {
+    static int t = [] {
+        const char *e = std::getenv("LDPC_GNN_STREAMS");
+        return (e && std::atoi(e) == 1) ? 1 : 2;
+    }();
+    return t;
+}
+
 int mlp_variant() {
     static int v = [] {
         const char *e = std::getenv("LDPC_GNN_BF16_MLP");
@@ -650,37 +660,41 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     const float *kd_last = w.kd + (int64_t)(L - 1) * kd_floats(T);
     const float *bo_last = layer_w(d_weights, T, L - 1).bo;
 
+    // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
+    auto run_range = [&](int64_t b0, int64_t nb, hipStream_t st) -> int {
+    const int64_t xoff = b0 * p->E * H;
+    uint8_t *act = et ? w.active + b0 : nullptr;
     const __bf16 *x_in = nullptr;
     for (int l = 0; l < L; ++l) {
         const LayerW lw = layer_w(d_weights, T, l);
         GmArgs gm{};
         gm.x_in = x_in;
-        gm.llr = d_llr;
+        gm.llr = d_llr + b0 * N;
         gm.msg_var = d_msg_var;
         gm.w_in = d_weights;
         gm.b_in = d_weights + H;
         gm.memb = w.memb + (int64_t)l * Gtot * H;
         gm.G = G;
         if (d1 && l > 0) gm.G.first = p->n_gtiles_v1;
-        gm.Mv = w.Mv;
-        gm.Mc = w.Mc;
+        gm.Mv = w.Mv + b0 * p->Gv * H;
+        gm.Mc = w.Mc + b0 * p->Gc * H;
         gm.Gv = p->Gv;
         gm.Gc = p->Gc;
         gm.E = (int)p->E;
         gm.N = N;
-        gm.B = B;
-        gm.active = active;
-        const int64_t gwaves = B * (gm.G.n_tiles - gm.G.first);
-        hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, s, gm);
+        gm.B = nb;
+        gm.active = act;
+        const int64_t gwaves = nb * (gm.G.n_tiles - gm.G.first);
+        hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, st, gm);
         LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
 
         MlpArgs m{};
         m.x_in = x_in;
-        m.x_out = l == L - 1 ? nullptr : (l % 2 == 0 ? w.xa : w.xb);
-        m.Mv = w.Mv;
-        m.Mc = w.Mc;
+        m.x_out = l == L - 1 ? nullptr : (l % 2 == 0 ? w.xa : w.xb) + xoff;
+        m.Mv = w.Mv + b0 * p->Gv * H;
+        m.Mc = w.Mc + b0 * p->Gc * H;
         m.info = w.info;
-        m.llr = d_llr;
+        m.llr = d_llr + b0 * N;
         m.w1v = lw.w1v;
         m.w1c = lw.w1c;
         m.w2v = lw.w2v;
@@ -694,22 +708,38 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.N = N;
         m.tpf = (int)tpf;
         m.d1 = d1 ? 1 : 0;
-        m.B = B;
-        m.msg_out = w.msg_out;
-        m.active = active;
+        m.B = nb;
+        m.msg_out = w.msg_out + b0 * p->E;
+        m.active = act;
         m.kd_last = et && l < L - 1 ? kd_last : nullptr;
         m.bo_last = bo_last;
         const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0);
-        const int rc = launch_mlp(mlp_variant(), mode, B * tpf, lds, s, m);
+        const int rc = launch_mlp(mlp_variant(), mode, nb * tpf, lds, st, m);
         if (rc != LDPC_OK) return rc;
         LDPC_CHECK_LAUNCH("gnn_bf16_mlp_kernel");
         if (m.kd_last) {
-            hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)B), dim3(256), (size_t)(N + 31) / 32 * 4, s,
-                               w.msg_out, w.csr, p->E, d_llr, N, p->cg_ptr, p->cg_mem, p->Gc, d_msg_var, l, w.active, d_iters,
-                               d_probs);
+            hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)nb), dim3(256), (size_t)(N + 31) / 32 * 4, st,
+                               w.msg_out + b0 * p->E, w.csr, p->E, d_llr + b0 * N, N, p->cg_ptr, p->cg_mem, p->Gc,
+                               d_msg_var, l, act, d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N);
             LDPC_CHECK_LAUNCH("gnn_bf16_syndrome_kernel");
         }
         x_in = m.x_out;
+    }
+    return LDPC_OK;
+    };
+    if (gnn_streams_bf16() == 2 && B >= 2 * 64) {
+        hipStream_t s2;
+        hipEvent_t fork, join;
+        if (int rc = gnn_side_stream(&s2, &fork, &join)) return rc;
+        const int64_t b1 = B / 2;
+        LDPC_HIP(hipEventRecord(fork, s));
+        LDPC_HIP(hipStreamWaitEvent(s2, fork, 0));
+        if (int rc = run_range(0, b1, s)) return rc;
+        if (int rc = run_range(b1, B - b1, s2)) return rc;
+        LDPC_HIP(hipEventRecord(join, s2));
+        LDPC_HIP(hipStreamWaitEvent(s, join, 0));
+    } else if (int rc = run_range(0, B, s)) {
+        return rc;
     }
     return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s);
 }
