@@ -96,6 +96,19 @@ int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_llr, int64_t
                       int32_t *d_batch_iters, uint64_t *d_counters, void *d_work,
                       int64_t work_bytes, void *stream);
 
+/* ------------------------------------------------------------------ hybrid min-sum
+ * Replaces: CustomMinSumMessageGNNDecoder.forward (models/message_gnn_decoder.py:1167-1251) with
+ * CustomVariableMessageGNNLayer.variable_layer_update (:611-670) and
+ * CustomCheckMessageGNNLayer.check_layer_update (:976-1044).  The reference cannot run these
+ * (SURVEY.md section 0); the semantics this build defines from them (total-minus-own variable update,
+ * damping 0.5 with the incoming c2v from the second iteration on, unscaled min-sum check update,
+ * probs = sigmoid(llr + sum of c2v)) are spelled out in csrc/flood.hip and DESIGN.md.
+ * d_llr (B, N) float32 -> d_probs (B, N) float32.  No early stop (the reference has none).
+ * d_work: ldpc_custom_minsum_workspace_size(g, B) bytes.  B <= 4194240 per call. */
+int64_t ldpc_custom_minsum_workspace_size(const ldpc_graph *g, int64_t B);
+int ldpc_custom_minsum_decode(const ldpc_graph *g, const float *d_llr, int64_t B, int iterations,
+                              float *d_probs, void *d_work, int64_t work_bytes, void *stream);
+
 /* ------------------------------------------------------------------ channel
  * Replaces: qpsk_modulate -> awgn_channel -> qpsk_demodulate (utils/channel.py:4-154) fused:
  *   s = 1/sqrt2 - b*sqrt2 (I = even bits, Q = odd bits), n ~ N(0, (1/snr)/2) per component,

@@ -1480,6 +1480,69 @@ __global__ __launch_bounds__(256) void stream_emit_kernel(StreamArgs S, int max_
     }
 }
 
+// ---------------------------------------------------------------- hybrid min-sum (CustomMinSum*)
+// CustomMinSumMessageGNNDecoder (message_gnn_decoder.py:1137-1251) cannot run in the reference
+// (MGD:1270 TypeError; its variable / check updates index per-node tensors as if
+// they were per-message, MGD:636-657 / :999-1038).  This build defines the decoder by the updates those
+// loops spell out, per edge m = (check c, variable v), one frame at a time, c2v = 0 at the start:
+//   S_v     = sum of c2v over v's edges, ascending message order               (MGD:650 / :1231)
+//   v2c_m   = (llr_v + S_v) - c2v_m                       "total minus own"     (MGD:650-654)
+//   v2c_m   = 0.5 v2c_m + 0.5 c2v_m    from the second iteration on (damping)  (MGD:659-663)
+//   c2v_m   = prod_{m' != m} sign(v2c_m') * min_{m' != m} |v2c_m'|  (unscaled; the learnable
+//             alpha of MGD:974 is never used by the update, MGD:1009-1032)       (MGD:1006-1038)
+//   probs_v = sigmoid(llr_v + S_v) after the last iteration                     (MGD:1222-1240)
+// Same streaming layout as above (msg[e][b]); the check phase is stream_check_kernel<MINSUM> with
+// alpha = 1 (exact: 1 * min = min).  Oracle: oracle/ldpc_oracle.c ldpc_oracle_custom_minsum.
+template <int DV>
+__device__ __forceinline__ void custom_col(const StreamArgs &S, float *m, const int32_t *edges, float l, bool damp) {
+    float c[DV];
+    int64_t off[DV];
+#pragma unroll
+    for (int p = 0; p < DV; ++p) {
+        off[p] = (int64_t)edges[p] * S.B;
+        c[p] = m[off[p]];
+    }
+    float sum = c[0];
+#pragma unroll
+    for (int p = 1; p < DV; ++p) sum = sum + c[p];
+    const float total = l + sum;
+#pragma unroll
+    for (int p = 0; p < DV; ++p) {
+        float v = total - c[p];
+        if (damp) v = 0.5f * v + 0.5f * c[p];
+        m[off[p]] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void custom_var_kernel(StreamArgs S, int damp) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)S.N * S.B) return;
+    const int64_t j = t / S.B, b = t - j * S.B;
+    const int p0 = S.var_ptr[j], dv = S.var_ptr[j + 1] - p0;
+    const float l = S.llrT[t];
+    switch (dv) {  // degrees above 32 are refused on the host; a variable without edges sends nothing
+#define X(n) case n: custom_col<n>(S, S.msg + b, S.var_edge + p0, l, damp != 0); break;
+        LDPC_STREAM_DEG_CASES(X)
+#undef X
+        default: break;
+    }
+}
+
+// probsT[v][b] = sigmoid(llr_v + S_v), S_v in ascending message order
+__global__ __launch_bounds__(256) void custom_output_kernel(StreamArgs S, float *__restrict__ probsT) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)S.N * S.B) return;
+    const int64_t j = t / S.B, b = t - j * S.B;
+    const int p0 = S.var_ptr[j], p1 = S.var_ptr[j + 1];
+    float out = S.llrT[t];
+    if (p1 > p0) {
+        float sum = S.msg[(int64_t)S.var_edge[p0] * S.B + b];
+        for (int p = p0 + 1; p < p1; ++p) sum = sum + S.msg[(int64_t)S.var_edge[p] * S.B + b];
+        out = out + sum;
+    }
+    probsT[t] = 1.0f / (1.0f + expf(-out));
+}
+
 // ---------------------------------------------------------------- host side
 #ifndef LDPC_FLOOD_KERNELS_ONLY  // (defined by kernel-only experiment builds)
 namespace {
@@ -1589,6 +1652,39 @@ int run_stream(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, f
     hipLaunchKernelGGL(counters_reduce_kernel, dim3(1), dim3(1024), 0, s, w.partials, (B + 63) / 64, counters,
                        es == LDPC_ES_OFF ? nullptr : batch_iters, nullptr);
     LDPC_CHECK_LAUNCH("counters_reduce_kernel");
+    return LDPC_OK;
+}
+
+// CustomMinSum workspace: the streaming arrays (msg, llrT) + probsT [N][B]
+int64_t custom_ws_bytes(const ldpc_graph *g, int64_t B) {
+    return (int64_t)(align256((size_t)g->E * B * 4) + 2 * align256((size_t)g->N * B * 4));
+}
+
+int run_custom_minsum(const ldpc_graph *g, const float *llr, int64_t B, int iterations, float *probs, void *work,
+                      hipStream_t s) {
+    char *base = static_cast<char *>(work);
+    StreamArgs S{};
+    S.chk_ptr = g->chk_ptr; S.ev = g->ev; S.var_ptr = g->var_ptr; S.var_edge = g->var_edge;
+    S.M = g->M; S.N = g->N; S.E = g->E; S.B = B;
+    S.msg = reinterpret_cast<float *>(base);
+    S.llrT = reinterpret_cast<float *>(base + align256((size_t)g->E * B * 4));
+    float *probsT = reinterpret_cast<float *>(base + align256((size_t)g->E * B * 4) + align256((size_t)g->N * B * 4));
+    S.alpha = 1.0f;
+    S.es = LDPC_ES_OFF;
+    LDPC_HIP(hipMemsetAsync(S.msg, 0, (size_t)g->E * B * 4, s));  // c2v = 0 (MGD:1193)
+    hipLaunchKernelGGL(stream_transpose_llr_kernel, dim3((unsigned)((B + 63) / 64), (unsigned)((g->N + 63) / 64)),
+                       dim3(256), 0, s, llr, B, g->N, S.llrT);
+    auto blocks = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    for (int it = 0; it < iterations; ++it) {
+        hipLaunchKernelGGL(custom_var_kernel, blocks((int64_t)g->N * B), dim3(256), 0, s, S, it > 0 ? 1 : 0);
+        hipLaunchKernelGGL(stream_check_kernel<LDPC_ALGO_MINSUM>, blocks((int64_t)g->M * B), dim3(256), 0, s, S);
+        LDPC_CHECK_LAUNCH("custom min-sum iteration");
+    }
+    hipLaunchKernelGGL(custom_output_kernel, blocks((int64_t)g->N * B), dim3(256), 0, s, S, probsT);
+    // (N, B) -> (B, N): the transpose kernel with the roles of the two extents swapped
+    hipLaunchKernelGGL(stream_transpose_llr_kernel, dim3((unsigned)((g->N + 63) / 64), (unsigned)((B + 63) / 64)),
+                       dim3(256), 0, s, probsT, (int64_t)g->N, (int)B, probs);
+    LDPC_CHECK_LAUNCH("custom min-sum output");
     return LDPC_OK;
 }
 
@@ -1712,5 +1808,25 @@ extern "C" int ldpc_flood_decode(const ldpc_graph *g, int algo, const float *d_l
                                              d_counters, d_batch_iters, d_work, s)
                : run_flood<LDPC_ALGO_BP>(g, d_llr, B, max_iter, alpha, early_stop, out_dtype, d_bits, d_iters,
                                          d_counters, d_batch_iters, d_work, s);
+}
+
+extern "C" int64_t ldpc_custom_minsum_workspace_size(const ldpc_graph *g, int64_t B) {
+    if (!g || B < 0) return fail(LDPC_EINVAL, "bad arguments");
+    return B == 0 ? 0 : custom_ws_bytes(g, B);
+}
+
+extern "C" int ldpc_custom_minsum_decode(const ldpc_graph *g, const float *d_llr, int64_t B, int iterations,
+                                         float *d_probs, void *d_work, int64_t work_bytes, void *stream) {
+    if (!g) return fail(LDPC_EINVAL, "graph is NULL");
+    if (B < 0) return fail(LDPC_EINVAL, "negative batch");
+    if (iterations < 0 || iterations > 1024) return fail(LDPC_EINVAL, "iterations must be in [0, 1024]");
+    if (B == 0) return LDPC_OK;
+    if (B > 65535LL * 64) return fail(LDPC_EUNSUPPORTED, "batch above 4194240 frames in one call (chunk it)");
+    if (!d_llr || !d_probs) return fail(LDPC_EINVAL, "llr / probs is NULL");
+    if (g->max_dv > kStreamMaxDeg || g->max_dc > kStreamMaxDeg)
+        return fail(LDPC_EUNSUPPORTED, "node degree above " + std::to_string(kStreamMaxDeg));
+    const int64_t need = custom_ws_bytes(g, B);
+    if (!d_work || work_bytes < need) return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes");
+    return run_custom_minsum(g, d_llr, B, iterations, d_probs, d_work, static_cast<hipStream_t>(stream));
 }
 #endif  // LDPC_FLOOD_KERNELS_ONLY

@@ -33,6 +33,8 @@ SIGNATURES = {
     "ldpc_graph_edges": (ctypes.c_int, [_P, _P, _P]),
     "ldpc_graph_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
     "ldpc_flood_workspace_size": (_I64, [_P, _I64, ctypes.c_int, ctypes.c_int]),
+    "ldpc_custom_minsum_workspace_size": (_I64, [_P, _I64]),
+    "ldpc_custom_minsum_decode": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, _P, _I64, _P]),
     "ldpc_flood_decode": (ctypes.c_int, [_P, ctypes.c_int, _P, _I64, ctypes.c_int, _F32, ctypes.c_int,
                                          ctypes.c_int, _P, _P, _P, _P, _P, _I64, _P]),
     "ldpc_awgn_llr": (ctypes.c_int, [_U64, _U64, _F32, _P, _I64, ctypes.c_int, ctypes.c_int, _P, _P]),

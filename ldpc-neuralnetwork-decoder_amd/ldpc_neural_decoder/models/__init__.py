@@ -5,9 +5,14 @@ from ldpc_neural_decoder.models.traditional_decoders import (
     BeliefPropagationDecoder, MinSumScaledDecoder)
 from ldpc_neural_decoder.models.message_gnn_decoder import (
     MessageGNNLayer, MessageGNNDecoder, TannerToMessageGraph, create_message_gnn_decoder)
+from ldpc_neural_decoder.models.custom_decoders import (
+    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder, CustomVariableMessageGNNLayer,
+    create_custom_minsum_message_gnn_decoder)
 
 __all__ = [
     "CheckLayer", "VariableLayer", "ResidualLayer", "OutputLayer", "LDPCNeuralDecoder",
     "BeliefPropagationDecoder", "MinSumScaledDecoder",
     "MessageGNNLayer", "MessageGNNDecoder", "TannerToMessageGraph", "create_message_gnn_decoder",
+    "CustomCheckMessageGNNLayer", "CustomMinSumMessageGNNDecoder", "CustomVariableMessageGNNLayer",
+    "create_custom_minsum_message_gnn_decoder",
 ]

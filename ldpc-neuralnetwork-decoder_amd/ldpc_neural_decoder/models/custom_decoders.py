@@ -1,0 +1,193 @@
+"""Hybrid "Custom*" message decoders (drop-in for message_gnn_decoder.py:585-1291, min-sum part).
+
+The reference's CustomMinSumMessageGNNDecoder (MGD:1137-1251) cannot run: its factory calls
+TannerToMessageGraph() without H (MGD:1270), and its variable / check updates index per-node
+tensors as if they were per-message (MGD:636-657, :999-1038).  This module
+keeps its classes, constructors, parameters (state_dict keys) and forward signature, and defines
+the decode by the updates those loops spell out -- per edge m = (check c, variable v), c2v = 0 at
+the start (MGD:1193), for iteration = 0 .. num_iterations - 1:
+
+  S_v   = sum of c2v over v's edges in ascending message order        (MGD:650, :1231)
+  v2c_m = (llr_v + S_v) - c2v_m                 "total minus own"      (MGD:650-654)
+  v2c_m = 0.5 v2c_m + 0.5 c2v_m     when iteration > 0 (damping)      (MGD:659-663)
+  c2v_m = prod_{m' != m} sign(v2c_m') * min_{m' != m} |v2c_m'|        (MGD:1006-1038)
+          unscaled: the learnable alpha of MGD:974 is never read by the update
+  probs_v = sigmoid(llr_v + S_v)                                       (MGD:1214-1240)
+  loss  = binary_cross_entropy(probs, ground_truth) (mean)             (MGD:1246-1249)
+
+The whole decode runs in libldpc_amd (ldpc_custom_minsum_decode, csrc/flood.hip: streaming
+kernels, any graph).  The check update is pinned to the reference's own check_layer_update
+(tests/golden/make_custom_golden.py); the variable update and damping cannot execute in the
+reference, so their restatement (oracle/ldpc_oracle.c) is the definition.
+"""
+from collections import deque
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ldpc_neural_decoder import _native as N
+from ldpc_neural_decoder.models.message_gnn_decoder import (
+    MessageGNNDecoder, MessageGNNLayer, TannerToMessageGraph)
+
+
+class CustomVariableMessageGNNLayer(MessageGNNLayer):
+    """MGD:585-755: a MessageGNNLayer plus the min-sum variable update's parameters (w_ch, w_res,
+    unused by the update itself) and its residual storage."""
+
+    def __init__(self, num_message_types=1, hidden_dim=64, depth_L=3):
+        super().__init__(num_message_types, hidden_dim)
+        self.depth_L = depth_L
+        self.w_ch = nn.Parameter(torch.ones(1))
+        self.w_res = nn.Parameter(torch.ones(depth_L))
+        self.previous_VL_storage = deque(maxlen=depth_L + 1)
+
+    def variable_layer_update(self, *args, **kwargs):
+        raise NotImplementedError("the hybrid variable update runs inside CustomMinSumMessageGNNDecoder.forward "
+                                  "(libldpc_amd ldpc_custom_minsum_decode); see the module docstring")
+
+
+class CustomCheckMessageGNNLayer(MessageGNNLayer):
+    """MGD:966-1082: a MessageGNNLayer plus the (unused) learnable min-sum scale alpha = 0.8."""
+
+    def __init__(self, num_message_types, hidden_dim, depth=2, dropout=0.0):
+        super().__init__(num_message_types, hidden_dim)
+        self.alpha = nn.Parameter(torch.tensor(0.8))
+
+    def check_layer_update(self, *args, **kwargs):
+        raise NotImplementedError("the hybrid check update runs inside CustomMinSumMessageGNNDecoder.forward "
+                                  "(libldpc_amd ldpc_custom_minsum_decode); see the module docstring")
+
+
+def _graph_from_index_tensors(check_index_tensor, variable_index_tensor, num_checks, num_variables):
+    """Edges (check, variable) of the messages the two index tensors list (rows = nodes, entries =
+    message ids, -1 padding), check-major with variables ascending."""
+    ci = torch.as_tensor(check_index_tensor).cpu().numpy()
+    vi = torch.as_tensor(variable_index_tensor).cpu().numpy()
+    if ci.ndim != 2 or vi.ndim != 2 or ci.shape[0] != num_checks or vi.shape[0] != num_variables:
+        raise ValueError("index tensors must be (num_checks, max_dc) and (num_variables, max_dv)")
+    chk_of, var_of = {}, {}
+    for c in range(ci.shape[0]):
+        for m in ci[c][ci[c] >= 0]:
+            chk_of[int(m)] = c
+    for v in range(vi.shape[0]):
+        for m in vi[v][vi[v] >= 0]:
+            var_of[int(m)] = v
+    if set(chk_of) != set(var_of):
+        raise ValueError("the check and variable index tensors list different messages")
+    pairs = sorted({(chk_of[m], var_of[m]) for m in chk_of})
+    edge_chk = np.array([p[0] for p in pairs], dtype=np.int32)
+    edge_var = np.array([p[1] for p in pairs], dtype=np.int32)
+    return edge_chk, edge_var
+
+
+class CustomMinSumMessageGNNDecoder(MessageGNNDecoder):
+    """MGD:1137-1251.  forward(input_llrs, variable_adjacency, check_adjacency, message_types,
+    variable_to_message_mapping, ground_truth=None) -> probs, or (probs, loss) with ground truth.
+    The adjacency / type / mapping arguments are accepted for signature compatibility; the graph
+    comes from the index tensors (set_variable_index_tensor / set_check_index_tensor), as in the
+    reference's update loops."""
+
+    def __init__(self, num_messages, num_iterations, hidden_dim, num_message_types=1, depth=2, dropout=0.0):
+        super().__init__(num_messages, num_iterations, hidden_dim, num_message_types)
+        self.variable_layer = CustomVariableMessageGNNLayer(num_message_types, hidden_dim, depth)
+        self.check_layer = CustomCheckMessageGNNLayer(num_message_types, hidden_dim, depth, dropout)
+        self.gnn_layers = nn.ModuleList([
+            CustomCheckMessageGNNLayer(num_message_types, hidden_dim, depth, dropout)
+            for _ in range(num_iterations)])
+        self.variable_index_tensor = None
+        self.check_index_tensor = None
+        self._graphs = {}
+
+    def set_variable_index_tensor(self, variable_index_tensor):
+        self.variable_index_tensor = variable_index_tensor
+        self._graphs = {}
+
+    def set_check_index_tensor(self, check_index_tensor):
+        self.check_index_tensor = check_index_tensor
+        self._graphs = {}
+
+    def _graph(self, num_variables, device):
+        if self.variable_index_tensor is None or self.check_index_tensor is None:
+            raise RuntimeError("set_variable_index_tensor / set_check_index_tensor first "
+                               "(create_custom_minsum_message_gnn_decoder does)")
+        key = str(device)
+        if key not in self._graphs:
+            M = torch.as_tensor(self.check_index_tensor).shape[0]
+            ec, ev = _graph_from_index_tensors(self.check_index_tensor, self.variable_index_tensor, M, num_variables)
+            self._graphs[key] = N.NativeGraph(ec, ev, M, num_variables, device)
+        return self._graphs[key]
+
+    def forward(self, input_llrs, variable_adjacency=None, check_adjacency=None, message_types=None,
+                variable_to_message_mapping=None, ground_truth=None):
+        home = input_llrs.device
+        dev = N.device_of(input_llrs)
+        x = input_llrs.to(dev, torch.float32).contiguous()
+        if x.dim() != 2:
+            raise ValueError(f"input_llrs must be (batch, num_variables), got {tuple(input_llrs.shape)}")
+        B, n = x.shape
+        g = self._graph(n, dev)
+        probs = torch.empty((B, n), dtype=torch.float32, device=dev)
+        if B:
+            wsb = N.check(N.lib().ldpc_custom_minsum_workspace_size(g.handle, B))
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            N.check(N.lib().ldpc_custom_minsum_decode(g.handle, N.ptr(x), B, int(self.num_iterations), N.ptr(probs),
+                                                     N.ptr(ws), wsb, N.stream_ptr(dev)))
+        if home != dev:
+            probs = probs.to(home)
+        if ground_truth is not None:
+            return probs, F.binary_cross_entropy(probs, ground_truth.to(probs.device).float())
+        return probs
+
+    def decode(self, input_llrs, *args, **kwargs):
+        """Hard decisions (probs > 0.5) -- the MessageGNNDecoder.decode convention (MGD:319-353)."""
+        with torch.no_grad():
+            probs = self.forward(input_llrs, *args, **kwargs)
+        return (probs > 0.5).float()
+
+
+def create_variable_index_tensor(H, converter):
+    """MGD:938-964: (num_vars, max variable degree) message ids, -1 padding."""
+    num_vars = H.shape[1]
+    width = max(len(v) for v in converter.var_to_messages.values())
+    out = -torch.ones((num_vars, width), dtype=torch.long)
+    for v in range(num_vars):
+        msgs = converter.var_to_messages[v]
+        out[v, :len(msgs)] = torch.as_tensor(msgs, dtype=torch.long)
+    return out
+
+
+def create_check_index_tensor(H, message_type_map=None):
+    """MGD:1085-1134: (num_checks, max check degree), -1 padding.  With message_type_map
+    ({(check, variable): message id}) the entries are message ids; without it the reference's
+    fallback id c * num_variables + v."""
+    Hn = np.asarray(torch.as_tensor(H).cpu())
+    M, Nv = Hn.shape
+    width = int(Hn.sum(axis=1).max())
+    out = torch.full((M, width), -1, dtype=torch.long)
+    for c in range(M):
+        k = 0
+        for v in np.nonzero(Hn[c] > 0)[0]:
+            if message_type_map is not None:
+                m = message_type_map.get((c, int(v)))
+                if m is None:
+                    continue
+            else:
+                m = c * Nv + int(v)
+            out[c, k] = m
+            k += 1
+    return out
+
+
+def create_custom_minsum_message_gnn_decoder(H, num_iterations=5, hidden_dim=8, depth=2, dropout=0.0):
+    """MGD:1254-1292 -> (decoder, converter), with the converter built from H (the reference's
+    TannerToMessageGraph() call without H fails) and the index tensors in message ids."""
+    converter = TannerToMessageGraph(H)
+    num_messages = len(converter.messages)
+    num_message_types = 1
+    decoder = CustomMinSumMessageGNNDecoder(num_messages, num_iterations, hidden_dim, num_message_types, depth,
+                                            dropout)
+    decoder.set_variable_index_tensor(create_variable_index_tensor(H, converter))
+    decoder.set_check_index_tensor(create_check_index_tensor(H, converter.message_type_map))
+    return decoder, converter

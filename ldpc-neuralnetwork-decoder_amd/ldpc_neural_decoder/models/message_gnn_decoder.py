@@ -456,6 +456,12 @@ class TannerToMessageGraph:
             self._map = m
         return self._map
 
+    @property
+    def message_type_map(self):
+        """{(check, variable): message id} -- what the reference's Custom* factory expects of its
+        converter (MGD:1273-1286)."""
+        return {(c, v): m for m, (v, c) in enumerate(self.messages)}
+
     def message_to_var_index(self):
         """The 1-D message -> variable index (the mapping form the decoder wants)."""
         return torch.as_tensor(self.edge_var.astype(np.int64))
@@ -501,3 +507,9 @@ def load_message_gnn_model(model_path, H, device):
         decoder = MessageGNNDecoder(len(converter.messages), num_iterations, hidden_dim, T)
     decoder.load_state_dict(sd)
     return decoder.to(device), converter
+
+
+# Hybrid Custom* decoders (MGD:585-1291), importable from here as in the reference
+from ldpc_neural_decoder.models.custom_decoders import (  # noqa: E402
+    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder, CustomVariableMessageGNNLayer,
+    create_check_index_tensor, create_custom_minsum_message_gnn_decoder, create_variable_index_tensor)

@@ -46,6 +46,9 @@ def lib():
                                               ctypes.c_int64, P]
         _lib.ldpc_oracle_set_threads.argtypes = [ctypes.c_int]
         _lib.ldpc_oracle_set_threads.restype = ctypes.c_int
+        _lib.ldpc_oracle_custom_minsum.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P,
+                                                   ctypes.c_int64, ctypes.c_int, P]
+        _lib.ldpc_oracle_custom_minsum.restype = ctypes.c_int
     return _lib
 
 
@@ -107,6 +110,19 @@ def flood_decode(graph, llr, algo, max_iter, alpha=0.75, early_stop=0):
     if r < 0:
         raise MemoryError("oracle allocation failed")
     return bits, app, r, iters
+
+
+def custom_minsum(graph, llr, iterations):
+    """Hybrid min-sum (CustomMinSumMessageGNNDecoder, message_gnn_decoder.py:1167-1251) under the
+    semantics this build defines for it (ldpc_oracle.c).  Returns probs f32 (B, N)."""
+    llr = np.ascontiguousarray(llr, dtype=np.float32)
+    probs = np.zeros_like(llr)
+    r = lib().ldpc_oracle_custom_minsum(graph.M, graph.N, graph.E, _p(graph.chk_ptr), _p(graph.edge_var),
+                                        _p(graph.var_ptr), _p(graph.var_edge), _p(llr), llr.shape[0],
+                                        int(iterations), _p(probs))
+    if r < 0:
+        raise MemoryError("oracle allocation failed")
+    return probs
 
 
 def syndrome_valid(graph, bits):
