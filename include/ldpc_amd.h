@@ -167,6 +167,17 @@ int ldpc_gnn_plan_create_csr(int64_t E, const int32_t *h_v_ptr, const int32_t *h
                              const int32_t *h_c_ptr, const int32_t *h_c_col, const float *h_c_val,
                              ldpc_gnn_plan **out);
 int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p);
+/* Hybrid GNN (CustomVariableMessageGNNDecoder.forward, models/message_gnn_decoder.py:798-879 with
+ * CustomVariableMessageGNNLayer.forward :672-755).  The reference cannot run it;
+ * the semantics this build defines (check-side MLP + the layer's own output head, min-sum variable
+ * update on those LLRs with damping 0.5, the decoder's Linear(1, H) back to features, mean-normalised
+ * output) are spelled out in csrc/gnn.hip and DESIGN.md.  hidden must be 64; group plans only.
+ * Weights: the ldpc_gnn_forward blob.  d_probs (B, N). */
+int64_t ldpc_gnn_custom_var_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers);
+int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                                const float *d_weights, const int32_t *d_msg_type,
+                                const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
+                                float *d_probs, void *d_work, int64_t work_bytes, void *stream);
 int64_t ldpc_gnn_weights_size(int hidden, int types, int layers);
 int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers,
                                 int precision);

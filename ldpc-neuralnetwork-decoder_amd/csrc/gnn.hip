@@ -106,6 +106,7 @@ struct GnnLayer {
     float *x_out;    // (B, E, H); null on the last layer unless training saves its features
     float *msg_out;  // (B, E) projected message LLRs, last layer only
     int residual, last;
+    int vside;       // 0: the check side alone (hybrid decoder, gnn_custom_var_forward)
     int d1;          // degree-1 var groups have no Mv row: the MLP uses the message's own c as g
 };
 
@@ -452,6 +453,7 @@ struct ProjTiles {
     const int4 *meta;
     const int32_t *grp, *deg, *mem;
     int n_tiles;
+    int first;  // tiles before `first` are skipped (the var-side tiles, for the check side alone)
 };
 
 template <int NT>
@@ -475,11 +477,12 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
     // this wave's 32 group means, [32][68] after the shared image
     float *gm = lds + kPOffEmb + P.T * kPS + wave * 32 * kPS;
     const int c4 = 4 * (lane & 15), r4 = lane >> 4;
-    const int64_t ntiles = P.B * T.n_tiles;
+    const int nt = T.n_tiles - T.first;
+    const int64_t ntiles = P.B * nt;
     const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
     for (int64_t tt = tw.first; tt < tw.end; tt += tw.stride) {
-        const int64_t b = tt / T.n_tiles;
-        const int t = (int)(tt - b * T.n_tiles);
+        const int64_t b = tt / nt;
+        const int t = T.first + (int)(tt - b * nt);
         const int4 md = T.meta[t];
         // group means, 16 lanes x 16 B per 256-B row: lane (r, c) owns units 4c .. 4c+3 of the tile's
         // groups 4p + r, p < 8, all eight summed side by side so that every lane keeps eight rows in
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
         lds[kM2OffW2c + o * kPS + k] = P.w2c[i];
     }
     if (tid < 64) {
-        lds[kM2OffB + tid] = P.b2v[tid];
+        lds[kM2OffB + tid] = P.vside ? P.b2v[tid] : 0.0f;
         lds[kM2OffB + 64 + tid] = P.b2c[tid];
         lds[kM2OffB + 128 + tid] = P.last ? P.wo[tid] : 0.0f;
     }
@@ -663,6 +666,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
         asm volatile("" : "+v"(w1lane), "+v"(w2lane));
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
+            if (side == 0 && !P.vside) continue;
             const float *pr = side == 0 ? pv : pc;
             f32x16 h0, h1;
 #pragma unroll
@@ -874,6 +878,81 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     return w;
 }
 
+// ------------------------------------------------------------------------ hybrid GNN (CustomVariable*)
+// CustomVariableMessageGNNDecoder (message_gnn_decoder.py:758-879) cannot run in the reference
+// (SURVEY.md section 0).  This build defines a layer by the steps MGD:672-755 spell out, per frame:
+//   c = x + emb[type];  b = A_c c (check groups);  F = MLP_c([c; b])                      (:704-726)
+//   l_m = output_projection(F_m)                     the layer's own head               (:729)
+//   v2c_m = (llr_v + sum_{m' -> v} l_m') - l_m,  then 0.5 v2c_m + 0.5 l_m  (every layer: the
+//           decoder passes iteration i + 1 >= 1, MGD:851, so the damping of :659-663 always applies)
+//   x <- input_embedding(v2c_m) + F_m   (the decoder's Linear(1, H): the layer has none, :745)  (:745-753)
+// and the decoder's output (:855-877): out_m = output_projection_L(x_m),
+//   probs_v = sigmoid(sum_{m -> v} out_m / deg_v + llr_v)   (row-normalised mapping, :858-870).
+// Kernels: the projection / MLP kernels above on the check side alone (vside = 0), then these.
+
+// v2c (B, E) from the layer's projected check messages l = msg_out (B, E); one thread per (frame,
+// variable), its messages in ascending order (the per-call CSR of msg_var)
+__global__ __launch_bounds__(256) void custom_var_llr_kernel(const float *__restrict__ l, const int32_t *__restrict__ csr,
+                                                             const float *__restrict__ llr, int64_t E, int N, int64_t B,
+                                                             float *__restrict__ v2c) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * N) return;
+    const int64_t b = i / N;
+    const int v = (int)(i - b * N);
+    const int32_t *ptr = csr_ptr(csr), *mem = csr_mem(csr, N);
+    const int p0 = ptr[v], p1 = ptr[v + 1];
+    if (p1 == p0) return;
+    const float *lb = l + b * E;
+    float sum = lb[mem[p0]];
+    for (int q = p0 + 1; q < p1; ++q) sum = sum + lb[mem[q]];
+    const float total = llr[i] + sum;
+    for (int q = p0; q < p1; ++q) {
+        const float c = lb[mem[q]];
+        const float x = total - c;
+        v2c[b * E + mem[q]] = 0.5f * x + 0.5f * c;
+    }
+}
+
+// x_m = (v2c_m w_in + b_in) + F_m in place (64 floats per message, 16 lanes x float4); on the last
+// layer instead out_m = wo . x_m + bo into msg_out
+__global__ __launch_bounds__(256) void custom_combine_kernel(float *__restrict__ x, const float *__restrict__ v2c,
+                                                             const float *__restrict__ w_in, const float *__restrict__ b_in,
+                                                             int64_t R, const float *__restrict__ wo,
+                                                             const float *__restrict__ bo, float *__restrict__ msg_out) {
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int q = threadIdx.x & 15;
+    if (r >= R) return;
+    const float v = v2c[r];
+    float4 *xr = reinterpret_cast<float4 *>(x + r * 64) + q;
+    const float4 f = *xr, w = reinterpret_cast<const float4 *>(w_in)[q], c = reinterpret_cast<const float4 *>(b_in)[q];
+    const float4 o = make_float4((v * w.x + c.x) + f.x, (v * w.y + c.y) + f.y, (v * w.z + c.z) + f.z, (v * w.w + c.w) + f.w);
+    if (!wo) {
+        *xr = o;
+        return;
+    }
+    const float4 k = reinterpret_cast<const float4 *>(wo)[q];
+    float part = o.x * k.x + o.y * k.y + o.z * k.z + o.w * k.w;
+    for (int off = 8; off > 0; off >>= 1) part += __shfl_xor(part, off, 16);
+    if (q == 0) msg_out[r] = part + bo[0];
+}
+
+// probs[b][v] = sigmoid(sum_{m -> v} out_m * (1 / deg_v) + llr[b][v]), ascending message order
+__global__ void custom_output_kernel(const float *__restrict__ msg_out, const int32_t *__restrict__ csr,
+                                     const float *__restrict__ llr, int64_t E, int N, int64_t n,
+                                     float *__restrict__ probs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t b = i / N;
+    const int v = (int)(i - b * N);
+    const int32_t *ptr = csr_ptr(csr), *mem = csr_mem(csr, N);
+    const int p0 = ptr[v], p1 = ptr[v + 1];
+    const float w = 1.0f / ((float)(p1 - p0) + 1e-10f);  // mapping / (row sum + 1e-10), :859
+    const float *mo = msg_out + b * E;
+    float s = 0.0f;
+    for (int q = p0; q < p1; ++q) s += mo[mem[q]] * w;
+    probs[i] = 1.0f / (1.0f + expf(-(s + llr[i])));
+}
+
 int g_num_cus = 0;
 
 constexpr int kMlp2Wps = LDPC_MLP2_WPS, kMlp2Nt = LDPC_MLP2_NT;
@@ -1025,6 +1104,7 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         }
     };
     add_ptiles(vptr, vmem, n_vgroups, 0);
+    const int n_ptiles_v = (int)(pt_meta.size() / 4);
     add_ptiles(cptr, cmem, n_cgroups, 1);
     pt.insert(pt.end(), pt_meta.begin(), pt_meta.end());
     pt.insert(pt.end(), pt_grp.begin(), pt_grp.end());
@@ -1064,6 +1144,7 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         return fail(LDPC_EHIP, "GNN plan upload failed");
     }
     p->n_ptiles = (int)(pt_meta.size() / 4);
+    p->n_ptiles_v = n_ptiles_v;
     p->pt_meta = reinterpret_cast<const int4 *>(p->d_pt);
     p->pt_grp = p->d_pt + pt_meta.size();
     p->pt_deg = p->pt_grp + pt_grp.size();
@@ -1196,6 +1277,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     L.Gv = p->Gv; L.Gc = p->Gc;
     L.E = p->E; L.B = B;
     L.Mv = w.Mv; L.Mc = w.Mc;
+    L.vside = 1;
     const bool mfma = H == kMfmaH;
     if (!mfma && H > 128) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be 64 (MFMA path) or <= 128");
     const size_t mfma_lds = (size_t)(kOffEmb + types * kEmbStride) * 4;
@@ -1257,7 +1339,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.d1 = H == 64 && gm_tiles() && d1_skip() && !p->weighted;
         if (proj) {
             L.d1 = 0;
-            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles};
+            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, 0};
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;
             const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
@@ -1357,4 +1439,86 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
                                 void *stream) {
     return ldpc_gnn_forward_ex(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, precision, 0,
                                d_probs, nullptr, d_work, work_bytes, stream);
+}
+
+// ------------------------------------------------------------------------ hybrid GNN host side
+extern "C" int64_t ldpc_gnn_custom_var_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers) {
+    if (!p || hidden <= 0 || N <= 0 || B < 0 || layers <= 0) return fail(LDPC_EINVAL, "bad arguments");
+    // carve() with at least 3 layers keeps both feature buffers; + v2c (B, E)
+    return carve(p, hidden, N, B, std::max(layers, 3), 0, nullptr).bytes + (B * p->E * 4 + 255) / 256 * 256;
+}
+
+extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                                           const float *d_weights, const int32_t *d_msg_type,
+                                           const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
+                                           float *d_probs, void *d_work, int64_t work_bytes, void *stream) {
+    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    if (hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "the hybrid GNN runs at hidden_dim 64");
+    if (p->weighted || p->n_ptiles == 0) return fail(LDPC_EUNSUPPORTED, "the hybrid GNN needs a group plan");
+    if (types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
+    if (B == 0) return LDPC_OK;
+    if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs) return fail(LDPC_EINVAL, "NULL tensor");
+    const int64_t need = ldpc_gnn_custom_var_workspace_size(p, hidden, N, B, layers);
+    if (!d_work || work_bytes < need) return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes");
+    if (B * p->E >= (1LL << 31) / 16) return fail(LDPC_EUNSUPPORTED, "batch too large for one launch (chunk it)");
+    const int H = kMfmaH;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Ws w = carve(p, H, N, B, std::max(layers, 3), 0, d_work);
+    float *v2c = reinterpret_cast<float *>(static_cast<char *>(d_work) + w.bytes);
+    if (!g_num_cus) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const size_t proj_lds = proj_lds_bytes(types, 4), mlp2_lds = mlp2_lds_bytes(types);
+    if (proj_lds > 160 * 1024 || mlp2_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_group_proj_kernel<256>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
+    const int mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
+    const int proj_per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
+    if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
+    GnnLayer L{};
+    L.llr = d_llr; L.msg_var = d_msg_var; L.w_in = d_weights; L.b_in = d_weights + H; L.N = N; L.T = types;
+    L.msg_type = d_msg_type;
+    L.vgroup = p->vgroup; L.cgroup = p->cgroup; L.vg_ptr = p->vg_ptr; L.vg_mem = p->vg_mem;
+    L.cg_ptr = p->cg_ptr; L.cg_mem = p->cg_mem; L.inv_v = p->inv_v; L.inv_c = p->inv_c;
+    L.Gv = p->Gv; L.Gc = p->Gc; L.E = p->E; L.B = B; L.Mv = w.Mv; L.Mc = w.Mc;
+    L.vside = 0; L.residual = 0; L.last = 1; L.d1 = 0;
+    L.msg_out = w.msg_out;
+    const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, p->n_ptiles_v};
+    const int64_t R = B * p->E;
+    const float *x_in = nullptr;
+    for (int l = 0; l < layers; ++l) {
+        const float *lw = d_weights + 2 * H + (int64_t)l * layer_floats(H, types);
+        L.emb = lw;
+        L.w1v = L.emb + (int64_t)types * H; L.b1v = L.w1v + 2LL * H * H; L.w2v = L.b1v + H; L.b2v = L.w2v + (int64_t)H * H;
+        L.w1c = L.b2v + H; L.b1c = L.w1c + 2LL * H * H; L.w2c = L.b1c + H; L.b2c = L.w2c + (int64_t)H * H;
+        L.wo = L.b2c + H; L.bo = L.wo + H;
+        L.x_in = x_in;
+        L.x_out = (l % 2 == 0) ? w.xa : w.xb;  // F, then x in place
+        const int64_t ptiles = B * (int64_t)(T.n_tiles - T.first);
+        hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3((unsigned)std::min<int64_t>((ptiles + 3) / 4, (int64_t)g_num_cus * proj_per_cu)),
+                           dim3(256), proj_lds, s, L, T);
+        LDPC_CHECK_LAUNCH("gnn_group_proj_kernel (check side)");
+        constexpr int wpb = kMlp2Nt / 64;
+        const int64_t tiles = (R + 31) / 32;
+        hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
+                           dim3((unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu)),
+                           dim3(kMlp2Nt), mlp2_lds, s, L);
+        LDPC_CHECK_LAUNCH("gnn_mlp2_kernel (check side)");
+        hipLaunchKernelGGL(custom_var_llr_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, w.msg_out, w.csr,
+                           d_llr, p->E, N, B, v2c);
+        const bool last = l == layers - 1;
+        const float *wl = last ? L.wo : nullptr;  // the decoder's output head: the last layer's (:855)
+        hipLaunchKernelGGL(custom_combine_kernel, dim3((unsigned)((R * 16 + 255) / 256)), dim3(256), 0, s, L.x_out, v2c,
+                           d_weights, d_weights + H, R, wl, L.bo, w.msg_out);
+        LDPC_CHECK_LAUNCH("hybrid GNN variable update");
+        x_in = L.x_out;
+    }
+    hipLaunchKernelGGL(custom_output_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, w.msg_out, w.csr, d_llr,
+                       p->E, N, B * N, d_probs);
+    LDPC_CHECK_LAUNCH("custom_output_kernel");
+    return LDPC_OK;
 }

@@ -32,6 +32,7 @@ struct ldpc_gnn_plan {
     // its degree (0 for padding); pt_mem[off + 32 i + j] = i-th member message of lane j's group
     // (message 0 past its degree; max degree + 1 rows per tile).
     int n_ptiles = 0;
+    int n_ptiles_v = 0;  // the leading tiles are the var side's
     int32_t *d_pt = nullptr;
     const int4 *pt_meta = nullptr;
     const int32_t *pt_grp = nullptr, *pt_deg = nullptr, *pt_mem = nullptr;

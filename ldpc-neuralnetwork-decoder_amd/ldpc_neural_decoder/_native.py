@@ -34,6 +34,9 @@ SIGNATURES = {
     "ldpc_graph_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
     "ldpc_flood_workspace_size": (_I64, [_P, _I64, ctypes.c_int, ctypes.c_int]),
     "ldpc_custom_minsum_workspace_size": (_I64, [_P, _I64]),
+    "ldpc_gnn_custom_var_workspace_size": (_I64, [_P, ctypes.c_int, ctypes.c_int, _I64, ctypes.c_int]),
+    "ldpc_gnn_custom_var_forward": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
+                                                   ctypes.c_int, _I64, _P, _P, _I64, _P]),
     "ldpc_custom_minsum_decode": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, _P, _I64, _P]),
     "ldpc_flood_decode": (ctypes.c_int, [_P, ctypes.c_int, _P, _I64, ctypes.c_int, _F32, ctypes.c_int,
                                          ctypes.c_int, _P, _P, _P, _P, _P, _I64, _P]),

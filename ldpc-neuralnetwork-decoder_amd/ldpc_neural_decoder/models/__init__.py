@@ -6,13 +6,15 @@ from ldpc_neural_decoder.models.traditional_decoders import (
 from ldpc_neural_decoder.models.message_gnn_decoder import (
     MessageGNNLayer, MessageGNNDecoder, TannerToMessageGraph, create_message_gnn_decoder)
 from ldpc_neural_decoder.models.custom_decoders import (
-    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder, CustomVariableMessageGNNLayer,
-    create_custom_minsum_message_gnn_decoder)
+    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder, CustomVariableMessageGNNDecoder,
+    CustomVariableMessageGNNLayer, create_custom_minsum_message_gnn_decoder,
+    create_custom_variable_message_gnn_decoder)
 
 __all__ = [
     "CheckLayer", "VariableLayer", "ResidualLayer", "OutputLayer", "LDPCNeuralDecoder",
     "BeliefPropagationDecoder", "MinSumScaledDecoder",
     "MessageGNNLayer", "MessageGNNDecoder", "TannerToMessageGraph", "create_message_gnn_decoder",
     "CustomCheckMessageGNNLayer", "CustomMinSumMessageGNNDecoder", "CustomVariableMessageGNNLayer",
-    "create_custom_minsum_message_gnn_decoder",
+    "create_custom_minsum_message_gnn_decoder", "CustomVariableMessageGNNDecoder",
+    "create_custom_variable_message_gnn_decoder",
 ]

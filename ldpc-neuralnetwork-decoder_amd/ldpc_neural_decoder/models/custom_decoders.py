@@ -1,4 +1,7 @@
-"""Hybrid "Custom*" message decoders (drop-in for message_gnn_decoder.py:585-1291, min-sum part).
+"""Hybrid "Custom*" message decoders (drop-in for message_gnn_decoder.py:585-1291).
+
+Two decoders: CustomMinSumMessageGNNDecoder (pure message passing, below) and
+CustomVariableMessageGNNDecoder (the GNN's check side + a min-sum variable update, further down).
 
 The reference's CustomMinSumMessageGNNDecoder (MGD:1137-1251) cannot run: its factory calls
 TannerToMessageGraph() without H (MGD:1270), and its variable / check updates index per-node
@@ -20,6 +23,7 @@ kernels, any graph).  The check update is pinned to the reference's own check_la
 (tests/golden/make_custom_golden.py); the variable update and damping cannot execute in the
 reference, so their restatement (oracle/ldpc_oracle.c) is the definition.
 """
+import os
 from collections import deque
 
 import numpy as np
@@ -29,7 +33,7 @@ import torch.nn.functional as F
 
 from ldpc_neural_decoder import _native as N
 from ldpc_neural_decoder.models.message_gnn_decoder import (
-    MessageGNNDecoder, MessageGNNLayer, TannerToMessageGraph)
+    MessageGNNDecoder, MessageGNNLayer, TannerToMessageGraph, _aggregation_specs, _io_mapping, _types_for)
 
 
 class CustomVariableMessageGNNLayer(MessageGNNLayer):
@@ -44,8 +48,8 @@ class CustomVariableMessageGNNLayer(MessageGNNLayer):
         self.previous_VL_storage = deque(maxlen=depth_L + 1)
 
     def variable_layer_update(self, *args, **kwargs):
-        raise NotImplementedError("the hybrid variable update runs inside CustomMinSumMessageGNNDecoder.forward "
-                                  "(libldpc_amd ldpc_custom_minsum_decode); see the module docstring")
+        raise NotImplementedError("the hybrid variable update runs inside the decoders' forward (libldpc_amd "
+                                  "ldpc_custom_minsum_decode / ldpc_gnn_custom_var_forward); see the module docstring")
 
 
 class CustomCheckMessageGNNLayer(MessageGNNLayer):
@@ -190,4 +194,104 @@ def create_custom_minsum_message_gnn_decoder(H, num_iterations=5, hidden_dim=8, 
                                             dropout)
     decoder.set_variable_index_tensor(create_variable_index_tensor(H, converter))
     decoder.set_check_index_tensor(create_check_index_tensor(H, converter.message_type_map))
+    return decoder, converter
+
+
+class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
+    """MGD:758-879.  The reference cannot run it (IndexError at MGD:829-834 /
+    :637-654, and MGD:745 calls a Linear(1, H) the layer does not have).  This build defines each
+    layer i by the steps MGD:672-755 spell out, per frame and message m (check c, variable v):
+
+      c    = x + emb_i[type]                                                   (:704-709)
+      b    = A_c c  (the check adjacency; the identity when none is given, :825-826)
+      F    = check_to_var_update_i([c; b])                                     (:724-726)
+      l_m  = output_projection_i(F_m)                                          (:729)
+      v2c_m = (llr_v + sum_{m' -> v} l_m') - l_m, then 0.5 v2c_m + 0.5 l_m     (:650-663; the
+             decoder passes iteration i + 1 >= 1, :851, so the damping applies at every layer)
+      x    = input_embedding(v2c_m) + F_m    (the decoder's Linear(1, H))      (:745-753)
+
+    and the output (:855-877): out_m = output_projection_L(x_m), probs_v = sigmoid(mean over v's
+    messages of out_m + llr_v).  forward(...) returns (probs, None), or (probs, max over bits of
+    the per-bit BCE) with ground truth, as the reference does.  Inference only (no backward);
+    hidden_dim 64; clique / identity check adjacencies.  Kernels: ldpc_gnn_custom_var_forward
+    (csrc/gnn.hip).  Oracle: oracle/oracle.py custom_variable_forward."""
+
+    def __init__(self, num_messages, num_iterations=5, hidden_dim=64, num_message_types=1, depth_L=3):
+        super().__init__(num_messages, num_iterations, hidden_dim, num_message_types)
+        self.gnn_layers = nn.ModuleList([
+            CustomVariableMessageGNNLayer(num_message_types, hidden_dim, depth_L) for _ in range(num_iterations)])
+        self.variable_index_tensor = None
+
+    def set_variable_index_tensor(self, variable_index_tensor):
+        self.variable_index_tensor = variable_index_tensor
+
+    def forward(self, input_llr, message_to_var_mapping, message_types=None, var_to_check_adjacency=None,
+                check_to_var_adjacency=None, ground_truth=None):
+        home = input_llr.device
+        dev = N.device_of(input_llr)
+        E = self.num_messages
+        llr = input_llr.to(dev, torch.float32).contiguous()
+        B, Nv = llr.shape
+        io_map = _io_mapping(message_to_var_mapping, E, Nv, dev)
+        T = self.gnn_layers[0].message_type_embeddings.shape[0]
+        types = _types_for(message_types, E, T, dev)
+        vspec = (io_map.cpu().numpy().astype(np.int64), Nv)  # the plan's var side (unused by the kernels)
+        if check_to_var_adjacency is None:
+            cspec = (np.arange(E, dtype=np.int64), E)          # torch.eye (:825-826): every message alone
+        else:
+            _, cspec = _aggregation_specs(var_to_check_adjacency if var_to_check_adjacency is not None
+                                          else check_to_var_adjacency, check_to_var_adjacency, E)
+            if isinstance(cspec[0], str) and cspec[0] == "csr":
+                raise NotImplementedError("the hybrid GNN runs with clique (TannerToMessageGraph) or identity "
+                                          "check adjacencies")
+        if self.hidden_dim != 64:
+            raise NotImplementedError("the hybrid GNN runs at hidden_dim 64")
+        plan = self._plan(vspec, cspec, dev)
+        blob = self._weights_blob(dev)
+        L = len(self.gnn_layers)
+        probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
+        if B:
+            lib = N.lib()
+            ws1 = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, 64, Nv, 1, L))
+            per = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, 64, Nv, 2, L)) - ws1
+            budget = int(os.environ.get("LDPC_GNN_WORKSPACE_BYTES", 48 << 30))
+            limit = max(1, ((1 << 31) // 16 - 1) // E)  # the kernels' per-launch message bound
+            chunk = max(1, min(B, limit, max(1, (budget - ws1) // max(per, 1))))
+            wsb = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, 64, Nv, chunk, L))
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            with torch.no_grad():
+                for s in range(0, B, chunk):
+                    n = min(chunk, B - s)
+                    N.check(lib.ldpc_gnn_custom_var_forward(
+                        plan.handle, 64, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr[s:s + n]), Nv, n,
+                        N.ptr(probs[s:s + n]), N.ptr(ws), wsb, N.stream_ptr(dev)))
+        if home != dev:
+            probs = probs.to(home)
+        if ground_truth is not None:
+            loss = F.binary_cross_entropy(probs, ground_truth.to(probs.device).float(), reduction="none")
+            return probs, torch.max(loss, dim=1).values
+        return probs, None
+
+    def decode(self, input_llr, message_to_var_mapping, message_types=None, var_to_check_adjacency=None,
+               check_to_var_adjacency=None):
+        with torch.no_grad():
+            probs, _ = self.forward(input_llr, message_to_var_mapping, message_types, var_to_check_adjacency,
+                                    check_to_var_adjacency)
+        return (probs > 0.5).float()
+
+
+def create_custom_variable_message_gnn_decoder(H, num_iterations=5, hidden_dim=64, depth_L=3, base_graph=None, Z=None):
+    """MGD:882-936 -> (decoder, converter)."""
+    converter = TannerToMessageGraph(H)
+    num_messages = len(converter.messages)
+    if base_graph is not None and Z is not None:
+        base = np.asarray(torch.as_tensor(base_graph).cpu())
+        shifts = {int(v) for v in base.ravel() if v >= 0}
+        num_message_types = len(shifts) if shifts else 1
+    else:
+        num_message_types = 1
+    decoder = CustomVariableMessageGNNDecoder(num_messages=num_messages, num_iterations=num_iterations,
+                                              hidden_dim=hidden_dim, num_message_types=num_message_types,
+                                              depth_L=depth_L)
+    decoder.set_variable_index_tensor(create_variable_index_tensor(H, converter))
     return decoder, converter

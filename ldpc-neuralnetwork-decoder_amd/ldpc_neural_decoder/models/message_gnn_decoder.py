@@ -511,5 +511,6 @@ def load_message_gnn_model(model_path, H, device):
 
 # Hybrid Custom* decoders (MGD:585-1291), importable from here as in the reference
 from ldpc_neural_decoder.models.custom_decoders import (  # noqa: E402
-    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder, CustomVariableMessageGNNLayer,
-    create_check_index_tensor, create_custom_minsum_message_gnn_decoder, create_variable_index_tensor)
+    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder, CustomVariableMessageGNNDecoder,
+    CustomVariableMessageGNNLayer, create_check_index_tensor, create_custom_minsum_message_gnn_decoder,
+    create_custom_variable_message_gnn_decoder, create_variable_index_tensor)

@@ -192,6 +192,58 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
     return probs
 
 
+def custom_variable_forward(sd, llr, msg_var_io, edge_chk, num_vars, num_checks, types=None, check_identity=False,
+                            ground_truth=None):
+    """CustomVariableMessageGNNDecoder.forward (message_gnn_decoder.py:798-879, layer :672-755) under the
+    semantics this build defines for it (models/custom_decoders.py; the reference cannot run it):
+    per layer the check side's MLP over [c; A_c c] (A_c = group mean over the check's messages, or the
+    identity), the layer's output head on it, the damped min-sum variable update on those LLRs and the
+    decoder's Linear(1, H) back to features; output = sigmoid(mean of the last head over a variable's
+    messages + llr).  torch fp32; returns probs, or (probs, max per-bit BCE) with ground truth."""
+    import torch
+    import torch.nn.functional as F
+
+    llr = torch.as_tensor(llr, dtype=torch.float32)
+    mv = torch.as_tensor(msg_var_io, dtype=torch.long)
+    ec = torch.as_tensor(edge_chk, dtype=torch.long)
+    B, E = llr.shape[0], mv.numel()
+    n_layers = len({k.split(".")[1] for k in sd if k.startswith("gnn_layers.")})
+    w_in, b_in = sd["input_embedding.weight"][:, 0], sd["input_embedding.bias"]
+    x = llr[:, mv].unsqueeze(-1) * w_in + b_in
+    t = torch.zeros(E, dtype=torch.long) if types is None else torch.as_tensor(types).long()
+    deg_c = torch.bincount(ec, minlength=num_checks).float()
+    deg_v = torch.bincount(mv, minlength=num_vars).float()
+
+    def mlp(p, z):
+        h = torch.relu(z @ sd[p + ".0.weight"].T + sd[p + ".0.bias"])
+        return h @ sd[p + ".2.weight"].T + sd[p + ".2.bias"]
+
+    for i in range(n_layers):
+        p = f"gnn_layers.{i}."
+        emb = sd[p + "message_type_embeddings"]
+        c = x + emb[t.clamp(0, emb.shape[0] - 1)]
+        if check_identity:
+            b = c
+        else:
+            s = torch.zeros(B, num_checks, c.shape[-1]).index_add_(1, ec, c)
+            b = (s / deg_c.clamp(min=1).view(1, -1, 1))[:, ec]
+        Fm = mlp(p + "check_to_var_update", torch.cat([c, b], 2))
+        lm = Fm @ sd[p + "output_projection.weight"][0] + sd[p + "output_projection.bias"][0]
+        tot = llr + torch.zeros(B, num_vars).index_add_(1, mv, lm)
+        v2c = tot[:, mv] - lm
+        v2c = 0.5 * v2c + 0.5 * lm
+        x = (v2c.unsqueeze(-1) * w_in + b_in) + Fm
+    last = f"gnn_layers.{n_layers - 1}.output_projection."
+    out = (x @ sd[last + "weight"][0]) + sd[last + "bias"][0]
+    w = 1.0 / (deg_v + 1e-10)
+    var_llrs = torch.zeros(B, num_vars).index_add_(1, mv, out * w[mv])
+    probs = torch.sigmoid(var_llrs + llr)
+    if ground_truth is not None:
+        loss = F.binary_cross_entropy(probs, torch.as_tensor(ground_truth).float(), reduction="none")
+        return probs, loss.max(dim=1).values
+    return probs
+
+
 def gnn_forward_dense(sd, llr, msg_var_io, num_vars, Av, Ac, types=None):
     """MessageGNNDecoder.forward restated with the reference's own aggregation: dense
     bmm(A, x + emb) with whatever adjacencies are given, zero-padded / cropped to E as

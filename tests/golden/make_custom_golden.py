@@ -15,7 +15,8 @@ for seeded inputs (with exact zeros for torch.sign(0) = 0) on BG2 Z = 4, as plai
   custom_check_z4.npz   llr (B, N) f32; msg_chk, msg_var (E,) int32 check-major message list;
                         c2v (B, E) f32 = check_layer_update(llr[:, msg_var]) from the reference;
                         sd_keys / sd_numel: CustomMinSumMessageGNNDecoder(E, 3, 8, 1, 2, 0.0)'s
-                        state_dict layout (numel, 0 for scalars; its constructor runs, its factory does not).
+                        state_dict layout (numel, 0 for scalars; its constructor runs, its factory does not);
+                        sdv_keys / sdv_numel: the same for CustomVariableMessageGNNDecoder(E, 3, 64, 1, 3).
 """
 import contextlib
 import io
@@ -31,7 +32,7 @@ sys.path.insert(0, REF)
 
 from ldpc_neural_decoder.utils.ldpc_utils import load_base_matrix, expand_base_matrix  # noqa: E402
 from ldpc_neural_decoder.models.message_gnn_decoder import (  # noqa: E402
-    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder)
+    CustomCheckMessageGNNLayer, CustomMinSumMessageGNNDecoder, CustomVariableMessageGNNDecoder)
 
 
 def main():
@@ -72,8 +73,12 @@ def main():
     sd = CustomMinSumMessageGNNDecoder(E, 3, 8, 1, 2, 0.0).state_dict()
     keys = sorted(sd)
     shapes = np.array([len(sd[k].shape) and int(np.prod(sd[k].shape)) for k in keys], dtype=np.int64)
+    sdv = CustomVariableMessageGNNDecoder(E, 3, 64, 1, 3).state_dict()
+    vkeys = sorted(sdv)
+    vshapes = np.array([len(sdv[k].shape) and int(np.prod(sdv[k].shape)) for k in vkeys], dtype=np.int64)
     np.savez(os.path.join(HERE, "custom_check_z4.npz"), llr=llr.numpy(), msg_chk=msg_chk, msg_var=msg_var,
-             c2v=c2v.detach().numpy().astype(np.float32), sd_keys=np.array(keys), sd_numel=shapes)
+             c2v=c2v.detach().numpy().astype(np.float32), sd_keys=np.array(keys), sd_numel=shapes,
+             sdv_keys=np.array(vkeys), sdv_numel=vshapes)
     print("custom_check_z4.npz", E, "messages", B, "frames")
 
 

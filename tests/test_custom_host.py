@@ -139,3 +139,12 @@ def test_index_tensors_rebuild_the_graph():
     for c in range(12):
         row = ci[c][ci[c] >= 0].tolist()
         assert row == conv.check_to_messages[c]
+
+
+def test_variable_decoder_state_dict_layout_matches_reference():
+    from ldpc_neural_decoder.models import CustomVariableMessageGNNDecoder
+    d = golden("custom_check_z4.npz")
+    dec = CustomVariableMessageGNNDecoder(len(d["msg_chk"]), 3, 64, 1, 3)
+    sd = dec.state_dict()
+    assert sorted(sd) == list(d["sdv_keys"])
+    assert [len(sd[k].shape) and sd[k].numel() for k in sorted(sd)] == list(d["sdv_numel"])
