@@ -197,6 +197,20 @@ def create_custom_minsum_message_gnn_decoder(H, num_iterations=5, hidden_dim=8, 
     return decoder, converter
 
 
+def _one_hot_index(mapping, E, Nv, device):
+    """The reference multiplies by message_to_var_mapping (MGD:829-830, :858-864): the (E, N) one-hot of
+    TannerToMessageGraph.message_to_var_mapping.  Accepted as that matrix or as its 1-D index."""
+    m = torch.as_tensor(mapping)
+    if m.dim() == 2:
+        if m.shape != (E, Nv):
+            raise ValueError(f"message_to_var_mapping must be ({E}, {Nv}), got {tuple(m.shape)}")
+        mf = m.float()
+        if not bool(((mf == 0) | (mf == 1)).all()) or not bool((mf.sum(dim=1) == 1).all()):
+            raise NotImplementedError("message_to_var_mapping must be one-hot per message")
+        m = mf.argmax(dim=1)
+    return _io_mapping(m.long(), E, Nv, device)
+
+
 class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
     """MGD:758-879.  The reference cannot run it (IndexError at MGD:829-834 /
     :637-654, and MGD:745 calls a Linear(1, H) the layer does not have).  This build defines each
@@ -232,7 +246,7 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
         E = self.num_messages
         llr = input_llr.to(dev, torch.float32).contiguous()
         B, Nv = llr.shape
-        io_map = _io_mapping(message_to_var_mapping, E, Nv, dev)
+        io_map = _one_hot_index(message_to_var_mapping, E, Nv, dev)
         T = self.gnn_layers[0].message_type_embeddings.shape[0]
         types = _types_for(message_types, E, T, dev)
         vspec = (io_map.cpu().numpy().astype(np.int64), Nv)  # the plan's var side (unused by the kernels)
