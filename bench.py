@@ -27,6 +27,10 @@ Workloads (BASELINE.json configs):
               VariableLayer -> ResidualLayer(depth 2) + OutputLayer on the var-major edge vector
   gnn-train-z32 / gnn-train-z4  one training step (fp32 forward saving features, BCE, HIP backward,
                 SGD with the trainer's momentum 0.9 / weight decay 1e-4), frames/s
+  hybrid-minsum-z32  CustomMinSumMessageGNNDecoder as this build defines it (models/custom_decoders.py):
+              damped, unscaled min-sum on the streaming kernels, soft output, 10 iterations
+  hybrid-gnn-z32     CustomVariableMessageGNNDecoder as defined there: check-side MLP + damped
+              min-sum variable update, 10 layers, fp32
 """
 import argparse
 import json
@@ -63,6 +67,8 @@ WORKLOADS = {
     "gnn-train-z32": ("gnn-train", 32, 10, 256, 2.0),
     "lay-z32": ("lay", 32, 10, 4096, 2.0),
     "gnn-train-z4": ("gnn-train", 4, 5, 4096, 2.0),
+    "hybrid-minsum-z32": ("hybrid-minsum", 32, 10, 65536, 2.0),
+    "hybrid-gnn-z32": ("hybrid-gnn", 32, 10, 32768, 2.0),
 }
 
 
@@ -162,6 +168,37 @@ def cpu_baseline(workload, z, iters, target_s):
         noise = rng.normal(0.0, np.sqrt(1 / (2 * s)), size=(b, g.N))
         return (2 * s * (1 / np.sqrt(2) + noise)).astype(np.float32)
 
+    if kind.startswith("hybrid"):
+        if kind == "hybrid-minsum":
+            def run(b):
+                oracle.custom_minsum(g, sample(b), iters)
+            what = "oracle/ldpc_oracle.c custom_minsum, 1 thread"
+        else:
+            from ldpc_neural_decoder.models import create_custom_variable_message_gnn_decoder
+            torch.manual_seed(7)
+            dec, conv = create_custom_variable_message_gnn_decoder(torch.from_numpy(H), num_iterations=iters,
+                                                                   hidden_dim=64, base_graph=torch.from_numpy(base),
+                                                                   Z=z)
+            sd = {k: v.detach() for k, v in dec.state_dict().items()}
+            types = conv.get_message_types(torch.from_numpy(base), z)
+
+            def run(b):
+                with torch.no_grad():
+                    oracle.custom_variable_forward(sd, torch.from_numpy(sample(b)), conv.edge_var, conv.edge_chk,
+                                                   g.N, g.M, types)
+            what = f"oracle.custom_variable_forward (torch CPU, {torch.get_num_threads()} threads)"
+        run(1)
+        b = 2
+        t0 = time.perf_counter()
+        run(b)
+        dt = max(time.perf_counter() - t0, 1e-6)
+        b = int(min(1 << 16, max(2, b * target_s / dt)))
+        t0 = time.perf_counter()
+        run(b)
+        dt = time.perf_counter() - t0
+        cores = 1 if kind == "hybrid-minsum" else torch.get_num_threads()
+        return {"value": b / dt, "unit": "codewords/s", "cores": cores, "kind": "port",
+                "sample": f"{b} frames, BG2 Z={z}, {iters} iterations, {what} on {cpu}, {dt:.1f} s"}
     if kind.startswith("gnn"):
         snr = 2.0 if snr is None else snr
         from ldpc_neural_decoder.models import create_message_gnn_decoder
@@ -300,6 +337,29 @@ def main():
             bound, unit, peak = "valu", "Ginst/s", VALU_PEAK_GINST
             fixed = os.environ.get("LDPC_FLOOD_FIXED", "1") != "0"
             dominant = f"flood_fixed_kernel<BG2_Z{z}, {kind}>" if fixed else f"flood_kernel<{kind}>"
+    elif kind == "hybrid-minsum":
+        from ldpc_neural_decoder.models import create_custom_minsum_message_gnn_decoder
+        from ldpc_neural_decoder.utils import count_errors
+        hdec, _ = create_custom_minsum_message_gnn_decoder(H, num_iterations=iters)
+        g = hdec._graph(n, dev)
+        probs = torch.empty((B, n), dtype=torch.float32, device=dev)
+        wsb = N.check(N.lib().ldpc_custom_minsum_workspace_size(g.handle, B))
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        stream = N.stream_ptr(dev)
+
+        def step(count):
+            N.check(N.lib().ldpc_custom_minsum_decode(g.handle, N.ptr(llr), B, iters, N.ptr(probs), N.ptr(ws), wsb,
+                                                      stream))
+            if count:
+                count_errors((probs > 0.5).to(torch.uint8), counters=counters)
+
+        dtype = "f32"
+        # per frame-iteration, messages in HBM: variable phase reads + writes every edge message and
+        # reads the LLRs; check phase reads + writes every edge message (fp32); + LLR transpose and
+        # the output pass once
+        per_launch_alg = (iters * (4 * g.E * 4 + g.N * 4) + 3 * g.N * 4 + g.E * 4) * B
+        bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+        dominant = "custom_var_kernel + stream_check_kernel<minsum> (all iterations)"
     elif kind == "lay":
         from ldpc_neural_decoder.models import CheckLayer, OutputLayer, ResidualLayer, VariableLayer
         from ldpc_neural_decoder.utils import create_LLR_mapping
@@ -344,7 +404,20 @@ def main():
         sweep_snrs = [float(x) for x in range(0, 7)]
         sweep_out = {}
 
-        if kind == "gnn-sweep":
+        if kind == "hybrid-gnn":
+            from ldpc_neural_decoder.models import create_custom_variable_message_gnn_decoder
+            from ldpc_neural_decoder.utils import count_errors
+            torch.manual_seed(7)
+            hdec, hconv = create_custom_variable_message_gnn_decoder(H, num_iterations=iters, hidden_dim=64,
+                                                                     base_graph=base, Z=z)
+            hdec = hdec.to(dev)
+            Avh, Ach = hconv.var_to_check_adjacency, hconv.check_to_var_adjacency
+
+            def step(count):
+                p, _ = hdec(llr, io, types, Avh, Ach)
+                if count:
+                    count_errors((p > 0.5).to(torch.uint8), counters=counters)
+        elif kind == "gnn-sweep":
             from ldpc_neural_decoder.sweep import evaluate_message_gnn
 
             def step(count):  # trial t of each SNR -> rank t: every rank decodes B frames per SNR
@@ -377,7 +450,11 @@ def main():
         # (gnn.hip, gnn_group_proj_kernel), so 8 H^2 per message + 2 H^2 per var / check group
         fwd_flops = 8 * 64 * 64 * E + 2 * 64 * 64 * (g_n + g_m)
         nominal_flops = 12 * 64 * 64 * E
-        if kind == "gnn-sweep":
+        if kind == "hybrid-gnn":
+            # check side only: 4 H^2 per message (W1 over c + W2) + 2 H^2 per check group (projection)
+            per_launch_alg = (4 * 64 * 64 * E + 2 * 64 * 64 * g_m) * B * iters
+            bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
+        elif kind == "gnn-sweep":
             per_launch_alg = fwd_flops * B * iters * len(sweep_snrs)  # MLP FLOPs per sweep
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         elif kind == "gnn-bf16":
@@ -393,7 +470,8 @@ def main():
         else:
             per_launch_alg = fwd_flops * B * iters  # MLP FLOPs per forward, as executed
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
-        dominant = {"gnn-train": "gnn training step", "gnn-sweep": "SNR sweep (7 x channel + gnn forward + count)"}.get(
+        dominant = {"gnn-train": "gnn training step", "gnn-sweep": "SNR sweep (7 x channel + gnn forward + count)",
+                    "hybrid-gnn": "hybrid gnn forward (all layers)"}.get(
             kind, "gnn forward (all layers)")
 
     for _ in range(a.warmup):
