@@ -529,6 +529,11 @@ def main():
                      "nominal_frac": nominal_flops / fwd_flops * achieved / peak}
         if bound == "valu":
             achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg)
+            if a.early_stop != "off" or a.iterations or a.snr is not None:
+                # the PMC pass ran the default workload (10 iterations, no stop): its instruction
+                # count does not describe this run
+                achieved = None
+                notes = {"valu": "not measured for this variant (the PMC pass is of the default workload)"}
         cpu = None
         if world == 1 and a.cpu_baseline_seconds > 0:
             cpu = cpu_baseline(a.workload, z, iters, a.cpu_baseline_seconds)
