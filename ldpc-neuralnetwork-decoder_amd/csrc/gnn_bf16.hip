@@ -581,11 +581,14 @@ int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpAr
 //   0 = 768 threads, 3 waves/SIMD, no register prefetch
 //   2 = 512 threads, 4 waves/SIMD, no prefetch (spills at 128 VGPRs)
 //   3 = 512 threads, 2 waves/SIMD, prefetch: one workgroup (one LDS weight copy) per CU
+//   4 = 768 threads, 3 waves/SIMD, prefetch; 5 = 1024 threads, 4 waves/SIMD, no prefetch
 int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (variant) {
         case 0: return launch_mlp_v<768, 3, false>(mode, tiles, lds, s, m);
         case 2: return launch_mlp_v<512, 4, false>(mode, tiles, lds, s, m);
         case 3: return launch_mlp_v<512, 2, true>(mode, tiles, lds, s, m);
+        case 4: return launch_mlp_v<768, 3, true>(mode, tiles, lds, s, m);
+        case 5: return launch_mlp_v<1024, 4, false>(mode, tiles, lds, s, m);
         default: return launch_mlp_v<256, 2, true>(mode, tiles, lds, s, m);
     }
 }
