@@ -834,6 +834,9 @@ struct FxPlan {
 #ifndef LDPC_SEL_ASM
 #define LDPC_SEL_ASM 1
 #endif
+#ifndef LDPC_ZFLAG
+#define LDPC_ZFLAG 0  // zero inputs join the sticky NaN flag: one slow/fast branch per check phase
+#endif
 #ifndef LDPC_ADDTID
 #define LDPC_ADDTID 1  // check-phase stores as ds_write_addtid_b32 (the slot entry of a row is slot[lane])
 #endif
@@ -863,7 +866,11 @@ struct FixedBody {
                 if constexpr (G::ROW_SLOT[P0 + E] < 0) {
                     constexpr int X = P::ext_index(I, E), COL = G::ROW_COL[P0 + E], S4 = 4 * G::ROW_SHIFT[P0 + E];
                     ext[X] = L.llr_at(COL * 4 * G::Z + ((L.k4 + S4) & ZM4));
+#if LDPC_ZFLAG
+                    nan |= is_zero_sign(ext[X]);  // zero or NaN
+#else
                     nan |= ext[X] != ext[X];
+#endif
                 }
             });
         });
@@ -875,7 +882,11 @@ struct FixedBody {
             constexpr int I = decltype(i)::value, COL = G::VAR_COLS[P::C0 + I];
             constexpr int P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
             cllr[I] = L.llr_at(COL * 4 * G::Z + L.k4);
+#if LDPC_ZFLAG
+            nan |= is_zero_sign(cllr[I]);
+#else
             nan |= cllr[I] != cllr[I];
+#endif
             sfor<DV>([&](auto jj) {
                 constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
                 constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
@@ -898,7 +909,7 @@ struct FixedBody {
         });
     }
 
-    template <int I, bool DEC>
+    template <int I, bool DEC, bool SLOW = false>
     __device__ __forceinline__ void row(const Ctx &C, const Lane &L, const float (&v)[MAXDC], bool nanflag,
                                         int &errs) const {
         constexpr int R = G::CHK_ROWS[P::R0 + I], P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
@@ -926,7 +937,15 @@ struct FixedBody {
             //   c2v_e = (par ^ sign(x_e)) * (alpha * (|x_e| == m1 ? m2 : m1))
             // bit for bit (a tie at m1 puts m1 in m2 too).  Otherwise MinSumStats (exact
             // torch.sign(0) = 0 and NaN semantics).
+#if LDPC_ZFLAG
+            // the workgroup's sticky flag (init / var) covers zero and NaN inputs: one branch per
+            // phase (check) instead of one per row, and the hot loop holds the fast code only
+            if (!SLOW) {
+#elif LDPC_EXP_NOSLOW  // timing experiment only: the fast path unconditionally (inexact for zeros / NaN)
+            if (true) {
+#else
             if (!nanflag && !__any(m1 == 0.0f)) {
+#endif
                 const uint32_t par = sign_parity_n<DC>(v) & 0x80000000u;
                 const uint32_t s1 = __float_as_uint(C.alpha * m1) ^ par, s2 = __float_as_uint(C.alpha * m2) ^ par;
 #if LDPC_SEL_ASM
@@ -976,6 +995,20 @@ struct FixedBody {
     __device__ __forceinline__ void check(const Ctx &C, const Lane &L, int &errs) const {
         bool nanflag = false;
         if constexpr (ALGO == LDPC_ALGO_MINSUM) nanflag = __builtin_amdgcn_readfirstlane(*C.flag) != 0;
+#if LDPC_ZFLAG
+        if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+            if (nanflag)
+                rows<DEC, true>(C, L, errs);
+            else
+                rows<DEC, false>(C, L, errs);
+            return;
+        }
+#endif
+        rows<DEC, false>(C, L, errs, nanflag);
+    }
+
+    template <bool DEC, bool SLOW>
+    __device__ __forceinline__ void rows(const Ctx &C, const Lane &L, int &errs, bool nanflag = false) const {
         float va[MAXDC], vb[MAXDC];
 #if LDPC_ADDTID
         addtid_begin(C.lds);
@@ -985,10 +1018,10 @@ struct FixedBody {
             constexpr int I = decltype(i)::value;
             if constexpr (I % 2 == 0) {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, vb);
-                row<I, DEC>(C, L, va, nanflag, errs);
+                row<I, DEC, SLOW>(C, L, va, nanflag, errs);
             } else {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, va);
-                row<I, DEC>(C, L, vb, nanflag, errs);
+                row<I, DEC, SLOW>(C, L, vb, nanflag, errs);
             }
         });
 #if LDPC_ADDTID
@@ -1014,7 +1047,7 @@ struct FixedBody {
     // running sums (two independent IEEE fp32 adds, the same sequence per element)
     template <int I, bool DEC, bool WRITE>
     __device__ __forceinline__ void col(const Ctx &C, const Lane &L, const float (&c)[MAXDV], int &errs,
-                                        bool &bad) const {
+                                        bool &bad, float &mz) const {
         constexpr int COL = G::VAR_COLS[P::C0 + I], P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
         float Pp = cllr[I];
         f32x2 acc[(DV + 1) / 2];
@@ -1036,6 +1069,17 @@ struct FixedBody {
                 constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
                 lds_wr(C.lds + SL * 256, rot[SI], J % 2 == 0 ? acc[J / 2].x : acc[J / 2].y);
             });
+#if LDPC_ZFLAG
+            if constexpr (ALGO == LDPC_ALGO_MINSUM) {  // smallest |v2c| written: a zero sets the flag
+                sfor<(DV + 1) / 2>([&](auto pp) {
+                    constexpr int Q = decltype(pp)::value;
+                    if constexpr (2 * Q + 1 < DV)
+                        mz = fminf(mz, fminf(fabsf(acc[Q].x), fabsf(acc[Q].y)));
+                    else
+                        mz = fminf(mz, fabsf(acc[Q].x));
+                });
+            }
+#endif
         }
         // a NaN v2c implies a NaN or infinite APP of its column (every summand of a v2c is a
         // summand of the APP; +-inf is absorbing), so this flag bounds the fast check path
@@ -1048,6 +1092,7 @@ struct FixedBody {
     template <bool DEC, bool WRITE>
     __device__ __forceinline__ void var(const Ctx &C, const Lane &L, int &errs) const {
         bool bad = false;
+        float mz = INFINITY;
         if constexpr (P::NC > 0) {
             float ca[MAXDV], cb[MAXDV];
             load_col<0>(C, ca);
@@ -1056,18 +1101,22 @@ struct FixedBody {
                 constexpr bool ahead = I + 1 < P::NC && dv_of(I) + dv_of(I + 1) <= kVarPipe;
                 if constexpr (I % 2 == 0) {
                     if constexpr (ahead) load_col<I + 1>(C, cb);
-                    col<I, DEC, WRITE>(C, L, ca, errs, bad);
+                    col<I, DEC, WRITE>(C, L, ca, errs, bad, mz);
                     if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, cb);
                 } else {
                     if constexpr (ahead) load_col<I + 1>(C, ca);
-                    col<I, DEC, WRITE>(C, L, cb, errs, bad);
+                    col<I, DEC, WRITE>(C, L, cb, errs, bad, mz);
                     if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, ca);
                 }
             });
         }
         if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+#if LDPC_ZFLAG
+            bad |= mz == 0.0f;
+#endif
             if (__any(bad) && L.lane == 0) *C.flag = 1;
         }
+        (void)mz;
     }
 
     __device__ __forceinline__ int parity(const Ctx &C, const Lane &L) const {
