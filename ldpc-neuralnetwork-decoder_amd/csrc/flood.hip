@@ -835,7 +835,7 @@ struct FxPlan {
 #define LDPC_SEL_ASM 1
 #endif
 #ifndef LDPC_ZFLAG
-#define LDPC_ZFLAG 0  // zero inputs join the sticky NaN flag: one slow/fast branch per check phase
+#define LDPC_ZFLAG 1  // zero inputs join the sticky NaN flag: one slow/fast branch per check phase (+5%)
 #endif
 #ifndef LDPC_ADDTID
 #define LDPC_ADDTID 1  // check-phase stores as ds_write_addtid_b32 (the slot entry of a row is slot[lane])

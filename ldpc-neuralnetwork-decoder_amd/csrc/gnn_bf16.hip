@@ -47,6 +47,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int H = 64;
+#ifndef LDPC_BF16_RELU_I16
+#define LDPC_BF16_RELU_I16 1
+#endif
 
 __host__ __device__ constexpr int pi_unit(int p) {
     return 32 * (p >> 5) + 16 * ((p >> 4) & 1) + 8 * ((p >> 2) & 1) + 4 * ((p >> 3) & 1) + (p & 3);
@@ -246,11 +249,24 @@ __device__ __forceinline__ f32x16 ld16(const float *p) {
     }
     return v;
 }
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+// ReLU of 8 accumulators as bf16: round first, then max(., 0) on the bf16 bit patterns as int16
+// (v_pk_max_i16, two values per instruction): a negative bf16 -- -0 included -- is a negative
+// int16, a positive one keeps its bits.  Same values as rounding max(x, 0.0f) (rounding keeps the
+// sign), without the per-value canonicalize + max pair fmaxf costs on an MFMA result.
 __device__ __forceinline__ bf16x8 relu8(const f32x16 &a, int half) {
     bf16x8 o;
 #pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (__bf16)a[8 * half + i];
+#if LDPC_BF16_RELU_I16
+    s16x8 b = __builtin_bit_cast(s16x8, o);
+    b = __builtin_elementwise_max(b, (s16x8)0);
+    return __builtin_bit_cast(bf16x8, b);
+#else
+#pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (__bf16)fmaxf(a[8 * half + i], 0.0f);
     return o;
+#endif
 }
 __device__ __forceinline__ bf16x8 pack8(const f32x16 &a, int half) {
     bf16x8 o;
