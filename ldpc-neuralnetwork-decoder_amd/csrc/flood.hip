@@ -139,9 +139,28 @@ __device__ __forceinline__ uint32_t sign_parity_n(const float (&v)[CAP]) {
 
 // m2 = median(m1, |x|, m2) then m1 = min(m1, |x|): the two smallest magnitudes of a row with no
 // NaN (v_min / v_med3 with |x| as a source modifier; fminf would add a NaN-quieting v_max)
-__device__ __forceinline__ void two_min_step(float &m1, float &m2, float x) {
+#ifndef LDPC_MIN_ASM
+#define LDPC_MIN_ASM 0
+#endif
+// -inf in a VGPR the compiler cannot see through: med3(m, |x|, -inf) = min(m, |x|) for non-NaN
+// operands, and an opaque third operand keeps the compiler from turning it back into a
+// canonicalising fminf
+// (an SGPR: one scalar operand per v_med3 is within the constant-bus limit)
+__device__ __forceinline__ float opaque_sf(float v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+__device__ __forceinline__ void two_min_step(float &m1, float &m2, float x, float ninf) {
+#if LDPC_MIN_ASM
+    (void)ninf;
     asm("v_med3_f32 %0, %1, |%2|, %3" : "=v"(m2) : "v"(m1), "v"(x), "v"(m2));
     asm("v_min_f32 %0, %1, |%2|" : "=v"(m1) : "v"(m1), "v"(x));
+#else
+    // builtins, not inline asm: a VALU reading a VGPR written by inline asm gets a conservative
+    // s_nop from the hazard recognizer (one per edge in the check phase)
+    m2 = __builtin_amdgcn_fmed3f(m1, fabsf(x), m2);
+    m1 = __builtin_amdgcn_fmed3f(m1, fabsf(x), ninf);
+#endif
 }
 
 // lane mask of |x| == m (v_cmp_eq_f32 into an SGPR pair) and a select by it; volatile so that the
@@ -911,7 +930,7 @@ struct FixedBody {
 
     template <int I, bool DEC, bool SLOW = false>
     __device__ __forceinline__ void row(const Ctx &C, const Lane &L, const float (&v)[MAXDC], bool nanflag,
-                                        int &errs) const {
+                                        int &errs, float ninf, float pinf) const {
         constexpr int R = G::CHK_ROWS[P::R0 + I], P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
         // an output is needed for a slot edge always, for a degree-1 edge only to take its decision
         auto needed = [](int e) constexpr { return DEC || G::ROW_SLOT[P0 + e] >= 0; };
@@ -930,8 +949,10 @@ struct FixedBody {
         };
         if constexpr (ALGO == LDPC_ALGO_MINSUM) {
             // the two smallest magnitudes (v_med3 / v_min with |x| source modifiers)
-            float m1 = fabsf(v[0]), m2 = INFINITY;
-            sfor<DC - 1>([&](auto e) { two_min_step(m1, m2, v[decltype(e)::value + 1]); });
+            // m2 starts as an opaque +inf: a constant one lets the compiler rewrite the first
+            // v_med3 as a canonicalising fmaxf
+            float m1 = fabsf(v[0]), m2 = pinf;
+            sfor<DC - 1>([&](auto e) { two_min_step(m1, m2, v[decltype(e)::value + 1], ninf); });
             // Fast path: no zero message in the row (then m1 > 0) and no possible NaN in the
             // workgroup (the sticky flag, see var()): torch.sign is +-1 on every message, so
             //   c2v_e = (par ^ sign(x_e)) * (alpha * (|x_e| == m1 ? m2 : m1))
@@ -1013,15 +1034,16 @@ struct FixedBody {
 #if LDPC_ADDTID
         addtid_begin(C.lds);
 #endif
+        const float ninf = opaque_sf(-INFINITY), pinf = opaque_sf(INFINITY);
         load_row<0>(C, L, va);
         sfor<P::NR>([&](auto i) {
             constexpr int I = decltype(i)::value;
             if constexpr (I % 2 == 0) {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, vb);
-                row<I, DEC, SLOW>(C, L, va, nanflag, errs);
+                row<I, DEC, SLOW>(C, L, va, nanflag, errs, ninf, pinf);
             } else {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, va);
-                row<I, DEC, SLOW>(C, L, vb, nanflag, errs);
+                row<I, DEC, SLOW>(C, L, vb, nanflag, errs, ninf, pinf);
             }
         });
 #if LDPC_ADDTID
@@ -1333,11 +1355,12 @@ __device__ __forceinline__ void stream_row(const StreamArgs &S, float *m, int e0
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
         // the LDS kernels' fast path (two minima by v_min / v_med3, sign parity by xor) when the
         // row has no zero and no NaN message; else MinSumStats (exact torch.sign semantics)
-        float m1 = fabsf(v[0]), m2 = INFINITY;
+        const float ninf = opaque_sf(-INFINITY);
+        float m1 = fabsf(v[0]), m2 = opaque_sf(INFINITY);
         bool special = is_zero_sign(v[0]);
 #pragma unroll
         for (int e = 1; e < DC; ++e) {
-            two_min_step(m1, m2, v[e]);
+            two_min_step(m1, m2, v[e], ninf);
             special |= is_zero_sign(v[e]);
         }
         if (!special) {
