@@ -150,6 +150,15 @@ __device__ __forceinline__ float opaque_sf(float v) {
     asm volatile("" : "+s"(v));
     return v;
 }
+// a uniform constant held in a VGPR: a VALU op with an SGPR source issues at half rate
+__device__ __forceinline__ uint32_t opaque_vu(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ float opaque_vf(float v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 __device__ __forceinline__ void two_min_step(float &m1, float &m2, float x, float ninf) {
 #if LDPC_MIN_ASM
     (void)ninf;
@@ -851,10 +860,19 @@ struct FxPlan {
 #define LDPC_VAR_PIPE 24
 #endif
 #ifndef LDPC_SEL_ASM
+// 1: the select by v_cmp / v_cndmask in asm (measured fastest); 0: the compare-free select (fewer
+// VALU pipe cycles but one more instruction per edge: 3.7 % slower, the kernel is bound by the
+// per-wave issue and dependency latency rather than by the VALU pipe)
 #define LDPC_SEL_ASM 1
 #endif
 #ifndef LDPC_ZFLAG
 #define LDPC_ZFLAG 1  // zero inputs join the sticky NaN flag: one slow/fast branch per check phase (+5%)
+#endif
+#ifndef LDPC_VAR_PK
+#define LDPC_VAR_PK 0  // 1: variable update on v_pk_add_f32 pairs (6 % slower than scalar adds)
+#endif
+#ifndef LDPC_MIN_SPLIT
+#define LDPC_MIN_SPLIT 0  // 1: the row's two minima as two half-row chains + a merge (shorter chain)
 #endif
 #ifndef LDPC_ADDTID
 #define LDPC_ADDTID 1  // check-phase stores as ds_write_addtid_b32 (the slot entry of a row is slot[lane])
@@ -930,7 +948,7 @@ struct FixedBody {
 
     template <int I, bool DEC, bool SLOW = false>
     __device__ __forceinline__ void row(const Ctx &C, const Lane &L, const float (&v)[MAXDC], bool nanflag,
-                                        int &errs, float ninf, float pinf) const {
+                                        int &errs, float ninf, float pinf, uint32_t sgn, float alv) const {
         constexpr int R = G::CHK_ROWS[P::R0 + I], P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
         // an output is needed for a slot edge always, for a degree-1 edge only to take its decision
         auto needed = [](int e) constexpr { return DEC || G::ROW_SLOT[P0 + e] >= 0; };
@@ -952,7 +970,26 @@ struct FixedBody {
             // m2 starts as an opaque +inf: a constant one lets the compiler rewrite the first
             // v_med3 as a canonicalising fmaxf
             float m1 = fabsf(v[0]), m2 = pinf;
+#if LDPC_MIN_SPLIT
+            if constexpr (DC >= 6) {
+                // two independent chains over the halves, then the second smallest of the union =
+                // med3(m1a, m1b, min(m2a, m2b)) (both minima are <= their chains' second minima)
+                constexpr int H1 = DC / 2;
+                float m1b = fabsf(v[H1]), m2b = pinf;
+                sfor<H1 - 1>([&](auto e) {
+                    two_min_step(m1, m2, v[decltype(e)::value + 1], ninf);
+                    two_min_step(m1b, m2b, v[H1 + decltype(e)::value + 1], ninf);
+                });
+                if constexpr (DC - H1 > H1) two_min_step(m1b, m2b, v[DC - 1], ninf);
+                const float t = __builtin_amdgcn_fmed3f(m2, m2b, ninf);  // min(m2, m2b)
+                m2 = __builtin_amdgcn_fmed3f(m1, m1b, t);
+                m1 = __builtin_amdgcn_fmed3f(m1, m1b, ninf);
+            } else {
+                sfor<DC - 1>([&](auto e) { two_min_step(m1, m2, v[decltype(e)::value + 1], ninf); });
+            }
+#else
             sfor<DC - 1>([&](auto e) { two_min_step(m1, m2, v[decltype(e)::value + 1], ninf); });
+#endif
             // Fast path: no zero message in the row (then m1 > 0) and no possible NaN in the
             // workgroup (the sticky flag, see var()): torch.sign is +-1 on every message, so
             //   c2v_e = (par ^ sign(x_e)) * (alpha * (|x_e| == m1 ? m2 : m1))
@@ -967,9 +1004,9 @@ struct FixedBody {
 #else
             if (!nanflag && !__any(m1 == 0.0f)) {
 #endif
+#if LDPC_SEL_ASM
                 const uint32_t par = sign_parity_n<DC>(v) & 0x80000000u;
                 const uint32_t s1 = __float_as_uint(C.alpha * m1) ^ par, s2 = __float_as_uint(C.alpha * m2) ^ par;
-#if LDPC_SEL_ASM
                 // |x_e| == m1 ? s2 : s1, with each compare issued three instructions ahead of its
                 // select (a VALU-written lane mask read by a VALU needs 2 wait states on gfx950;
                 // left to the compiler, every edge paid an s_nop 1)
@@ -985,11 +1022,23 @@ struct FixedBody {
                     if constexpr (needed(E)) emit(e, __uint_as_float((__float_as_uint(v[E]) & 0x80000000u) ^ sel[E]));
                 });
 #else
-                bool eq[DC];
-                sfor<DC>([&](auto e) { eq[decltype(e)::value] = fabsf(v[decltype(e)::value]) == m1; });
+                // The select without compares: t = m1 - |x_e| is +0 exactly when |x_e| == m1 and
+                // negative otherwise (x - y == 0 only for x == y; a flushed tiny difference is -0),
+                // so its arithmetic shift by 31 is the "use s1" mask.  v_sub / v_ashr / v_bitop3
+                // with VGPR operands issue at the full VALU rate, where v_cmp, v_cndmask and any
+                // op with an SGPR operand take two passes (measured: tools/ubench).  The sign
+                // mask and alpha are opaque VGPRs for the same reason.
+                const uint32_t par = sign_parity_n<DC>(v) & sgn;
+                const uint32_t s1 = __float_as_uint(alv * m1) ^ par, s2 = __float_as_uint(alv * m2) ^ par;
                 sfor<DC>([&](auto e) {
                     constexpr int E = decltype(e)::value;
-                    emit(e, __uint_as_float((__float_as_uint(v[E]) & 0x80000000u) ^ (eq[E] ? s2 : s1)));
+                    if constexpr (needed(E)) {
+                        // (opaque: the compiler would turn the mask back into v_cmp + v_cndmask)
+                        const uint32_t mk = opaque_vu((uint32_t)((int32_t)__float_as_uint(m1 - fabsf(v[E])) >> 31));
+                        const uint32_t sel = (s1 & mk) | (s2 & ~mk);
+                        // sel ^ (x & SIGN) as one v_bitop3 (the compiler splits it into and + xor)
+                        emit(e, __uint_as_float(__builtin_amdgcn_bitop3_b32(sel, __float_as_uint(v[E]), sgn, 0x78)));
+                    }
                 });
 #endif
             } else {
@@ -1035,15 +1084,17 @@ struct FixedBody {
         addtid_begin(C.lds);
 #endif
         const float ninf = opaque_sf(-INFINITY), pinf = opaque_sf(INFINITY);
+        const uint32_t sgn = opaque_vu(0x80000000u);
+        const float alv = opaque_vf(C.alpha);
         load_row<0>(C, L, va);
         sfor<P::NR>([&](auto i) {
             constexpr int I = decltype(i)::value;
             if constexpr (I % 2 == 0) {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, vb);
-                row<I, DEC, SLOW>(C, L, va, nanflag, errs, ninf, pinf);
+                row<I, DEC, SLOW>(C, L, va, nanflag, errs, ninf, pinf, sgn, alv);
             } else {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, va);
-                row<I, DEC, SLOW>(C, L, vb, nanflag, errs, ninf, pinf);
+                row<I, DEC, SLOW>(C, L, vb, nanflag, errs, ninf, pinf, sgn, alv);
             }
         });
 #if LDPC_ADDTID
@@ -1073,6 +1124,7 @@ struct FixedBody {
         constexpr int COL = G::VAR_COLS[P::C0 + I], P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
         float Pp = cllr[I];
         f32x2 acc[(DV + 1) / 2];
+#if LDPC_VAR_PK
         sfor<DV>([&](auto jj) {
             constexpr int J = decltype(jj)::value;
             const f32x2 cc = {c[J], c[J]};
@@ -1085,6 +1137,21 @@ struct FixedBody {
             }
             Pp = Pp + c[J];
         });
+#else
+        // scalar v_add_f32 (measured 6 % faster for the whole kernel than v_pk_add_f32 pairs: the
+        // running sums are dependency chains, and a packed add's chain latency is longer)
+        float a[DV];
+        sfor<DV>([&](auto jj) {
+            constexpr int J = decltype(jj)::value;
+            sfor<J>([&](auto p) { a[decltype(p)::value] = a[decltype(p)::value] + c[J]; });
+            a[J] = Pp;
+            Pp = Pp + c[J];
+        });
+        sfor<DV>([&](auto jj) {
+            constexpr int J = decltype(jj)::value;
+            if constexpr (J % 2 == 0) acc[J / 2].x = a[J]; else acc[J / 2].y = a[J];
+        });
+#endif
         if constexpr (WRITE) {
             sfor<DV>([&](auto jj) {
                 constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
