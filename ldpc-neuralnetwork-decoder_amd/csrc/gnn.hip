@@ -965,6 +965,17 @@ bool proj_path() {
     return t;
 }
 
+// LDPC_GNN_PROJ_WGS=n caps the projection kernel's workgroups per CU (speed only; 0 = as many as
+// the LDS allows, at most 3): fewer waves in flight keep fewer frames' feature rows competing for an
+// XCD's L2 between a row's check-side and var-side reads
+int proj_wgs_cap() {
+    static int t = [] {
+        const char *e = std::getenv("LDPC_GNN_PROJ_WGS");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    return t;
+}
+
 // LDPC_GNN_STREAMS=1 runs the fp32 forward as one frame range on the caller's stream (A/B runs);
 // default 2: two frame halves on two streams, so one half's HBM-bound group-mean launch runs in
 // the register/wave slots the other half's MFMA-bound MLP leaves free on every CU.
@@ -1300,6 +1311,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         if (mlp2_lds > 160 * 1024 || proj_lds > 160 * 1024)
             return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
         proj_per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
+        if (proj_wgs_cap()) proj_per_cu = std::min(proj_per_cu, proj_wgs_cap());
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
