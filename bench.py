@@ -78,7 +78,7 @@ def flood_bytes_per_cw(E, N, iters):
     return iters * 8 * (E + N) + 5 * N
 
 
-def valu_roofline(B, n, kern_ms, traffic, pmc, pmc_path, alg_bytes, minsum=False):
+def valu_roofline(B, n, kern_ms, traffic, pmc, pmc_path, alg_bytes):
     """The flood decoders keep every message in LDS: HBM sees the LLRs once and the decisions once,
     so SURVEY 8(d)'s streaming byte model is not their bound.  Their bound is VALU issue: the
     reference's exact float32 operation order (ascending, exclusive variable sums) is a fixed
@@ -101,15 +101,6 @@ def valu_roofline(B, n, kern_ms, traffic, pmc, pmc_path, alg_bytes, minsum=False
         "traffic_over_compulsory": (traffic / comp) if traffic else None,
     }
     notes.update((pmc or {}).get("derived", {}))
-    # issue-cost weighting (measured per-instruction costs, tools/ubench): half the hot loop's VALU
-    # ops (v_med3, v_cmp, v_cndmask, SGPR-operand ops) take 4 cycles per wave64 instruction, not 2
-    import glob
-    costs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_cost_minsum_z32.json")))
-    if costs and achieved and minsum:
-        w = json.load(open(costs[-1]))["weight"]
-        notes["valu_cost_source"] = os.path.relpath(costs[-1], ROOT)
-        notes["valu_issue_cost_weight"] = w
-        notes["valu_issue_weighted_frac"] = achieved / VALU_PEAK_GINST * w
     return achieved, notes
 
 
@@ -537,8 +528,7 @@ def main():
                      "nominal_12H2E_per_launch": nominal_flops * B * iters * (len(sweep_snrs) if kind == "gnn-sweep" else 1),
                      "nominal_frac": nominal_flops / fwd_flops * achieved / peak}
         if bound == "valu":
-            achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg,
-                                           minsum=kind == "minsum")
+            achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg)
             if a.early_stop != "off" or a.iterations or a.snr is not None:
                 # the PMC pass ran the default workload (10 iterations, no stop): its instruction
                 # count does not describe this run

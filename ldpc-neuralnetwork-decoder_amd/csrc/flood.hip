@@ -1005,8 +1005,11 @@ struct FixedBody {
             if (!nanflag && !__any(m1 == 0.0f)) {
 #endif
 #if LDPC_SEL_ASM
-                const uint32_t par = sign_parity_n<DC>(v) & 0x80000000u;
-                const uint32_t s1 = __float_as_uint(C.alpha * m1) ^ par, s2 = __float_as_uint(C.alpha * m2) ^ par;
+                // the sign mask and alpha as VGPR operands: an SGPR (or SGPR-held constant) source
+                // halves a VALU op's issue rate (tools/ubench), so the per-edge v_bitop3 below and
+                // the per-row products run at the full rate
+                const uint32_t par = sign_parity_n<DC>(v) & sgn;
+                const uint32_t s1 = __float_as_uint(alv * m1) ^ par, s2 = __float_as_uint(alv * m2) ^ par;
                 // |x_e| == m1 ? s2 : s1, with each compare issued three instructions ahead of its
                 // select (a VALU-written lane mask read by a VALU needs 2 wait states on gfx950;
                 // left to the compiler, every edge paid an s_nop 1)
@@ -1019,7 +1022,8 @@ struct FixedBody {
                 });
                 sfor<DC>([&](auto e) {
                     constexpr int E = decltype(e)::value;
-                    if constexpr (needed(E)) emit(e, __uint_as_float((__float_as_uint(v[E]) & 0x80000000u) ^ sel[E]));
+                    if constexpr (needed(E))
+                        emit(e, __uint_as_float(__builtin_amdgcn_bitop3_b32(sel[E], __float_as_uint(v[E]), sgn, 0x78)));
                 });
 #else
                 // The select without compares: t = m1 - |x_e| is +0 exactly when |x_e| == m1 and

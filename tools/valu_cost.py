@@ -2,7 +2,8 @@
 """Static VALU pipe-cycle count of a kernel's hot blocks, with the issue costs measured on MI355X
 by tools/ubench/valu_banks (profiles/r02_ubench_valu_banks.jsonl, one workgroup of 4 waves per SIMD):
     2 cycles per wave64 instruction: v_add_f32, v_xor_b32, v_bitop3_b32 with VGPR operands, ...
-    4 cycles: v_min/v_max/v_med3_f32, v_cmp_*, v_cndmask_b32, and any VALU op with an SGPR source
+    4 cycles: v_min/v_max/v_med3_f32, v_cmp_*, v_cndmask_b32, v_bfi_b32, v_exp/v_log/v_rcp, and any
+              VALU op with an SGPR source (literal and inline constants are full rate)
     ~2.5 cycles: v_pk_add_f32 (two adds)
 usage: valu_cost.py <kernel.s> [min-instructions-per-block | --hot]
 (kernel.s: hipcc -S --cuda-device-only of a file that includes csrc/flood.hip with
@@ -11,7 +12,8 @@ LDPC_FLOOD_KERNELS_ONLY and instantiates flood_fixed_kernel<BG2_Z32, MINSUM, ES_
 import re
 import sys
 
-HALF = ("v_min_", "v_max_", "v_med3_", "v_cmp_", "v_cndmask_", "v_readfirstlane", "v_readlane", "v_writelane")
+HALF = ("v_min_", "v_max_", "v_med3_", "v_cmp_", "v_cndmask_", "v_bfi_", "v_readfirstlane", "v_readlane", "v_writelane",
+        "v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_")  # transcendentals: 4 at 4 waves/SIMD (8 alone)
 
 
 def cost(ins):
