@@ -22,6 +22,7 @@
 // SLEEF float versions; neither is correctly rounded, so BP parity is "within float32
 // tolerance", not bitwise).
 // Compile with -ffp-contract=off: no a*b+c may fuse on this path.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -1471,20 +1472,13 @@ __device__ __forceinline__ void stream_row(const StreamArgs &S, float *m, int e0
     X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) \
     X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
 
-template <int ALGO>
-__global__ __launch_bounds__(256) void stream_check_kernel(StreamArgs S) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)S.M * S.B) return;
-    const int64_t i = t / S.B, b = t - i * S.B;
-    if (stream_skip(S, b)) return;
-    const int e0 = S.chk_ptr[i], dc = S.chk_ptr[i + 1] - e0;
-    float *m = S.msg + b;
-    switch (dc) {  // degrees above 32 are refused on the host
-#define X(n) case n: stream_row<ALGO, n>(S, m, e0); break;
-        LDPC_STREAM_DEG_CASES(X)
-#undef X
-        default: break;
-    }
+// one launch per check degree DC (graph.cpp groups the checks by degree): thread = (k-th check of
+// the degree, frame), the frame fastest, so a wave is 64 frames of one check (coalesced rows)
+template <int ALGO, int DC>
+__global__ __launch_bounds__(256) void stream_check_kernel(StreamArgs S, const int32_t *__restrict__ rows) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // grid: (frames, checks)
+    if (b >= S.B || stream_skip(S, b)) return;
+    stream_row<ALGO, DC>(S, S.msg + b, S.chk_ptr[rows[blockIdx.y]]);
 }
 
 // one (variable, frame): v2c_e = llr + sum_{e' != e} c_e' in ascending check order as the prefix
@@ -1492,11 +1486,11 @@ __global__ __launch_bounds__(256) void stream_check_kernel(StreamArgs S) {
 template <int DV>
 __device__ __forceinline__ float stream_col(const StreamArgs &S, float *m, const int32_t *edges, float l, bool write) {
     float c[DV];
-    int64_t off[DV];
+    int32_t ed[DV];  // edge ids (the 64-bit offsets are recomputed at the store: fewer live VGPRs)
 #pragma unroll
     for (int p = 0; p < DV; ++p) {
-        off[p] = (int64_t)edges[p] * S.B;
-        c[p] = m[off[p]];
+        ed[p] = edges[p];
+        c[p] = m[(int64_t)ed[p] * S.B];
     }
     f32x2 acc[(DV + 1) / 2];
     float P = l;
@@ -1515,26 +1509,22 @@ __device__ __forceinline__ float stream_col(const StreamArgs &S, float *m, const
     }
     if (write) {
 #pragma unroll
-        for (int p = 0; p < DV; ++p) m[off[p]] = p % 2 == 0 ? acc[p / 2].x : acc[p / 2].y;
+        for (int p = 0; p < DV; ++p) m[(int64_t)ed[p] * S.B] = p % 2 == 0 ? acc[p / 2].x : acc[p / 2].y;
     }
     return P;
 }
 
-__global__ __launch_bounds__(256) void stream_var_kernel(StreamArgs S, int write) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)S.N * S.B) return;
-    const int64_t j = t / S.B, b = t - j * S.B;
-    if (stream_skip(S, b)) return;
-    const int p0 = S.var_ptr[j], dv = S.var_ptr[j + 1] - p0;
-    const float l = S.llrT[t];
+// one launch per variable degree DV (0 included: APP = llr)
+template <int DV>
+__global__ __launch_bounds__(256) void stream_var_kernel(StreamArgs S, const int32_t *__restrict__ cols, int write) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // grid: (frames, variables)
+    if (b >= S.B || stream_skip(S, b)) return;
+    const int j = cols[blockIdx.y];
+    const int64_t jb = (int64_t)j * S.B + b;
+    const float l = S.llrT[jb];
     float app = l;
-    switch (dv) {  // degrees above 32 are refused on the host
-#define X(n) case n: app = stream_col<n>(S, S.msg + b, S.var_edge + p0, l, write != 0); break;
-        LDPC_STREAM_DEG_CASES(X)
-#undef X
-        default: break;
-    }
-    S.bitsT[t] = app < 0.0f;  // NaN < 0 is false -> 0
+    if constexpr (DV > 0) app = stream_col<DV>(S, S.msg + b, S.var_edge + S.var_ptr[j], l, write != 0);
+    S.bitsT[jb] = app < 0.0f;  // NaN < 0 is false -> 0
 }
 
 // per-frame syndrome after an iteration: LDPC_ES_FRAME freezes valid frames, LDPC_ES_BATCH
@@ -1639,11 +1629,11 @@ __global__ __launch_bounds__(256) void stream_emit_kernel(StreamArgs S, int max_
 template <int DV>
 __device__ __forceinline__ void custom_col(const StreamArgs &S, float *m, const int32_t *edges, float l, bool damp) {
     float c[DV];
-    int64_t off[DV];
+    int32_t ed[DV];  // edge ids (the 64-bit offsets are recomputed at the store: fewer live VGPRs)
 #pragma unroll
     for (int p = 0; p < DV; ++p) {
-        off[p] = (int64_t)edges[p] * S.B;
-        c[p] = m[off[p]];
+        ed[p] = edges[p];
+        c[p] = m[(int64_t)ed[p] * S.B];
     }
     float sum = c[0];
 #pragma unroll
@@ -1653,22 +1643,17 @@ __device__ __forceinline__ void custom_col(const StreamArgs &S, float *m, const 
     for (int p = 0; p < DV; ++p) {
         float v = total - c[p];
         if (damp) v = 0.5f * v + 0.5f * c[p];
-        m[off[p]] = v;
+        m[(int64_t)ed[p] * S.B] = v;
     }
 }
 
-__global__ __launch_bounds__(256) void custom_var_kernel(StreamArgs S, int damp) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)S.N * S.B) return;
-    const int64_t j = t / S.B, b = t - j * S.B;
-    const int p0 = S.var_ptr[j], dv = S.var_ptr[j + 1] - p0;
-    const float l = S.llrT[t];
-    switch (dv) {  // degrees above 32 are refused on the host; a variable without edges sends nothing
-#define X(n) case n: custom_col<n>(S, S.msg + b, S.var_edge + p0, l, damp != 0); break;
-        LDPC_STREAM_DEG_CASES(X)
-#undef X
-        default: break;
-    }
+// one launch per variable degree >= 1 (a variable without edges sends nothing)
+template <int DV>
+__global__ __launch_bounds__(256) void custom_var_kernel(StreamArgs S, const int32_t *__restrict__ cols, int damp) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // grid: (frames, variables)
+    if (b >= S.B) return;
+    const int j = cols[blockIdx.y];
+    custom_col<DV>(S, S.msg + b, S.var_edge + S.var_ptr[j], S.llrT[(int64_t)j * S.B + b], damp != 0);
 }
 
 // probsT[v][b] = sigmoid(llr_v + S_v), S_v in ascending message order
@@ -1763,6 +1748,52 @@ StreamWs stream_ws(const ldpc_graph *g, int64_t B, int max_iter, void *base) {
     return w;
 }
 
+// one launch per node degree (graph.cpp groups the checks / variables by degree), on a 2-D grid
+// (frames, nodes) so a thread finds its (node, frame) without a 64-bit division; grid.y is
+// chunked to 65535 nodes
+constexpr int kGridY = 65535;
+template <class F>
+void per_degree(const std::vector<int> &seg, const int32_t *order, int64_t B, F &&launch) {
+    const unsigned gx = (unsigned)((B + 255) / 256);
+    for (size_t q = 0; q + 2 < seg.size(); q += 3)
+        for (int k0 = 0; k0 < seg[q + 2]; k0 += kGridY)
+            launch(seg[q], dim3(gx, (unsigned)std::min(kGridY, seg[q + 2] - k0)), order + seg[q + 1] + k0);
+}
+
+template <int ALGO>
+void launch_stream_check(const ldpc_graph *g, const StreamArgs &S, int64_t B, hipStream_t s) {
+    per_degree(g->row_seg, g->row_order, B, [&](int d, dim3 grid, const int32_t *rows) {
+        switch (d) {  // degree 0: no messages; degrees above 32 are refused on the host
+#define X(k) case k: hipLaunchKernelGGL((stream_check_kernel<ALGO, k>), grid, dim3(256), 0, s, S, rows); break;
+            LDPC_STREAM_DEG_CASES(X)
+#undef X
+            default: break;
+        }
+    });
+}
+
+void launch_stream_var(const ldpc_graph *g, const StreamArgs &S, int64_t B, int write, hipStream_t s) {
+    per_degree(g->col_seg, g->col_order, B, [&](int d, dim3 grid, const int32_t *cols) {
+        switch (d) {
+#define X(k) case k: hipLaunchKernelGGL(stream_var_kernel<k>, grid, dim3(256), 0, s, S, cols, write); break;
+            X(0) LDPC_STREAM_DEG_CASES(X)
+#undef X
+            default: break;
+        }
+    });
+}
+
+void launch_custom_var(const ldpc_graph *g, const StreamArgs &S, int64_t B, int damp, hipStream_t s) {
+    per_degree(g->col_seg, g->col_order, B, [&](int d, dim3 grid, const int32_t *cols) {
+        switch (d) {  // a variable without edges sends nothing
+#define X(k) case k: hipLaunchKernelGGL(custom_var_kernel<k>, grid, dim3(256), 0, s, S, cols, damp); break;
+            LDPC_STREAM_DEG_CASES(X)
+#undef X
+            default: break;
+        }
+    });
+}
+
 template <int ALGO>
 int run_stream(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha, int es, int out_dtype,
                void *bits, int32_t *iters_out, uint64_t *counters, int32_t *batch_iters, void *work, hipStream_t s) {
@@ -1778,8 +1809,8 @@ int run_stream(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, f
     hipLaunchKernelGGL(stream_init_kernel, blocks(g->E * B), dim3(256), 0, s, S);
     LDPC_CHECK_LAUNCH("stream init");
     for (int it = 0; it < max_iter; ++it) {
-        hipLaunchKernelGGL(stream_check_kernel<ALGO>, blocks((int64_t)g->M * B), dim3(256), 0, s, S);
-        hipLaunchKernelGGL(stream_var_kernel, blocks((int64_t)g->N * B), dim3(256), 0, s, S, it < max_iter - 1 ? 1 : 0);
+        launch_stream_check<ALGO>(g, S, B, s);
+        launch_stream_var(g, S, B, it < max_iter - 1 ? 1 : 0, s);
         if (es != LDPC_ES_OFF) {
             hipLaunchKernelGGL(stream_syndrome_kernel, blocks(B), dim3(256), 0, s, S, it);
             if (es == LDPC_ES_BATCH) hipLaunchKernelGGL(stream_batch_step_kernel, dim3(1), dim3(1), 0, s, S, it);
@@ -1819,8 +1850,8 @@ int run_custom_minsum(const ldpc_graph *g, const float *llr, int64_t B, int iter
                        dim3(256), 0, s, llr, B, g->N, S.llrT);
     auto blocks = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
     for (int it = 0; it < iterations; ++it) {
-        hipLaunchKernelGGL(custom_var_kernel, blocks((int64_t)g->N * B), dim3(256), 0, s, S, it > 0 ? 1 : 0);
-        hipLaunchKernelGGL(stream_check_kernel<LDPC_ALGO_MINSUM>, blocks((int64_t)g->M * B), dim3(256), 0, s, S);
+        launch_custom_var(g, S, B, it > 0 ? 1 : 0, s);
+        launch_stream_check<LDPC_ALGO_MINSUM>(g, S, B, s);
         LDPC_CHECK_LAUNCH("custom min-sum iteration");
     }
     hipLaunchKernelGGL(custom_output_kernel, blocks((int64_t)g->N * B), dim3(256), 0, s, S, probsT);

@@ -79,8 +79,8 @@ void schedule(const std::vector<int> &tasks, const std::vector<double> &cost, in
 int build_csr(ldpc_graph *g) {
     const int M = g->M, N = g->N;
     const int64_t E = g->E;
-    std::vector<int32_t> blob((size_t)(M + 1) + E + (N + 1) + E, 0);
-    int32_t *cp = blob.data(), *ev = cp + M + 1, *vp = ev + E, *ve = vp + N + 1;
+    std::vector<int32_t> blob((size_t)(M + 1) + E + (N + 1) + E + M + N, 0);
+    int32_t *cp = blob.data(), *ev = cp + M + 1, *vp = ev + E, *ve = vp + N + 1, *ro = ve + E, *co = ro + M;
     for (int64_t e = 0; e < E; ++e) {
         ++cp[g->edge_chk[e] + 1];
         ev[e] = g->edge_var[e];
@@ -90,12 +90,29 @@ int build_csr(ldpc_graph *g) {
     for (int j = 0; j < N; ++j) vp[j + 1] += vp[j];
     std::vector<int32_t> fill(vp, vp + N);
     for (int64_t e = 0; e < E; ++e) ve[fill[g->edge_var[e]]++] = (int32_t)e;  // edges ascend = checks ascend
+    // nodes grouped by degree, ascending index inside a degree
+    auto group = [](const int32_t *ptr, int n, int32_t *order, std::vector<int> &seg) {
+        std::vector<int> idx(n);
+        for (int i = 0; i < n; ++i) idx[i] = i;
+        std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return ptr[a + 1] - ptr[a] < ptr[b + 1] - ptr[b]; });
+        seg.clear();
+        for (int k = 0; k < n; ++k) {
+            order[k] = idx[k];
+            const int d = ptr[idx[k] + 1] - ptr[idx[k]];
+            if (seg.empty() || seg[seg.size() - 3] != d) seg.insert(seg.end(), {d, k, 0});
+            ++seg.back();
+        }
+    };
+    group(cp, M, ro, g->row_seg);
+    group(vp, N, co, g->col_seg);
     LDPC_HIP(hipMalloc(&g->d_csr, blob.size() * sizeof(int32_t)));
     LDPC_HIP(hipMemcpy(g->d_csr, blob.data(), blob.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     g->chk_ptr = g->d_csr;
     g->ev = g->chk_ptr + M + 1;
     g->var_ptr = g->ev + E;
     g->var_edge = g->var_ptr + N + 1;
+    g->row_order = g->var_edge + E;
+    g->col_order = g->row_order + M;
     return LDPC_OK;
 }
 

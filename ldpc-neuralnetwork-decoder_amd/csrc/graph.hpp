@@ -63,4 +63,8 @@ struct ldpc_graph {
     // streaming decoder (flood.hip, any graph): check-major CSR + per-variable edge lists
     int32_t *d_csr = nullptr;  // chk_ptr[M+1] edge_var[E] var_ptr[N+1] var_edge[E]
     const int32_t *chk_ptr = nullptr, *ev = nullptr, *var_ptr = nullptr, *var_edge = nullptr;
+    // checks / variables grouped by degree (stable): the streaming kernels run one launch per
+    // degree, so each is compiled for its degree alone (registers, and occupancy, of that degree)
+    const int32_t *row_order = nullptr, *col_order = nullptr;
+    std::vector<int> row_seg, col_seg;  // {degree, offset into *_order, count} triples
 };
