@@ -1387,6 +1387,11 @@ struct StreamArgs {
     int32_t *invalid;  // [max_iter] LDPC_ES_BATCH: frames failing H x = 0 after each iteration
     float alpha;
     int es;
+    // flooding decoders only (null for the hybrid min-sum): per edge, its variable when that has
+    // degree 1.  Such an edge's v2c is the channel LLR forever, so the check phase leaves it in
+    // place and takes the variable's decision itself (APP = llr + c2v = v2c + c2v, the same
+    // float add); the degree-1 variables get no variable-phase launch.
+    const int32_t *ext_var;
 };
 
 __device__ __forceinline__ bool stream_skip(const StreamArgs &S, int64_t b) {
@@ -1465,7 +1470,13 @@ __device__ __forceinline__ void stream_row(const StreamArgs &S, float *m, int e0
         for (int e = 0; e < DC; ++e) out[e] = two_atanh(acc[e]);
     }
 #pragma unroll
-    for (int e = 0; e < DC; ++e) m[(int64_t)(e0 + e) * S.B] = out[e];
+    for (int e = 0; e < DC; ++e) {
+        const int xv = S.ext_var ? S.ext_var[e0 + e] : -1;  // wave-uniform (scalar load)
+        if (xv < 0)
+            m[(int64_t)(e0 + e) * S.B] = out[e];
+        else  // m - msg = the frame b: bitsT[xv][b]
+            S.bitsT[(int64_t)xv * S.B + (m - S.msg)] = v[e] + out[e] < 0.0f;
+    }
 }
 
 #define LDPC_STREAM_DEG_CASES(X)                                                                       \
@@ -1774,6 +1785,7 @@ void launch_stream_check(const ldpc_graph *g, const StreamArgs &S, int64_t B, hi
 
 void launch_stream_var(const ldpc_graph *g, const StreamArgs &S, int64_t B, int write, hipStream_t s) {
     per_degree(g->col_seg, g->col_order, B, [&](int d, dim3 grid, const int32_t *cols) {
+        if (d == 1 && S.ext_var) return;  // degree-1 variables: handled by the check phase
         switch (d) {
 #define X(k) case k: hipLaunchKernelGGL(stream_var_kernel<k>, grid, dim3(256), 0, s, S, cols, write); break;
             X(0) LDPC_STREAM_DEG_CASES(X)
@@ -1799,7 +1811,7 @@ int run_stream(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, f
                void *bits, int32_t *iters_out, uint64_t *counters, int32_t *batch_iters, void *work, hipStream_t s) {
     const StreamWs w = stream_ws(g, B, max_iter, work);
     StreamArgs S{g->chk_ptr, g->ev, g->var_ptr, g->var_edge, g->M, g->N, g->E, B, w.msg, w.llrT, w.bitsT, w.done,
-                 w.iters, w.ctl, w.invalid, alpha, es};
+                 w.iters, w.ctl, w.invalid, alpha, es, g->ext_var};
     LDPC_HIP(hipMemsetAsync(w.done, 0, (size_t)B, s));
     LDPC_HIP(hipMemsetAsync(w.ctl, 0, 64, s));
     LDPC_HIP(hipMemsetAsync(w.invalid, 0, (size_t)max_iter * 4, s));

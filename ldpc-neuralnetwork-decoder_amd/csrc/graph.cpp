@@ -79,8 +79,9 @@ void schedule(const std::vector<int> &tasks, const std::vector<double> &cost, in
 int build_csr(ldpc_graph *g) {
     const int M = g->M, N = g->N;
     const int64_t E = g->E;
-    std::vector<int32_t> blob((size_t)(M + 1) + E + (N + 1) + E + M + N, 0);
-    int32_t *cp = blob.data(), *ev = cp + M + 1, *vp = ev + E, *ve = vp + N + 1, *ro = ve + E, *co = ro + M;
+    std::vector<int32_t> blob((size_t)(M + 1) + E + (N + 1) + E + M + N + E, 0);
+    int32_t *cp = blob.data(), *ev = cp + M + 1, *vp = ev + E, *ve = vp + N + 1, *ro = ve + E, *co = ro + M,
+            *xv = co + N;
     for (int64_t e = 0; e < E; ++e) {
         ++cp[g->edge_chk[e] + 1];
         ev[e] = g->edge_var[e];
@@ -103,6 +104,10 @@ int build_csr(ldpc_graph *g) {
             ++seg.back();
         }
     };
+    for (int64_t e = 0; e < E; ++e) {
+        const int v = g->edge_var[e];
+        xv[e] = vp[v + 1] - vp[v] == 1 ? v : -1;
+    }
     group(cp, M, ro, g->row_seg);
     group(vp, N, co, g->col_seg);
     LDPC_HIP(hipMalloc(&g->d_csr, blob.size() * sizeof(int32_t)));
@@ -113,6 +118,7 @@ int build_csr(ldpc_graph *g) {
     g->var_edge = g->var_ptr + N + 1;
     g->row_order = g->var_edge + E;
     g->col_order = g->row_order + M;
+    g->ext_var = g->col_order + N;
     return LDPC_OK;
 }
 

@@ -66,5 +66,6 @@ struct ldpc_graph {
     // checks / variables grouped by degree (stable): the streaming kernels run one launch per
     // degree, so each is compiled for its degree alone (registers, and occupancy, of that degree)
     const int32_t *row_order = nullptr, *col_order = nullptr;
+    const int32_t *ext_var = nullptr;   // per edge: its variable if that has degree 1, else -1
     std::vector<int> row_seg, col_seg;  // {degree, offset into *_order, count} triples
 };
