@@ -1414,20 +1414,21 @@ __global__ __launch_bounds__(256) void stream_transpose_llr_kernel(const float *
         if (v0 + r < N && b0 + tx < B) llrT[(int64_t)(v0 + r) * B + b0 + tx] = t[tx][r];
 }
 
-__global__ __launch_bounds__(256) void stream_init_kernel(StreamArgs S) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= S.E * S.B) return;
-    const int64_t e = t / S.B, b = t - e * S.B;
-    S.msg[t] = S.llrT[(int64_t)S.ev[e] * S.B + b];  // v2c <- llr (traditional_decoders.py:199-202)
-}
 
 // one (check, frame): the row's DC messages in registers (DC is the row's degree, uniform over a
 // wave of 64 consecutive frames of one row)
-template <int ALGO, int DC>
+// FIRST: the first iteration of a flooding decode reads v2c = LLR straight from llrT (no init pass
+// over the E x B messages) and seeds the degree-1 edges' messages with it
+template <int ALGO, int DC, bool FIRST = false>
 __device__ __forceinline__ void stream_row(const StreamArgs &S, float *m, int e0) {
     float v[DC];
 #pragma unroll
-    for (int e = 0; e < DC; ++e) v[e] = m[(int64_t)(e0 + e) * S.B];
+    for (int e = 0; e < DC; ++e) {
+        if constexpr (FIRST)
+            v[e] = S.llrT[(int64_t)S.ev[e0 + e] * S.B + (m - S.msg)];
+        else
+            v[e] = m[(int64_t)(e0 + e) * S.B];
+    }
     float out[DC];
     if constexpr (ALGO == LDPC_ALGO_MINSUM) {
         // the LDS kernels' fast path (two minima by v_min / v_med3, sign parity by xor) when the
@@ -1472,10 +1473,12 @@ __device__ __forceinline__ void stream_row(const StreamArgs &S, float *m, int e0
 #pragma unroll
     for (int e = 0; e < DC; ++e) {
         const int xv = S.ext_var ? S.ext_var[e0 + e] : -1;  // wave-uniform (scalar load)
-        if (xv < 0)
+        if (xv < 0) {
             m[(int64_t)(e0 + e) * S.B] = out[e];
-        else  // m - msg = the frame b: bitsT[xv][b]
+        } else {  // m - msg = the frame b: bitsT[xv][b]
+            if constexpr (FIRST) m[(int64_t)(e0 + e) * S.B] = v[e];
             S.bitsT[(int64_t)xv * S.B + (m - S.msg)] = v[e] + out[e] < 0.0f;
+        }
     }
 }
 
@@ -1485,11 +1488,11 @@ __device__ __forceinline__ void stream_row(const StreamArgs &S, float *m, int e0
 
 // one launch per check degree DC (graph.cpp groups the checks by degree): thread = (k-th check of
 // the degree, frame), the frame fastest, so a wave is 64 frames of one check (coalesced rows)
-template <int ALGO, int DC>
+template <int ALGO, int DC, bool FIRST>
 __global__ __launch_bounds__(256) void stream_check_kernel(StreamArgs S, const int32_t *__restrict__ rows) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // grid: (frames, checks)
     if (b >= S.B || stream_skip(S, b)) return;
-    stream_row<ALGO, DC>(S, S.msg + b, S.chk_ptr[rows[blockIdx.y]]);
+    stream_row<ALGO, DC, FIRST>(S, S.msg + b, S.chk_ptr[rows[blockIdx.y]]);
 }
 
 // one (variable, frame): v2c_e = llr + sum_{e' != e} c_e' in ascending check order as the prefix
@@ -1771,11 +1774,11 @@ void per_degree(const std::vector<int> &seg, const int32_t *order, int64_t B, F 
             launch(seg[q], dim3(gx, (unsigned)std::min(kGridY, seg[q + 2] - k0)), order + seg[q + 1] + k0);
 }
 
-template <int ALGO>
+template <int ALGO, bool FIRST = false>
 void launch_stream_check(const ldpc_graph *g, const StreamArgs &S, int64_t B, hipStream_t s) {
     per_degree(g->row_seg, g->row_order, B, [&](int d, dim3 grid, const int32_t *rows) {
         switch (d) {  // degree 0: no messages; degrees above 32 are refused on the host
-#define X(k) case k: hipLaunchKernelGGL((stream_check_kernel<ALGO, k>), grid, dim3(256), 0, s, S, rows); break;
+#define X(k) case k: hipLaunchKernelGGL((stream_check_kernel<ALGO, k, FIRST>), grid, dim3(256), 0, s, S, rows); break;
             LDPC_STREAM_DEG_CASES(X)
 #undef X
             default: break;
@@ -1818,10 +1821,11 @@ int run_stream(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, f
     const dim3 tgrid((unsigned)((B + 63) / 64), (unsigned)((g->N + 63) / 64));
     hipLaunchKernelGGL(stream_transpose_llr_kernel, tgrid, dim3(256), 0, s, llr, B, g->N, w.llrT);
     auto blocks = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
-    hipLaunchKernelGGL(stream_init_kernel, blocks(g->E * B), dim3(256), 0, s, S);
-    LDPC_CHECK_LAUNCH("stream init");
     for (int it = 0; it < max_iter; ++it) {
-        launch_stream_check<ALGO>(g, S, B, s);
+        if (it == 0)  // v2c = LLR (traditional_decoders.py:199-202) read in place of an init pass
+            launch_stream_check<ALGO, true>(g, S, B, s);
+        else
+            launch_stream_check<ALGO>(g, S, B, s);
         launch_stream_var(g, S, B, it < max_iter - 1 ? 1 : 0, s);
         if (es != LDPC_ES_OFF) {
             hipLaunchKernelGGL(stream_syndrome_kernel, blocks(B), dim3(256), 0, s, S, it);
