@@ -322,3 +322,38 @@ def test_lifting_sizes_beyond_lds(cuda, oracle_mod, z, B, es):
     assert it == (8 if es == 0 else (ref_it if es == 1 else it))
     if es == 2:
         assert np.array_equal(fr.cpu().numpy(), ref_frame_it)
+
+
+def test_streaming_large_sparse_code_chunked_grid(cuda, oracle_mod):
+    """A non-QC (3, 6)-regular code with 70 000 checks and 140 000 variables: beyond any LDS
+    schedule, and more nodes of one degree than a launch's grid.y (65 535), so the streaming
+    kernels' per-degree launches are chunked.  Decisions bit-exact to the oracle, on the C ABI
+    with the graph built from the edge list (ldpc_graph_create)."""
+    M, Nv, dv, dc = 70000, 140000, 3, 6
+    rng = np.random.default_rng(11)
+    sockets = np.repeat(np.arange(Nv, dtype=np.int64), dv)
+    rng.shuffle(sockets)
+    chk = np.repeat(np.arange(M, dtype=np.int64), dc)
+    pairs = np.unique(chk * Nv + sockets)  # drop repeated (check, var) pairs; sorted check-major
+    ec, ev = (pairs // Nv).astype(np.int32), (pairs % Nv).astype(np.int32)
+    g = N.NativeGraph(ec, ev, M, Nv, cuda)
+    assert g.Z == 1 and g.E == len(ec)
+    B, iters = 6, 4
+    x = rng.normal(1.0, 2.0, size=(B, Nv)).astype(np.float32)
+    bits = torch.empty((B, Nv), dtype=torch.uint8, device=cuda)
+    wsb = N.check(N.lib().ldpc_flood_workspace_size(g.handle, B, iters, N.LDPC_ES_OFF))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=cuda)
+    xt = torch.from_numpy(x).to(cuda)
+    N.check(N.lib().ldpc_flood_decode(g.handle, N.LDPC_ALGO_MINSUM, N.ptr(xt), B, iters, 0.75, N.LDPC_ES_OFF,
+                                      N.LDPC_OUT_U8, N.ptr(bits), None, None, None, N.ptr(ws), ws.numel(), None))
+    torch.cuda.synchronize()
+    og = object.__new__(oracle_mod.Graph)  # the oracle's graph from the same edge list
+    og.M, og.N, og.E = M, Nv, len(ec)
+    og.edge_chk, og.edge_var = ec, ev
+    og.chk_ptr = np.zeros(M + 1, dtype=np.int32)
+    np.cumsum(np.bincount(ec, minlength=M), out=og.chk_ptr[1:])
+    og.var_edge = np.lexsort((ec, ev)).astype(np.int32)
+    og.var_ptr = np.zeros(Nv + 1, dtype=np.int32)
+    np.cumsum(np.bincount(ev, minlength=Nv), out=og.var_ptr[1:])
+    ref, _, _, _ = oracle_mod.flood_decode(og, x, "minsum", iters, 0.75, 0)
+    assert np.array_equal(bits.cpu().numpy(), ref)
