@@ -1662,12 +1662,23 @@ __device__ __forceinline__ void custom_col(const StreamArgs &S, float *m, const 
 }
 
 // one launch per variable degree >= 1 (a variable without edges sends nothing)
-template <int DV>
+// FIRST (iteration 0, every c2v = +0): v2c = (llr + (+0 + ... + +0)) - (+0) = llr + 0.0f exactly
+// (the + 0.0f turns a -0 LLR into +0 as the full sum does), so nothing is read and the messages
+// need no zero-fill
+template <int DV, bool FIRST>
 __global__ __launch_bounds__(256) void custom_var_kernel(StreamArgs S, const int32_t *__restrict__ cols, int damp) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // grid: (frames, variables)
     if (b >= S.B) return;
     const int j = cols[blockIdx.y];
-    custom_col<DV>(S, S.msg + b, S.var_edge + S.var_ptr[j], S.llrT[(int64_t)j * S.B + b], damp != 0);
+    const float l = S.llrT[(int64_t)j * S.B + b];
+    if constexpr (FIRST) {
+        const int32_t *edges = S.var_edge + S.var_ptr[j];
+        const float v = l + 0.0f;
+#pragma unroll
+        for (int p = 0; p < DV; ++p) S.msg[(int64_t)edges[p] * S.B + b] = v;
+    } else {
+        custom_col<DV>(S, S.msg + b, S.var_edge + S.var_ptr[j], l, damp != 0);
+    }
 }
 
 // probsT[v][b] = sigmoid(llr_v + S_v), S_v in ascending message order
@@ -1798,10 +1809,11 @@ void launch_stream_var(const ldpc_graph *g, const StreamArgs &S, int64_t B, int 
     });
 }
 
+template <bool FIRST>
 void launch_custom_var(const ldpc_graph *g, const StreamArgs &S, int64_t B, int damp, hipStream_t s) {
     per_degree(g->col_seg, g->col_order, B, [&](int d, dim3 grid, const int32_t *cols) {
         switch (d) {  // a variable without edges sends nothing
-#define X(k) case k: hipLaunchKernelGGL(custom_var_kernel<k>, grid, dim3(256), 0, s, S, cols, damp); break;
+#define X(k) case k: hipLaunchKernelGGL((custom_var_kernel<k, FIRST>), grid, dim3(256), 0, s, S, cols, damp); break;
             LDPC_STREAM_DEG_CASES(X)
 #undef X
             default: break;
@@ -1861,12 +1873,17 @@ int run_custom_minsum(const ldpc_graph *g, const float *llr, int64_t B, int iter
     float *probsT = reinterpret_cast<float *>(base + align256((size_t)g->E * B * 4) + align256((size_t)g->N * B * 4));
     S.alpha = 1.0f;
     S.es = LDPC_ES_OFF;
-    LDPC_HIP(hipMemsetAsync(S.msg, 0, (size_t)g->E * B * 4, s));  // c2v = 0 (MGD:1193)
+    // c2v = 0 at the start (MGD:1193): the first variable phase's FIRST form needs no zero-fill,
+    // zero iterations read the zeros directly
+    if (iterations == 0) LDPC_HIP(hipMemsetAsync(S.msg, 0, (size_t)g->E * B * 4, s));
     hipLaunchKernelGGL(stream_transpose_llr_kernel, dim3((unsigned)((B + 63) / 64), (unsigned)((g->N + 63) / 64)),
                        dim3(256), 0, s, llr, B, g->N, S.llrT);
     auto blocks = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
     for (int it = 0; it < iterations; ++it) {
-        launch_custom_var(g, S, B, it > 0 ? 1 : 0, s);
+        if (it == 0)
+            launch_custom_var<true>(g, S, B, 0, s);
+        else
+            launch_custom_var<false>(g, S, B, 1, s);
         launch_stream_check<LDPC_ALGO_MINSUM>(g, S, B, s);
         LDPC_CHECK_LAUNCH("custom min-sum iteration");
     }

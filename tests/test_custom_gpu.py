@@ -31,7 +31,7 @@ def run(dec, llr, cuda):
         return dec(llr.to(cuda)).cpu().numpy()
 
 
-@pytest.mark.parametrize("z,B,iters", [(4, 37, 5), (32, 64, 10), (12, 65, 6)])
+@pytest.mark.parametrize("z,B,iters", [(4, 37, 5), (32, 64, 10), (12, 65, 6), (4, 7, 1), (4, 7, 0)])
 def test_custom_minsum_vs_oracle(cuda, oracle_mod, z, B, iters):
     base_file = code_path(z if z in (4, 32) else 32)
     H = expand_base_matrix(load_base_matrix(base_file), z)
@@ -41,6 +41,7 @@ def test_custom_minsum_vs_oracle(cuda, oracle_mod, z, B, iters):
     rng = np.random.default_rng(z)
     llr = rng.normal(1.0, 2.0, (B, H.shape[1])).astype(np.float32)
     llr[0, :40] = 0.0
+    llr[1, :20] = -0.0  # the first variable phase turns -0 into +0 as (llr + 0) - 0 does
     got = run(dec, torch.from_numpy(llr), cuda)
     ref = oracle_mod.custom_minsum(oracle_mod.Graph(H.numpy().astype(np.uint8)), llr, iters)
     np.testing.assert_allclose(got, ref, atol=TOL, rtol=0)
