@@ -108,7 +108,14 @@ struct GnnLayer {
     int residual, last;
     int vside;       // 0: the check side alone (hybrid decoder, gnn_custom_var_forward)
     int d1;          // degree-1 var groups have no Mv row: the MLP uses the message's own c as g
+    // hybrid decoder (gnn_custom_var_forward): x_in holds the previous layer's F and the features
+    // are x = (v2c w_in + b_in) + F, formed where a row is read (custom_combine_kernel's exact
+    // float sequence) instead of being written back between the layers
+    const float *hv2c = nullptr;  // (B, E)
 };
+__device__ __forceinline__ float4 hyb_x(float4 f, float v, float4 w, float4 c) {
+    return make_float4((v * w.x + c.x) + f.x, (v * w.y + c.y) + f.y, (v * w.z + c.z) + f.z, (v * w.w + c.w) + f.w);
+}
 
 // feature u of message m of frame b *before* the type embedding
 __device__ __forceinline__ float x_feat(const GnnLayer &P, int64_t b, int64_t m, int u, int H) {
@@ -456,7 +463,7 @@ struct ProjTiles {
     int first;  // tiles before `first` are skipped (the var-side tiles, for the check side alone)
 };
 
-template <int NT>
+template <int NT, bool HYB = false>
 __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group_proj_kernel(GnnLayer P, ProjTiles T) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
@@ -523,6 +530,16 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
                     y[p] = *reinterpret_cast<const float4 *>(xb + (int64_t)mj[p] * 64);
                     tx[p] = P.msg_type[mi[p]];
                     tyy[p] = P.msg_type[mj[p]];
+                }
+                if (HYB && P.hv2c) {  // hybrid: x = (v2c w_in + b_in) + F
+                    const float *vb = P.hv2c + (int64_t)b * P.E;
+                    const float4 w = *reinterpret_cast<const float4 *>(lds + kPOffB + 128 + c4);
+                    const float4 c = *reinterpret_cast<const float4 *>(lds + kPOffB + 192 + c4);
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        x[p] = hyb_x(x[p], vb[mi[p]], w, c);
+                        y[p] = hyb_x(y[p], vb[mj[p]], w, c);
+                    }
                 }
                 if (i + 2 < md.y) {
 #pragma unroll
@@ -607,7 +624,7 @@ constexpr int kM2OffW1c = 64 * kPS, kM2OffW2v = 2 * 64 * kPS, kM2OffW2c = 3 * 64
 constexpr int kM2OffB = 4 * 64 * kPS, kM2OffEmb = kM2OffB + 3 * 64;
 inline size_t mlp2_lds_bytes(int T) { return (size_t)(kM2OffEmb + T * kPS) * 4; }
 
-template <int NT, int WPS>
+template <int NT, int WPS, bool HYB = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
@@ -642,9 +659,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
             const float *e = lds + kM2OffEmb + P.msg_type[m] * kPS + 4 * half;
             if (P.x_in) {
                 const float *xr = P.x_in + rr * 64 + 4 * half;
+                const float hv = HYB && P.hv2c ? P.hv2c[rr] : 0.0f;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const float4 v = *reinterpret_cast<const float4 *>(xr + 8 * q);
+                    float4 v = *reinterpret_cast<const float4 *>(xr + 8 * q);
+                    if (HYB && P.hv2c)  // hybrid: x = (v2c w_in + b_in) + F
+                        v = hyb_x(v, hv, *reinterpret_cast<const float4 *>(P.w_in + 8 * q + 4 * half),
+                                  *reinterpret_cast<const float4 *>(P.b_in + 8 * q + 4 * half));
                     in[4 * q + 0] = v.x + e[8 * q + 0];
                     in[4 * q + 1] = v.y + e[8 * q + 1];
                     in[4 * q + 2] = v.z + e[8 * q + 2];
@@ -1484,9 +1505,9 @@ extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, i
     }
     const size_t proj_lds = proj_lds_bytes(types, 4), mlp2_lds = mlp2_lds_bytes(types);
     if (proj_lds > 160 * 1024 || mlp2_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
-    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_group_proj_kernel<256>),
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_group_proj_kernel<256, true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
-    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps, true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
     const int mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
     const int proj_per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
@@ -1509,24 +1530,25 @@ extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, i
         L.w1c = L.b2v + H; L.b1c = L.w1c + 2LL * H * H; L.w2c = L.b1c + H; L.b2c = L.w2c + (int64_t)H * H;
         L.wo = L.b2c + H; L.bo = L.wo + H;
         L.x_in = x_in;
-        L.x_out = (l % 2 == 0) ? w.xa : w.xb;  // F, then x in place
+        L.hv2c = l > 0 ? v2c : nullptr;        // layers >= 1 read x = (v2c w_in + b_in) + F_{l-1}
+        L.x_out = (l % 2 == 0) ? w.xa : w.xb;  // F
         const int64_t ptiles = B * (int64_t)(T.n_tiles - T.first);
-        hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3((unsigned)std::min<int64_t>((ptiles + 3) / 4, (int64_t)g_num_cus * proj_per_cu)),
+        hipLaunchKernelGGL((gnn_group_proj_kernel<256, true>), dim3((unsigned)std::min<int64_t>((ptiles + 3) / 4, (int64_t)g_num_cus * proj_per_cu)),
                            dim3(256), proj_lds, s, L, T);
         LDPC_CHECK_LAUNCH("gnn_group_proj_kernel (check side)");
         constexpr int wpb = kMlp2Nt / 64;
         const int64_t tiles = (R + 31) / 32;
-        hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
+        hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps, true>),
                            dim3((unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu)),
                            dim3(kMlp2Nt), mlp2_lds, s, L);
         LDPC_CHECK_LAUNCH("gnn_mlp2_kernel (check side)");
         hipLaunchKernelGGL(custom_var_llr_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, w.msg_out, w.csr,
                            d_llr, p->E, N, B, v2c);
-        const bool last = l == layers - 1;
-        const float *wl = last ? L.wo : nullptr;  // the decoder's output head: the last layer's (:855)
-        hipLaunchKernelGGL(custom_combine_kernel, dim3((unsigned)((R * 16 + 255) / 256)), dim3(256), 0, s, L.x_out, v2c,
-                           d_weights, d_weights + H, R, wl, L.bo, w.msg_out);
         LDPC_CHECK_LAUNCH("hybrid GNN variable update");
+        if (l == layers - 1)  // x_L and the decoder's output head, the last layer's (:855)
+            hipLaunchKernelGGL(custom_combine_kernel, dim3((unsigned)((R * 16 + 255) / 256)), dim3(256), 0, s, L.x_out,
+                               v2c, d_weights, d_weights + H, R, L.wo, L.bo, w.msg_out);
+        LDPC_CHECK_LAUNCH("hybrid GNN output head");
         x_in = L.x_out;
     }
     hipLaunchKernelGGL(custom_output_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, w.msg_out, w.csr, d_llr,
