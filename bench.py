@@ -104,6 +104,15 @@ def valu_roofline(B, n, kern_ms, traffic, pmc, pmc_path, alg_bytes):
     return achieved, notes
 
 
+def sha256_file(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -518,8 +527,19 @@ def main():
             natural = lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))]
             tj = max(found, key=natural) if found else ""
         tjd = None
+        pmc_stale = None
         if os.path.exists(tj):
             tjd = json.load(open(tj))
+            # a PMC summary describes the library build it profiled (tools/gpu_profile.sh stamps the
+            # sha256 of the .so it loaded): from any other build its counts are not this run's
+            lib_sha = sha256_file(N.LIB_PATH)
+            if tjd.get("lib_sha256") != lib_sha:
+                pmc_stale = {"pmc_source": os.path.relpath(tj, ROOT), "pmc_lib_sha256": tjd.get("lib_sha256"),
+                             "loaded_lib_sha256": lib_sha,
+                             "note": "the PMC summary was measured on another libldpc_amd.so build: its "
+                                     "instruction / byte counts are not reported for this one"}
+                tjd = None
+        if tjd is not None:
             # the PMC pass ran the same workload at the default batch; scale per launch to this B
             traffic = tjd.get("bytes_per_launch")
             if traffic is not None and tjd.get("batch") and tjd["batch"] != B:
@@ -534,11 +554,15 @@ def main():
                      "executed_frac": fwd_flops / nominal_flops * achieved / peak}
         if bound == "valu":
             achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg)
+            if tjd is None:
+                achieved = None  # no same-build PMC count: the VALU fraction is not measured
             if a.early_stop != "off" or a.iterations or a.snr is not None:
                 # the PMC pass ran the default workload (10 iterations, no stop): its instruction
                 # count does not describe this run
                 achieved = None
                 notes = {"valu": "not measured for this variant (the PMC pass is of the default workload)"}
+        if pmc_stale is not None:
+            notes = dict(notes or {}, pmc_stale=pmc_stale)
         cpu = None
         if world == 1 and a.cpu_baseline_seconds > 0:
             cpu = cpu_baseline(a.workload, z, iters, a.cpu_baseline_seconds)

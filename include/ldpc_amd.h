@@ -257,6 +257,21 @@ int ldpc_output_layer_backward(const float *d_soft, const float *d_gt, const flo
                                const float *d_grad_loss, const int32_t *d_argmax, int64_t B, int n,
                                float *d_grad_z, void *stream);
 
+/* ---- hybrid layers' per-message updates on index rows (message_gnn_decoder.py:611-670, :976-1044)
+ * d_rows (R, W) int64 row-major: row m = [node, incoming message ids..., -1 padding]; ids index the
+ * E_in columns of d_x / d_c2v (validated by the caller).  Outputs (B, R) fp32.
+ * ldpc_index_rows_minsum  CustomCheckMessageGNNLayer.check_layer_update (:976-1044): the min-sum
+ *                         update of the row's other entries, leaving out its last valid entry
+ *                         (torch.sign / torch.min semantics; 0 without two valid entries).
+ * ldpc_index_rows_varsum  CustomVariableMessageGNNLayer.variable_layer_update (:611-670):
+ *                         (llr[b, node] + sum of the valid entries, ascending) - the last one;
+ *                         llr[b, node] without valid entries; damp != 0 (iteration > 0):
+ *                         0.5 * out + 0.5 * c2v[b, m] (needs R == E_in).  d_llr (B, N_var). */
+int ldpc_index_rows_minsum(const float *d_x, int64_t B, int64_t E_in, const int64_t *d_rows, int64_t R, int W,
+                           float *d_out, void *stream);
+int ldpc_index_rows_varsum(const float *d_llr, int64_t B, int64_t N_var, const float *d_c2v, int64_t E_in,
+                           const int64_t *d_rows, int64_t R, int W, int damp, float *d_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,6 +35,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include "common.hpp"
@@ -1011,21 +1012,27 @@ int gnn_streams() {
 }  // namespace
 }  // namespace ldpc
 
-// One non-blocking side stream and a fork/join event pair per device, created on first use and kept
-// for the process (the forward is issued from the caller's thread; the events only order launches).
+// One non-blocking side stream per device, created once (under a lock) and kept for the process, and a
+// fork/join event pair per device AND calling thread: two host threads decoding on one device record
+// their own events, so a join never orders against another thread's launches.  (Launches of two
+// threads on the shared side stream serialise, which is correct.)
 int ldpc::gnn_side_stream(hipStream_t *side, hipEvent_t *fork, hipEvent_t *join) {
     constexpr int kMaxDev = 64;
     static hipStream_t streams[kMaxDev];
-    static hipEvent_t forks[kMaxDev], joins[kMaxDev];
+    static std::mutex mu;
+    thread_local hipEvent_t forks[kMaxDev], joins[kMaxDev];
     int dev = 0;
     LDPC_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= kMaxDev) return fail(LDPC_EUNSUPPORTED, "device index out of range");
-    if (!streams[dev]) {
-        LDPC_HIP(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!streams[dev]) LDPC_HIP(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
+        *side = streams[dev];
+    }
+    if (!forks[dev]) {
         LDPC_HIP(hipEventCreateWithFlags(&forks[dev], hipEventDisableTiming));
         LDPC_HIP(hipEventCreateWithFlags(&joins[dev], hipEventDisableTiming));
     }
-    *side = streams[dev];
     *fork = forks[dev];
     *join = joins[dev];
     return LDPC_OK;

@@ -58,7 +58,8 @@ int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, 
                      const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
                      float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s);
 
-// The per-device side stream and fork/join events the forwards split their frames over.
+// The per-device side stream and the calling thread's fork/join events the forwards split their
+// frames over (thread-safe: see gnn.hip).
 int gnn_side_stream(hipStream_t *side, hipEvent_t *fork, hipEvent_t *join);
 
 // bf16 forward (precision 1, H = 64); same arguments as ldpc_gnn_forward.

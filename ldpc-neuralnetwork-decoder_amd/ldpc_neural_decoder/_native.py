@@ -66,6 +66,9 @@ SIGNATURES = {
     "ldpc_gnn_train_workspace_size": (_I64, [_P, ctypes.c_int, ctypes.c_int, _I64, ctypes.c_int]),
     "ldpc_gnn_forward_train": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                               ctypes.c_int, _I64, _P, _P, _P, _I64, _P]),
+    "ldpc_index_rows_minsum": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, ctypes.c_int, _P, _P]),
+    "ldpc_index_rows_varsum": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, ctypes.c_int, ctypes.c_int, _P,
+                                              _P]),
     "ldpc_gnn_backward": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                          ctypes.c_int, _I64, _P, _P, _P, _P, _P, _I64, _P]),
 }

@@ -47,9 +47,30 @@ class CustomVariableMessageGNNLayer(MessageGNNLayer):
         self.w_res = nn.Parameter(torch.ones(depth_L))
         self.previous_VL_storage = deque(maxlen=depth_L + 1)
 
-    def variable_layer_update(self, *args, **kwargs):
-        raise NotImplementedError("the hybrid variable update runs inside the decoders' forward (libldpc_amd "
-                                  "ldpc_custom_minsum_decode / ldpc_gnn_custom_var_forward); see the module docstring")
+    def variable_layer_update(self, input_mapping_LLR, check_to_variable_messages, variable_index_tensor, iteration):
+        """MGD:611-670 on its index rows: row m = [variable, incoming message ids..., -1].  Per frame
+        b: v2c[b, m] = (llr[b, variable] + sum of the incoming c2v, ascending) - the row's last
+        incoming c2v (the loop's last assignment); llr[b, variable] for a row without ids; from
+        iteration 1 on, 0.5 v2c + 0.5 c2v[b, m] (MGD:659-663).  input_mapping_LLR (B, N) indexed by
+        the row's variable; check_to_variable_messages (B, E).  HIP: ldpc_index_rows_varsum."""
+        llr = torch.as_tensor(input_mapping_LLR)
+        c2v = torch.as_tensor(check_to_variable_messages)
+        home = llr.device
+        dev = N.device_of(llr)
+        rows = _index_rows(variable_index_tensor, llr.shape[1] if llr.dim() == 2 else 0,
+                           c2v.shape[1] if c2v.dim() == 2 else 0, dev)
+        if llr.dim() != 2 or c2v.dim() != 2 or llr.shape[0] != c2v.shape[0]:
+            raise ValueError("input_mapping_LLR (B, N) and check_to_variable_messages (B, E) expected")
+        B, R = llr.shape[0], rows.shape[0]
+        damp = int(iteration) > 0
+        if damp and R != c2v.shape[1]:
+            raise RuntimeError(f"damping mixes {R} outputs with {c2v.shape[1]} input messages")
+        x = llr.to(dev, torch.float32).contiguous()
+        c = c2v.to(dev, torch.float32).contiguous()
+        out = torch.empty((B, R), dtype=torch.float32, device=dev)
+        N.check(N.lib().ldpc_index_rows_varsum(N.ptr(x), B, x.shape[1], N.ptr(c), c.shape[1], N.ptr(rows), R,
+                                               rows.shape[1], int(damp), N.ptr(out), N.stream_ptr(dev)))
+        return out.to(home) if home != dev else out
 
 
 class CustomCheckMessageGNNLayer(MessageGNNLayer):
@@ -59,9 +80,39 @@ class CustomCheckMessageGNNLayer(MessageGNNLayer):
         super().__init__(num_message_types, hidden_dim)
         self.alpha = nn.Parameter(torch.tensor(0.8))
 
-    def check_layer_update(self, *args, **kwargs):
-        raise NotImplementedError("the hybrid check update runs inside CustomMinSumMessageGNNDecoder.forward "
-                                  "(libldpc_amd ldpc_custom_minsum_decode); see the module docstring")
+    def check_layer_update(self, message_features, message_types, check_index_tensor):
+        """MGD:976-1044 on its index rows: row m = [check, incoming message ids..., -1].  Per frame
+        b: c2v[b, m] = prod sign(x) * min |x| over the row's valid ids except its last one (the
+        loop's last assignment excludes it), torch.sign (sign(0) = sign(NaN) = 0) and torch.min (NaN
+        wins) semantics, 0 with fewer than two valid ids.  message_features (B, E).  The learnable
+        alpha is not used, as in the reference.  HIP: ldpc_index_rows_minsum."""
+        x = torch.as_tensor(message_features)
+        if x.dim() != 2:
+            raise ValueError(f"message_features must be (batch, num_messages), got {tuple(x.shape)}")
+        home = x.device
+        dev = N.device_of(x)
+        rows = _index_rows(check_index_tensor, None, x.shape[1], dev)
+        xf = x.to(dev, torch.float32).contiguous()
+        B, R = xf.shape[0], rows.shape[0]
+        out = torch.empty((B, R), dtype=torch.float32, device=dev)
+        N.check(N.lib().ldpc_index_rows_minsum(N.ptr(xf), B, xf.shape[1], N.ptr(rows), R, rows.shape[1], N.ptr(out),
+                                               N.stream_ptr(dev)))
+        return out.to(home) if home != dev else out
+
+
+def _index_rows(index_tensor, n_nodes, n_msgs, device):
+    """An index tensor (R, W) as int64 on `device`, validated as the reference's indexing would
+    be: ids in [-1, n_msgs) (-1 = padding), the node column in [0, n_nodes) when it is used."""
+    t = torch.as_tensor(index_tensor)
+    if t.dim() != 2 or t.shape[1] < 1:
+        raise ValueError(f"index tensor must be (rows, 1 + max degree), got {tuple(t.shape)}")
+    t = t.long()
+    ids = t[:, 1:]
+    if ids.numel() and (int(ids.max()) >= n_msgs or int(ids.min()) < -1):
+        raise IndexError(f"message id out of range for {n_msgs} messages")
+    if n_nodes is not None and t.shape[0] and (int(t[:, 0].max()) >= n_nodes or int(t[:, 0].min()) < 0):
+        raise IndexError(f"node index out of range for {n_nodes} nodes")
+    return t.to(device).contiguous()
 
 
 def _graph_from_index_tensors(check_index_tensor, variable_index_tensor, num_checks, num_variables):
@@ -132,6 +183,9 @@ class CustomMinSumMessageGNNDecoder(MessageGNNDecoder):
             raise ValueError(f"input_llrs must be (batch, num_variables), got {tuple(input_llrs.shape)}")
         B, n = x.shape
         g = self._graph(n, dev)
+        if n != g.N:  # the graph's variable count comes from the index tensors (the reference indexes
+            # past the LLR row and raises IndexError): the kernels take no N of their own
+            raise ValueError(f"input_llrs has {n} variables, the index tensors describe {g.N}")
         probs = torch.empty((B, n), dtype=torch.float32, device=dev)
         if B:
             wsb = N.check(N.lib().ldpc_custom_minsum_workspace_size(g.handle, B))
@@ -253,8 +307,15 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
         if check_to_var_adjacency is None:
             cspec = (np.arange(E, dtype=np.int64), E)          # torch.eye (:825-826): every message alone
         else:
-            _, cspec = _aggregation_specs(var_to_check_adjacency if var_to_check_adjacency is not None
-                                          else check_to_var_adjacency, check_to_var_adjacency, E)
+            if var_to_check_adjacency is None:
+                # the reference takes eye(E) for A_v (MGD:822-823) and resizes nothing: a mis-sized
+                # A_c then fails in its bmm
+                if tuple(check_to_var_adjacency.shape) != (E, E):
+                    raise RuntimeError(f"check_to_var_adjacency must be ({E}, {E}) when var_to_check_adjacency "
+                                       f"is None, got {tuple(check_to_var_adjacency.shape)}")
+                _, cspec = _aggregation_specs(check_to_var_adjacency, check_to_var_adjacency, E)
+            else:
+                _, cspec = _aggregation_specs(var_to_check_adjacency, check_to_var_adjacency, E)
             if isinstance(cspec[0], str) and cspec[0] == "csr":
                 raise NotImplementedError("the hybrid GNN runs with clique (TannerToMessageGraph) or identity "
                                           "check adjacencies")

@@ -58,9 +58,18 @@ class _FloodDecoder:
         """llr (B, N) float32 -> (decoded_bits (B, N) float32 0/1, iterations: int).
 
         counters: optional int64[4] device tensor += [bit errors vs all-zero, frame errors,
-        frames, iteration sum] (the sweep's fused BER/FER counting).  With counters the call
-        never waits for the device: `iterations` is then returned as a device int32 scalar
-        (its value is also in the counters' iteration sum) instead of a Python int."""
+        frames, iteration sum] (the sweep's fused BER/FER counting).  `iterations` is a Python int
+        as in the reference (traditional_decoders.py:107-109): with early stopping that is one host
+        sync (the sweep uses decode_async, which never waits)."""
+        out = self.decode_async(llr, out_dtype, counters, return_frame_iters)
+        it = out[1]
+        if torch.is_tensor(it):
+            it = int(it.item())
+        return (out[0], it) + tuple(out[2:])
+
+    def decode_async(self, llr, out_dtype=torch.float32, counters=None, return_frame_iters=False):
+        """decode() without a host sync: with early stopping `iterations` is a device int32 scalar
+        (its value is also in the counters' iteration sum).  The sweep's entry point."""
         if self.max_iterations < 1:
             # the reference's loop never binds decoded_bits (traditional_decoders.py:109)
             raise UnboundLocalError("local variable 'decoded_bits' referenced before assignment")
@@ -84,8 +93,8 @@ class _FloodDecoder:
             wsb, N.stream_ptr(dev)))
         if es == N.LDPC_ES_OFF:
             iterations = self.max_iterations
-        else:  # the reference returns an int (traditional_decoders.py:107-109): one host sync
-            iterations = batch_iters[0] if counters is not None else int(batch_iters.item())
+        else:
+            iterations = batch_iters[0]
         if home != dev:
             bits = bits.to(home)
         if return_frame_iters:

@@ -108,7 +108,7 @@ class ComparativeEvaluator:
         n = self.H.shape[1]
 
         def decode(llr, counters):
-            dec.decode(llr, out_dtype=torch.uint8, counters=counters)
+            dec.decode_async(llr, out_dtype=torch.uint8, counters=counters)
 
         counts = run_sweep(decode, self._llr_fn(), snr_range, batch_size, num_trials, n, rank, world,
                            self._dev, ar)

@@ -109,7 +109,129 @@ def gen(name, base, z):
     s += arr("VAR_COLS", vl)
     s += arr("BW_PTR", bp)
     s += arr("BW_COLS", bl)
+    s += pair_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z)
     s += "};\n\n"
+    return s
+
+
+# ---- frame-pair kernel (flood.hip flood_pair_kernel): 8 waves, each lane carries two frames
+PW = 8
+
+
+def n_min_ops(d):
+    """half-rate min / med3 ops for the two smallest of d magnitudes (flood.hip two_smallest)"""
+    if d <= 1:
+        return 0
+    if d == 2:
+        return 2
+    return 2 + 5 * ((d - 3) // 3) + 2 * ((d - 3) % 3)
+
+
+def var_task_adds(d, lo, hi):
+    """v_pk_add_f32 of a column task writing outputs [lo, hi): the prefix P_1..P_{hi-1} (P_d, the
+    APP, when hi == d) and the tails sum_{e in [lo, hi)} (d - 1 - e)"""
+    pre = d if hi == d else hi - 1
+    return pre + sum(d - 1 - e for e in range(lo, hi))
+
+
+def var_task_cost(d, lo, hi):
+    # pipe cycles at 4 waves / SIMD (tools/ubench): v_pk_add_f32 2.6; + LDS reads / writes issued
+    return 2.6 * var_task_adds(d, lo, hi) + 1.0 * d + 1.5 * (hi - lo) + 6.0
+
+
+def split_column(d, parts):
+    """output ranges [lo, hi) of a degree-d column cut into `parts` tasks of about equal cost"""
+    bounds = [0]
+    for q in range(1, parts):
+        # the cut after which the first q parts hold q/parts of the cost (greedy on prefix cost)
+        total = var_task_cost(d, 0, d)
+        best = min(range(bounds[-1] + 1, d), key=lambda h: abs(
+            sum(var_task_cost(d, bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1))
+            + var_task_cost(d, bounds[-1], h) - q * total / parts))
+        bounds.append(best)
+    bounds.append(d)
+    return [(bounds[i], bounds[i + 1]) for i in range(parts)]
+
+
+def row_cost(dcr, nslot):
+    # per frame: the two minima (half rate, 4.1), sign parity (bitop3 per two messages), per slot
+    # edge compare + select + sign (4.1 + 4.1 + 2.2), row constants; x 2 frames
+    return 2 * (4.1 * n_min_ops(dcr) + 2.2 * (dcr // 2) + 10.4 * nslot + 12.0) + 2.0 * dcr
+
+
+def makespan(tasks, cost, w):
+    per = lpt(tasks, cost, w)
+    loads = [sum(cost[tasks.index(t)] for t in p) for p in per]
+    return max(loads), per
+
+
+def pair_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z):
+    mb = len(dc)
+    nb = len(dv)
+    # rows
+    rows = list(range(mb))
+    rc = [row_cost(dc[r], sum(1 for i in range(row_ptr[r], row_ptr[r + 1]) if slot[i] >= 0)) for r in rows]
+    chk = lpt(rows, rc, PW)
+    # variable tasks: split the heaviest columns while the LPT makespan improves
+    vcols = [c for c in range(nb) if dv[c] >= 2]
+    parts = {c: 1 for c in vcols}
+
+    def tasks_of(parts):
+        t = []
+        for c in vcols:
+            for lo, hi in split_column(dv[c], parts[c]):
+                t.append((c, lo, hi))
+        return t
+
+    def span(parts):
+        t = tasks_of(parts)
+        cost = [var_task_cost(dv[c], lo, hi) for c, lo, hi in t]
+        return makespan(t, cost, PW)
+
+    best, per = span(parts)
+    while True:
+        t = tasks_of(parts)
+        cost = [var_task_cost(dv[c], lo, hi) for c, lo, hi in t]
+        heavy = t[max(range(len(t)), key=lambda i: cost[i])][0]
+        trial = dict(parts)
+        trial[heavy] += 1
+        if trial[heavy] > dv[heavy]:
+            break
+        m, p2 = span(trial)
+        if m >= best - 1e-9:
+            break
+        best, per, parts = m, p2, trial
+    # slot numbering of the pair image: column-major, heaviest columns first, so the slots of the
+    # waves with the most messages sit below the 64 KB reach of a ds_read's 16-bit offset
+    order = sorted(vcols, key=lambda c: -dv[c])
+    nslots = sum(1 for x in slot if x >= 0)
+    pslot = [-1] * nslots
+    n = 0
+    for c in order:
+        for i in col_blocks[c]:
+            pslot[slot[i]] = n
+            n += 1
+    vt_ptr, vt_col, vt_lo, vt_hi = [0], [], [], []
+    for p in per:
+        for c, lo, hi in sorted(p):
+            vt_col.append(c)
+            vt_lo.append(lo)
+            vt_hi.append(hi)
+        vt_ptr.append(len(vt_col))
+    cp = [0]
+    cl = []
+    for p in chk:
+        cl += p
+        cp.append(len(cl))
+    s = f"    // frame-pair kernel: {PW} waves; variable tasks (column, outputs [lo, hi)); slot remap\n"
+    s += f"    static constexpr int PW = {PW};\n"
+    s += arr("P_CHK_PTR", cp)
+    s += arr("P_CHK_ROWS", cl)
+    s += arr("P_VT_PTR", vt_ptr)
+    s += arr("P_VT_COL", vt_col)
+    s += arr("P_VT_LO", vt_lo)
+    s += arr("P_VT_HI", vt_hi)
+    s += arr("P_SLOT", pslot)
     return s
 
 

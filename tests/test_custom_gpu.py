@@ -89,3 +89,118 @@ def test_c_abi_arguments(cuda):
     x = torch.zeros(4, H.shape[1], device=cuda)
     p = torch.empty_like(x)
     assert lib.ldpc_custom_minsum_decode(g.handle, N.ptr(x), 4, 2, N.ptr(p), None, 0, N.stream_ptr(cuda)) == N.LDPC_EINVAL
+
+
+def _fixture_rows(chk):
+    """Row m = [check of m, the check's other messages ascending, m]: the rows
+    tests/golden/make_custom_golden.py handed the reference's check_layer_update."""
+    E = len(chk)
+    ptr = np.concatenate([[0], np.cumsum(np.bincount(chk))])
+    width = int((ptr[1:] - ptr[:-1]).max()) + 1
+    rows = -np.ones((E, width), dtype=np.int64)
+    for m in range(E):
+        c = chk[m]
+        others = [f for f in range(ptr[c], ptr[c + 1]) if f != m]
+        rows[m, 0] = c
+        rows[m, 1:1 + len(others)] = others
+        rows[m, 1 + len(others)] = m
+    return rows
+
+
+def _literal_check_rows(x, rows):
+    """Restatement of check_layer_update's loop (MGD:998-1038) per row: the last assignment
+    excludes the last valid entry; torch.sign / prod / min semantics in numpy float32."""
+    B = x.shape[0]
+    out = np.zeros((B, rows.shape[0]), dtype=np.float32)
+    for m, row in enumerate(rows):
+        ids = [int(i) for i in row[1:] if i >= 0]
+        if len(ids) < 2:
+            continue
+        others = ids[:-1]
+        v = x[:, others]
+        sg = np.prod(np.where(v > 0, 1.0, np.where(v < 0, -1.0, 0.0)).astype(np.float32), axis=1).astype(np.float32)
+        a = np.abs(v)
+        mn = np.where(np.isnan(a).any(axis=1), np.float32(np.nan), np.nanmin(np.where(np.isnan(a), np.inf, a), axis=1))
+        out[:, m] = (sg * mn.astype(np.float32)).astype(np.float32)
+    return out
+
+
+def test_check_layer_update_pinned_by_reference(cuda):
+    """CustomCheckMessageGNNLayer.check_layer_update on the fixture's rows reproduces the
+    reference's own output bit for bit (zeros and their signs included)."""
+    from ldpc_neural_decoder.models.custom_decoders import CustomCheckMessageGNNLayer
+    d = golden("custom_check_z4.npz")
+    llr, chk, var, ref = d["llr"], d["msg_chk"], d["msg_var"], d["c2v"]
+    rows = torch.from_numpy(_fixture_rows(chk))
+    v2c = torch.from_numpy(llr[:, var]).contiguous()
+    layer = CustomCheckMessageGNNLayer(1, 8)
+    got = layer.check_layer_update(v2c.to(cuda), torch.zeros(len(chk), dtype=torch.long), rows)
+    assert got.device == torch.device(cuda) and got.shape == ref.shape
+    g = got.cpu().numpy()
+    assert np.array_equal(g.view(np.uint32), ref.view(np.uint32))
+    # CPU tensors in, CPU tensor out (the computation still runs on the GPU)
+    assert np.array_equal(layer.check_layer_update(v2c, None, rows).numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_check_layer_update_general_rows(cuda):
+    """Rows with padding between ids, a repeated id, one or no valid id, NaN / zero inputs, against
+    the loop's restatement."""
+    from ldpc_neural_decoder.models.custom_decoders import CustomCheckMessageGNNLayer
+    rng = np.random.default_rng(5)
+    B, E = 9, 40
+    x = rng.normal(0, 2, (B, E)).astype(np.float32)
+    x[0, 3] = 0.0
+    x[1, 7] = -0.0
+    x[2, 11] = np.nan
+    rows = -np.ones((E, 7), dtype=np.int64)
+    for m in range(E):
+        k = rng.integers(0, 6)
+        ids = rng.choice(E, size=k, replace=True)
+        pos = np.sort(rng.choice(np.arange(1, 7), size=k, replace=False))
+        rows[m, 0] = rng.integers(0, 10)
+        rows[m, pos] = ids
+    rows[0, 1:] = [3, 7, 11, -1, 5, -1]
+    got = CustomCheckMessageGNNLayer(1, 8).check_layer_update(torch.from_numpy(x).to(cuda), None,
+                                                              torch.from_numpy(rows)).cpu().numpy()
+    ref = _literal_check_rows(x, rows)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.array_equal(got[ok].view(np.uint32), ref[ok].view(np.uint32))
+    with pytest.raises(IndexError):
+        bad = rows.copy()
+        bad[0, 1] = E
+        CustomCheckMessageGNNLayer(1, 8).check_layer_update(torch.from_numpy(x).to(cuda), None, torch.from_numpy(bad))
+
+
+@pytest.mark.parametrize("iteration", [0, 1])
+def test_variable_layer_update(cuda, iteration):
+    """CustomVariableMessageGNNLayer.variable_layer_update by its definition (MGD:611-670, per
+    frame): (llr + ascending sum of the incoming c2v) - the last one; the LLR alone without ids;
+    damping 0.5 / 0.5 with the message's own c2v from iteration 1 on."""
+    from ldpc_neural_decoder.models.custom_decoders import CustomVariableMessageGNNLayer
+    rng = np.random.default_rng(6 + iteration)
+    B, Nv, E = 5, 12, 30
+    llr = rng.normal(0, 2, (B, Nv)).astype(np.float32)
+    c2v = rng.normal(0, 2, (B, E)).astype(np.float32)
+    rows = -np.ones((E, 6), dtype=np.int64)
+    for m in range(E):
+        k = rng.integers(0, 6)
+        rows[m, 0] = rng.integers(0, Nv)
+        rows[m, 1:1 + k] = rng.choice(E, size=k, replace=False)
+    got = CustomVariableMessageGNNLayer(1, 64).variable_layer_update(
+        torch.from_numpy(llr).to(cuda), torch.from_numpy(c2v).to(cuda), torch.from_numpy(rows), iteration)
+    f32 = np.float32
+    ref = np.zeros((B, E), dtype=np.float32)
+    for b in range(B):
+        for m in range(E):
+            ids = [int(i) for i in rows[m, 1:] if i >= 0]
+            v = llr[b, rows[m, 0]]
+            if ids:
+                s = c2v[b, ids[0]]
+                for i in ids[1:]:
+                    s = f32(s + c2v[b, i])
+                v = f32(f32(v + s) - c2v[b, ids[-1]])
+            if iteration > 0:
+                v = f32(f32(f32(0.5) * v) + f32(f32(0.5) * c2v[b, m]))
+            ref[b, m] = v
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32))

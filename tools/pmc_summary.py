@@ -40,6 +40,11 @@ def main(d, kern, out, expected_read=None, per_call=None):
         res = {k: sum(v) / len(v) for k, v in agg.items()}
     waves = res.get("SQ_WAVES")
     out_d = {"kernel_substring": kern, "counters_per_launch": res}
+    # the library build these counters describe (tools/gpu_profile.sh writes the sha256 of the .so
+    # the profiled runs loaded); bench.py reports PMC-derived figures only for that same build
+    stamp = os.path.join(d, "lib_sha256.txt")
+    if os.path.exists(stamp):
+        out_d["lib_sha256"] = open(stamp).read().split()[0]
     if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
         read_b = 2 * res["FETCH_SIZE"] * 1024
         write_b = res["WRITE_SIZE"] * 1024
