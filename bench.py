@@ -129,6 +129,9 @@ def parse():
                          "batch-global rule, traditional_decoders.py:104-107), frame (per-frame freeze)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
                     help="target CPU work for the oracle baseline sample (0 disables)")
+    ap.add_argument("--checkpoint", default=None,
+                    help="MessageGNN weights (a trainer checkpoint dict, loaded weights_only); default: "
+                         "checkpoints/gnn_bg2_z<Z>_i<layers>_h64.pt when present, else random weights")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (profiles/*_pmc.json) to report as roofline.traffic")
     return ap.parse_args()
@@ -319,6 +322,7 @@ def main():
     llr = awgn_llr(B, n, snr, seed=20251015, frame_offset=rank * B, device=dev)
     counters = torch.zeros(4, dtype=torch.int64, device=dev)
 
+    weights = None
     if kind in ("minsum", "bp"):
         from ldpc_neural_decoder.models import BeliefPropagationDecoder, MinSumScaledDecoder
         dec = (MinSumScaledDecoder(H, iters, 0.75, early_stopping=False) if kind == "minsum"
@@ -399,6 +403,15 @@ def main():
         torch.manual_seed(7)
         gdec, conv = create_message_gnn_decoder(H, num_iterations=iters, hidden_dim=64,
                                                 base_graph=base, Z=z)
+        ckpt = a.checkpoint or os.path.join(ROOT, "checkpoints", f"gnn_bg2_z{z}_i{iters}_h64.pt")
+        if kind != "hybrid-gnn" and os.path.exists(ckpt):
+            # a checkpoint written by the trainer (tools/train_gnn_checkpoint.py): tensors and plain data only
+            ck = torch.load(ckpt, map_location="cpu", weights_only=True)
+            gdec.load_state_dict(ck["model_state_dict"])
+            weights = {"weights": "trained", "checkpoint": os.path.relpath(ckpt, ROOT),
+                       "train_config": ck.get("train_config")}
+        else:
+            weights = {"weights": "random (torch.manual_seed(7))", "checkpoint": None}
         gdec = gdec.to(dev)
         if kind == "gnn-bf16":
             gdec.precision = "bf16"
@@ -563,6 +576,11 @@ def main():
                 notes = {"valu": "not measured for this variant (the PMC pass is of the default workload)"}
         if pmc_stale is not None:
             notes = dict(notes or {}, pmc_stale=pmc_stale)
+        # BER / FER of a neural decoder with random weights say nothing about decoding: not reported
+        no_rates = kind == "lay" or (weights is not None and weights["checkpoint"] is None)
+        if no_rates and weights is not None:
+            notes = dict(notes or {}, ber_fer="not reported: random weights (no trained checkpoint for this "
+                                              "configuration; tools/train_gnn_checkpoint.py makes one)")
         cpu = None
         if world == 1 and a.cpu_baseline_seconds > 0:
             cpu = cpu_baseline(a.workload, z, iters, a.cpu_baseline_seconds)
@@ -588,9 +606,9 @@ def main():
                        "early_stop": a.early_stop if kind in ("minsum", "bp") else None,
                        "global_batch": B * world, "snr_db": "0..6" if sweep else snr,
                        "parallelism": f"dp{world}"},
-            "ber": None if kind == "lay" else (sweep_out["ber_fer"][0] if kind == "gnn-sweep"
-                                               else be / max(fr * n, 1)),
-            "fer": None if kind == "lay" else (sweep_out["ber_fer"][1] if kind == "gnn-sweep" else fe / max(fr, 1)),
+            "ber": None if no_rates else (sweep_out["ber_fer"][0] if kind == "gnn-sweep" else be / max(fr * n, 1)),
+            "fer": None if no_rates else (sweep_out["ber_fer"][1] if kind == "gnn-sweep" else fe / max(fr, 1)),
+            "model": weights,
             "roofline": {"bound": bound, "kernel": dominant, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": None if achieved is None else achieved / peak, "traffic": traffic,
                          "kernel_ms": kern_ms,

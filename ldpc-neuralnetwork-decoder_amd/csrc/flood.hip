@@ -212,12 +212,12 @@ int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter,
     return LDPC_OK;
 }
 
-// frame-pair kernel (flood_pair.inc): the reference's codes without early stopping.
-// LDPC_FLOOD_PAIR=0 keeps flood_fixed_kernel (A/B, tests)
+// frame-pair kernel (flood_pair.inc): the reference's codes without early stopping, opt-in with
+// LDPC_FLOOD_PAIR=1 (measured slower than flood_fixed_kernel on cfg3: DESIGN.md section 3.1)
 bool use_pair(const ldpc_graph *g) {
     if (g->fixed_id == 0) return false;
     const char *e = std::getenv("LDPC_FLOOD_PAIR");
-    return !(e && std::atoi(e) == 0);
+    return e && std::atoi(e) != 0;
 }
 int pair_frames(const ldpc_graph *g) { return 2 * g->FG; }
 

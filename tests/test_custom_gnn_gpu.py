@@ -55,3 +55,29 @@ def test_hybrid_gnn_loss_decode_and_one_hot_mapping(cuda, oracle_mod):
     assert torch.equal(dec.decode(llr, conv.message_to_var_index().to(cuda), types.to(cuda), Av, Ac), (p1 > 0.5).float())
     sub, _ = dec(llr[2:5], conv.message_to_var_index().to(cuda), types.to(cuda), Av, Ac)
     assert torch.equal(sub, p1[2:5])
+
+
+def test_hybrid_gnn_bench_size_chunks(cuda, oracle_mod):
+    """The hybrid-gnn-z32 bench shape: B = 32 768 frames, 10 layers, which the forward splits into
+    launches of at most ((1 << 31) // 16 - 1) // E = 21 291 frames (the kernels' per-launch message
+    bound).  Sub-batches -- one straddling the chunk boundary -- decode bit-identically to the same
+    frames inside the full batch, and four spot frames across both chunks match the oracle."""
+    H, dec, conv, types = setup(32, 10, 77)
+    from ldpc_neural_decoder.utils import awgn_llr
+    B = 32768
+    E = len(conv.messages)
+    limit = ((1 << 31) // 16 - 1) // E
+    assert limit < B  # two launches
+    llr = awgn_llr(B, H.shape[1], 2.0, seed=20251015, device=cuda)
+    io, ty = conv.message_to_var_index().to(cuda), types.to(cuda)
+    Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
+    with torch.no_grad():
+        full, _ = dec(llr, io, ty, Av, Ac)
+        for s, e in ((0, 7), (limit - 3, limit + 4), (B - 5, B)):
+            part, _ = dec(llr[s:e].contiguous(), io, ty, Av, Ac)
+            assert torch.equal(part, full[s:e]), (s, e)
+    spots = [0, limit - 1, limit, B - 1]
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    ref = oracle_mod.custom_variable_forward(sd, llr[spots].cpu(), conv.edge_var, conv.edge_chk, H.shape[1],
+                                             H.shape[0], types=types)
+    np.testing.assert_allclose(full[spots].cpu().numpy(), ref.numpy(), atol=TOL, rtol=0)

@@ -204,3 +204,21 @@ def test_variable_layer_update(cuda, iteration):
                 v = f32(f32(f32(0.5) * v) + f32(f32(0.5) * c2v[b, m]))
             ref[b, m] = v
     assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_hybrid_minsum_bench_size(cuda, oracle_mod):
+    """The hybrid-minsum-z32 bench shape: B = 65 536 frames, BG2 Z = 32, 10 iterations.  Sub-batches
+    decode identically to the same frames of the full batch and four spot frames match the C
+    oracle."""
+    from ldpc_neural_decoder.utils import awgn_llr
+    H = expand_base_matrix(load_base_matrix(code_path(32)), 32)
+    dec, _ = decoder_for(H, 10)
+    B = 65536
+    llr = awgn_llr(B, H.shape[1], 2.0, seed=20251015, device=cuda)
+    with torch.no_grad():
+        full = dec(llr)
+        for s, e in ((0, 3), (40000, 40037), (B - 2, B)):
+            assert torch.equal(dec(llr[s:e].contiguous()), full[s:e]), (s, e)
+    spots = [0, 1, 40001, B - 1]
+    ref = oracle_mod.custom_minsum(oracle_mod.Graph(H.numpy().astype(np.uint8)), llr[spots].cpu().numpy(), 10)
+    np.testing.assert_allclose(full[spots].cpu().numpy(), ref, atol=TOL, rtol=0)

@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""Train a MessageGNNDecoder checkpoint on the GPU with this build's HIP trainer path.
+
+    python tools/train_gnn_checkpoint.py --layers 15 --minutes 8 --out checkpoints/gnn_bg2_z32_i15_h64.pt
+
+The model is the reference's (create_message_gnn_decoder, message_gnn_decoder.py:539-582: BG2 Z=32,
+hidden_dim 64, message types = the base graph's 32 shifts).  Each step is the reference trainer's
+step (trainer.py:90-102: zero_grad, forward with ground truth -> BCE (MGD:314), loss.backward(),
+optimizer step) on the HIP forward/backward (csrc/gnn_train.hip), with two deliberate differences:
+  * the frames are random CODEWORDS (utils/encoding.py), not random bits (trainer.py:85): a
+    decoder trained on non-codewords can only learn a per-bit detector, never a decoder, so its
+    decisions would never satisfy the parity checks and early termination (cfg5) could not fire;
+  * Adam (lr 1e-3, global gradient-norm clip 1.0) instead of SGD + momentum (trainer.py:70), to
+    make progress within a bounded number of GPU minutes.
+LLRs: the on-device QPSK / AWGN channel (awgn_llr with the codeword bits, CH:4-154 semantics) at an
+SNR drawn per step from --snr-lo..--snr-hi dB.  The file holds the reference trainer's checkpoint
+dict (trainer.py:337-350 keys) plus num_iterations / hidden_dim (run_comparison_all.py:124-143) and
+the training configuration; every value is a tensor or plain Python data, so it loads with
+torch.load(..., weights_only=True).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ldpc-neuralnetwork-decoder_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=15)
+    ap.add_argument("--z", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--minutes", type=float, default=8.0)
+    ap.add_argument("--max-steps", type=int, default=1 << 30)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--snr-lo", type=float, default=0.0)
+    ap.add_argument("--snr-hi", type=float, default=4.0)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--init", default=None, help="continue from this checkpoint")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+
+    from ldpc_neural_decoder.models import create_message_gnn_decoder
+    from ldpc_neural_decoder.utils import awgn_llr, expand_base_matrix, load_base_matrix
+    from ldpc_neural_decoder.utils.encoding import SystematicEncoder
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(a.seed)
+    base = load_base_matrix(os.path.join(ROOT, "codes", f"NR_2_0_{a.z}.txt"))
+    H = expand_base_matrix(base, a.z)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=a.layers, hidden_dim=64, base_graph=base, Z=a.z)
+    if a.init:
+        ck = torch.load(a.init, map_location="cpu", weights_only=True)
+        dec.load_state_dict(ck["model_state_dict"])
+    dec = dec.to(dev)
+    types = conv.get_message_types(base, a.z).to(dev)
+    io = conv.message_to_var_index().to(dev)
+    Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
+    enc = SystematicEncoder(H, dev)
+    n = H.shape[1]
+    opt = torch.optim.Adam(dec.parameters(), lr=a.lr)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(a.seed)
+    rng = torch.Generator()
+    rng.manual_seed(a.seed)
+
+    losses, bers, log = [], [], []
+    t0 = time.time()
+    step = 0
+    run_loss = run_err = run_bits = 0.0
+    while step < a.max_steps and time.time() - t0 < a.minutes * 60:
+        snr = a.snr_lo + (a.snr_hi - a.snr_lo) * float(torch.rand(1, generator=rng))
+        bits = enc.random(a.batch, generator=gen)
+        llr = awgn_llr(a.batch, n, snr, seed=a.seed * 1000003 + step, device=dev, bits=bits)
+        opt.zero_grad(set_to_none=True)
+        p, loss = dec(llr, io, types, Av, Ac, ground_truth=bits)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(dec.parameters(), 1.0)
+        opt.step()
+        step += 1
+        with torch.no_grad():
+            run_loss += float(loss)
+            run_err += float(((p > 0.5).float() != bits).sum())
+            run_bits += bits.numel()
+        if step % 100 == 0:
+            losses.append(run_loss / 100)
+            bers.append(run_err / run_bits)
+            line = {"step": step, "t": round(time.time() - t0, 1), "loss": round(losses[-1], 5), "ber": bers[-1]}
+            log.append(line)
+            print(json.dumps(line), flush=True)
+            run_loss = run_err = run_bits = 0.0
+            if not math.isfinite(losses[-1]):
+                raise SystemExit("loss diverged")
+
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    out = {
+        "model_state_dict": sd,
+        "num_iterations": a.layers,
+        "hidden_dim": 64,
+        "train_losses": losses,
+        "val_losses": [],
+        "ber_history": bers,
+        "fer_history": [],
+        "train_config": {"code": f"5G NR BG2 Z={a.z}", "layers": a.layers, "batch": a.batch, "steps": step,
+                         "minutes": round((time.time() - t0) / 60, 2), "optimizer": "Adam", "lr": a.lr,
+                         "grad_clip": 1.0, "snr_db": [a.snr_lo, a.snr_hi], "data": "random codewords",
+                         "seed": a.seed, "init": a.init},
+    }
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    torch.save(out, a.out)
+    print(json.dumps({"saved": a.out, "steps": step, "minutes": out["train_config"]["minutes"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
