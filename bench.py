@@ -129,6 +129,10 @@ def parse():
                          "batch-global rule, traditional_decoders.py:104-107), frame (per-frame freeze)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
                     help="target CPU work for the oracle baseline sample (0 disables)")
+    ap.add_argument("--data", choices=("zero", "codewords"), default="zero",
+                    help="transmitted frames: the all-zero codeword (every reference harness, e.g. "
+                         "comparative_evaluation.py:133) or random codewords (utils/encoding.py), whose BER / "
+                         "FER show a neural decoder's decoding on typical frames")
     ap.add_argument("--checkpoint", default=None,
                     help="MessageGNN weights (a trainer checkpoint dict, loaded weights_only); default: "
                          "checkpoints/gnn_bg2_z<Z>_i<layers>_h64.pt when present, else random weights")
@@ -319,7 +323,13 @@ def main():
     base = load_base_matrix(os.path.join(ROOT, "codes", f"NR_2_0_{z if z in (4, 32) else 32}.txt"))
     H = expand_base_matrix(base, z)
     n = H.shape[1]
-    llr = awgn_llr(B, n, snr, seed=20251015, frame_offset=rank * B, device=dev)
+    ref_bits = None
+    if a.data == "codewords":
+        from ldpc_neural_decoder.utils.encoding import SystematicEncoder
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(20251015 + rank)
+        ref_bits = SystematicEncoder(H, dev).random(B, generator=gen).to(torch.uint8)
+    llr = awgn_llr(B, n, snr, seed=20251015, frame_offset=rank * B, bits=ref_bits, device=dev)
     counters = torch.zeros(4, dtype=torch.int64, device=dev)
 
     weights = None
@@ -336,9 +346,14 @@ def main():
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
 
         def step(count):
+            fused = count and ref_bits is None  # the fused counters count against the all-zero codeword
             N.check(N.lib().ldpc_flood_decode(
                 g.handle, algo, N.ptr(llr), B, iters, 0.75, es, N.LDPC_OUT_U8,
-                N.ptr(bits), None, None, N.ptr(counters) if count else None, N.ptr(ws), wsb, stream))
+                N.ptr(bits), None, None, N.ptr(counters) if fused else None, N.ptr(ws), wsb, stream))
+            if count and ref_bits is not None:
+                from ldpc_neural_decoder.utils import count_errors
+                count_errors(bits, ref=ref_bits, counters=counters)
+                counters[3] += iters * B
 
         dtype = "f32"
         per_launch_alg = flood_bytes_per_cw(g.E, g.N, iters) * B
@@ -364,7 +379,7 @@ def main():
             N.check(N.lib().ldpc_custom_minsum_decode(g.handle, N.ptr(llr), B, iters, N.ptr(probs), N.ptr(ws), wsb,
                                                       stream))
             if count:
-                count_errors((probs > 0.5).to(torch.uint8), counters=counters)
+                count_errors((probs > 0.5).to(torch.uint8), ref=ref_bits, counters=counters)
 
         dtype = "f32"
         # per frame-iteration, messages in HBM: variable phase reads + writes every edge message and
@@ -438,7 +453,7 @@ def main():
             def step(count):
                 p, _ = hdec(llr, io, types, Avh, Ach)
                 if count:
-                    count_errors((p > 0.5).to(torch.uint8), counters=counters)
+                    count_errors((p > 0.5).to(torch.uint8), ref=ref_bits, counters=counters)
         elif kind == "gnn-sweep":
             from ldpc_neural_decoder.sweep import evaluate_message_gnn
 
@@ -447,7 +462,7 @@ def main():
                                                             message_types=types)
         elif kind == "gnn-train":
             opt = torch.optim.SGD(gdec.parameters(), lr=1e-3, momentum=0.9, weight_decay=1e-4)
-            gt = torch.zeros((B, n), dtype=torch.float32, device=dev)
+            gt = torch.zeros((B, n), dtype=torch.float32, device=dev) if ref_bits is None else ref_bits.float()
             Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
 
             def step(count):  # trainer.py:90-102: zero_grad, forward + BCE, backward, SGD step
@@ -457,13 +472,13 @@ def main():
                 opt.step()
                 if count:
                     from ldpc_neural_decoder.utils import count_errors
-                    count_errors((p.detach() > 0.5).to(torch.uint8), counters=counters)
+                    count_errors((p.detach() > 0.5).to(torch.uint8), ref=ref_bits, counters=counters)
         else:
             def step(count):
                 p = gdec.native_forward(llr, io, types, vg, cg)
                 if count:
                     from ldpc_neural_decoder.utils import count_errors
-                    count_errors((p > 0.5).to(torch.uint8), counters=counters)
+                    count_errors((p > 0.5).to(torch.uint8), ref=ref_bits, counters=counters)
 
         dtype = "bf16" if kind == "gnn-bf16" else "f32"
         E = len(conv.messages)
@@ -598,7 +613,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": f"synthetic: all-zero codeword through the on-device QPSK/AWGN channel at "
+            "data": f"synthetic: {'random codewords (utils/encoding.py)' if ref_bits is not None else 'all-zero codeword'}"
+                    f" through the on-device QPSK/AWGN channel at "
                     f"{'0..6 (step 1)' if sweep else snr} dB "
                     f"(Philox seed 20251015, frame offset rank*B), resident in HBM",
             "config": {"workload": a.workload, "code": f"5G NR BG2 Z={z} (N={n})",

@@ -228,6 +228,14 @@ int launch_pair(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, 
     return launch_pair_kernel(ALGO, g->fixed_id, nwg, s, llr, B, max_iter, alpha, out_dtype, bits, O);
 }
 
+// 6-wave kernel (flood_w6.inc): the reference's codes without early stopping, opt-in with
+// LDPC_FLOOD_W6=1 (A/B)
+bool use_w6(const ldpc_graph *g) {
+    if (g->fixed_id == 0) return false;
+    const char *e = std::getenv("LDPC_FLOOD_W6");
+    return e && std::atoi(e) != 0;
+}
+
 int reduce_rows(const ldpc_graph *g, int64_t B, const uint32_t *partials, uint64_t *counters, int32_t *batch_iters,
                 const int32_t *gate, hipStream_t s, int frames_per_wg = 0) {
     if (!counters && !batch_iters) return LDPC_OK;
@@ -245,6 +253,12 @@ int run_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, fl
     if (es == LDPC_ES_OFF && use_pair(g)) {
         int rc = launch_pair<ALGO>(g, llr, B, max_iter, alpha, out_dtype, bits, O, s);
         return rc != LDPC_OK ? rc : reduce_rows(g, B, ws.partials, counters, nullptr, nullptr, s, pair_frames(g));
+    }
+    if (es == LDPC_ES_OFF && use_w6(g)) {
+        const int64_t nwg = (B + g->FG - 1) / g->FG;
+        int rc = launch_w6_kernel(ALGO, g->fixed_id, nwg, flood_lds_bytes(g, LDPC_ES_OFF), s, g->ft, llr, B, max_iter,
+                                  alpha, out_dtype, bits, O);
+        return rc != LDPC_OK ? rc : reduce_rows(g, B, ws.partials, counters, nullptr, nullptr, s);
     }
     if (es == LDPC_ES_OFF) {
         int rc = launch_flood<ALGO, LDPC_ES_OFF>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);

@@ -38,6 +38,44 @@ def lpt(tasks, cost, w):
     return [sorted(p) for p in per]
 
 
+def balance(tasks, cost, w):
+    """LPT, then moves / swaps of single tasks between the heaviest wave and the others while the
+    heaviest wave's load drops (the phase ends at a barrier: its time is the largest load)."""
+    per = lpt(tasks, cost, w)
+    c = dict(zip(tasks, cost))
+    load = lambda p: sum(c[t] for t in p)
+    improved = True
+    while improved:
+        improved = False
+        per.sort(key=load, reverse=True)
+        top = per[0]
+        best = (load(top), None)
+        for q in range(1, w):
+            o = per[q]
+            for t in top:  # move t from top to o
+                m = max(load(top) - c[t], load(o) + c[t])
+                if m < best[0] - 1e-9:
+                    best = (m, ("move", t, q))
+                for u in o:  # swap t and u
+                    m = max(load(top) - c[t] + c[u], load(o) - c[u] + c[t])
+                    if m < best[0] - 1e-9:
+                        best = (m, ("swap", t, q, u))
+        if best[1] is not None:
+            kind = best[1][0]
+            if kind == "move":
+                _, t, q = best[1]
+                top.remove(t)
+                per[q].append(t)
+            else:
+                _, t, q, u = best[1]
+                top.remove(t)
+                per[q].remove(u)
+                top.append(u)
+                per[q].append(t)
+            improved = True
+    return [sorted(p) for p in per]
+
+
 def arr(name, vals):
     vals = list(vals) or [0]
     body = ", ".join(str(v) for v in vals)
@@ -64,11 +102,16 @@ def gen(name, base, z):
     for r in range(mb):
         row_ptr.append(row_ptr[-1] + dc[r])
     rows = list(range(mb))
-    rcost = [6.0 * dc[r] + 0.5 * dc[r] * dc[r] + 8 for r in rows]
+    nslot = [sum(1 for i in range(row_ptr[r], row_ptr[r + 1]) if slot[i] >= 0) for r in rows]
+    # per-iteration SIMD pipe cycles of one wave's share (tools/ubench costs at 4 waves / SIMD):
+    # check row: the two minima (half-rate min / med3), sign parity, per slot edge compare +
+    # select + sign, row constants; column: the exclusive ordered sums (full-rate adds) + its LDS
+    # reads / writes issued
+    rcost = [4.1 * n_min_ops(dc[r]) + 2.2 * (dc[r] // 2) + 10.4 * nslot[r] + 12 + 2.0 * dc[r] for r in rows]
     vcols = [c for c in range(nb) if dv[c] != 1]
-    vcost = [0.5 * dv[c] * (dv[c] + 1) + 4.0 * dv[c] + 6 for c in vcols]
-    chk = lpt(rows, rcost, W)
-    var = lpt(vcols, vcost, W)
+    vcost = [1.94 * (dv[c] * (dv[c] - 1) // 2 + dv[c]) + 2.0 * dv[c] + 6 for c in vcols]
+    chk = balance(rows, rcost, W)
+    var = balance(vcols, vcost, W)
     bw = lpt(list(range(nb)), [1.0] * nb, W)
     col_blocks = [[i for i, b in enumerate(blocks) if b[1] == c] for c in range(nb)]
     col_ptr = [0]
@@ -109,7 +152,10 @@ def gen(name, base, z):
     s += arr("VAR_COLS", vl)
     s += arr("BW_PTR", bp)
     s += arr("BW_COLS", bl)
-    s += pair_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z)
+    s += task_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z)
+    # one frame per lane, 6 waves (flood_w6.inc): the fixed kernel's slot numbering
+    s += task_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z, W=6, prefix="S", frames=1, add=1.94,
+                       remap=False)
     s += "};\n\n"
     return s
 
@@ -134,29 +180,30 @@ def var_task_adds(d, lo, hi):
     return pre + sum(d - 1 - e for e in range(lo, hi))
 
 
-def var_task_cost(d, lo, hi):
-    # pipe cycles at 4 waves / SIMD (tools/ubench): v_pk_add_f32 2.6; + LDS reads / writes issued
-    return 2.6 * var_task_adds(d, lo, hi) + 1.0 * d + 1.5 * (hi - lo) + 6.0
+def var_task_cost(d, lo, hi, add=2.6):
+    # pipe cycles at 4 waves / SIMD (tools/ubench): v_pk_add_f32 2.6 (the pair kernel), v_add_f32
+    # 1.94 (one frame per lane); + LDS reads / writes issued
+    return add * var_task_adds(d, lo, hi) + 1.0 * d + 1.5 * (hi - lo) + 6.0
 
 
-def split_column(d, parts):
+def split_column(d, parts, add=2.6):
     """output ranges [lo, hi) of a degree-d column cut into `parts` tasks of about equal cost"""
     bounds = [0]
     for q in range(1, parts):
         # the cut after which the first q parts hold q/parts of the cost (greedy on prefix cost)
-        total = var_task_cost(d, 0, d)
+        total = var_task_cost(d, 0, d, add)
         best = min(range(bounds[-1] + 1, d), key=lambda h: abs(
-            sum(var_task_cost(d, bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1))
-            + var_task_cost(d, bounds[-1], h) - q * total / parts))
+            sum(var_task_cost(d, bounds[i], bounds[i + 1], add) for i in range(len(bounds) - 1))
+            + var_task_cost(d, bounds[-1], h, add) - q * total / parts))
         bounds.append(best)
     bounds.append(d)
     return [(bounds[i], bounds[i + 1]) for i in range(parts)]
 
 
-def row_cost(dcr, nslot):
+def row_cost(dcr, nslot, frames=2):
     # per frame: the two minima (half rate, 4.1), sign parity (bitop3 per two messages), per slot
-    # edge compare + select + sign (4.1 + 4.1 + 2.2), row constants; x 2 frames
-    return 2 * (4.1 * n_min_ops(dcr) + 2.2 * (dcr // 2) + 10.4 * nslot + 12.0) + 2.0 * dcr
+    # edge compare + select + sign (4.1 + 4.1 + 2.2), row constants; x frames per lane
+    return frames * (4.1 * n_min_ops(dcr) + 2.2 * (dcr // 2) + 10.4 * nslot + 12.0) + 2.0 * dcr
 
 
 def makespan(tasks, cost, w):
@@ -165,13 +212,17 @@ def makespan(tasks, cost, w):
     return max(loads), per
 
 
-def pair_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z):
+def task_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z, W=PW, prefix="P", frames=2, add=2.6,
+                  remap=True):
+    """Rows (LPT + refinement) and variable tasks (columns split by output range while that lowers
+    the LPT makespan) for W waves.  frames / add: lanes' frames and the pipe cost of one ordered
+    add (2 frames on v_pk_add_f32, or 1 on v_add_f32)."""
     mb = len(dc)
     nb = len(dv)
     # rows
     rows = list(range(mb))
-    rc = [row_cost(dc[r], sum(1 for i in range(row_ptr[r], row_ptr[r + 1]) if slot[i] >= 0)) for r in rows]
-    chk = lpt(rows, rc, PW)
+    rc = [row_cost(dc[r], sum(1 for i in range(row_ptr[r], row_ptr[r + 1]) if slot[i] >= 0), frames) for r in rows]
+    chk = balance(rows, rc, W)
     # variable tasks: split the heaviest columns while the LPT makespan improves
     vcols = [c for c in range(nb) if dv[c] >= 2]
     parts = {c: 1 for c in vcols}
@@ -179,19 +230,21 @@ def pair_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z):
     def tasks_of(parts):
         t = []
         for c in vcols:
-            for lo, hi in split_column(dv[c], parts[c]):
+            for lo, hi in split_column(dv[c], parts[c], add):
                 t.append((c, lo, hi))
         return t
 
     def span(parts):
         t = tasks_of(parts)
-        cost = [var_task_cost(dv[c], lo, hi) for c, lo, hi in t]
-        return makespan(t, cost, PW)
+        cost = [var_task_cost(dv[c], lo, hi, add) for c, lo, hi in t]
+        per = balance(t, cost, W)
+        c = dict(zip(t, cost))
+        return max(sum(c[x] for x in p) for p in per), per
 
     best, per = span(parts)
     while True:
         t = tasks_of(parts)
-        cost = [var_task_cost(dv[c], lo, hi) for c, lo, hi in t]
+        cost = [var_task_cost(dv[c], lo, hi, add) for c, lo, hi in t]
         heavy = t[max(range(len(t)), key=lambda i: cost[i])][0]
         trial = dict(parts)
         trial[heavy] += 1
@@ -211,6 +264,8 @@ def pair_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z):
         for i in col_blocks[c]:
             pslot[slot[i]] = n
             n += 1
+    if not remap:
+        pslot = list(range(nslots))
     vt_ptr, vt_col, vt_lo, vt_hi = [0], [], [], []
     for p in per:
         for c, lo, hi in sorted(p):
@@ -223,15 +278,15 @@ def pair_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z):
     for p in chk:
         cl += p
         cp.append(len(cl))
-    s = f"    // frame-pair kernel: {PW} waves; variable tasks (column, outputs [lo, hi)); slot remap\n"
-    s += f"    static constexpr int PW = {PW};\n"
-    s += arr("P_CHK_PTR", cp)
-    s += arr("P_CHK_ROWS", cl)
-    s += arr("P_VT_PTR", vt_ptr)
-    s += arr("P_VT_COL", vt_col)
-    s += arr("P_VT_LO", vt_lo)
-    s += arr("P_VT_HI", vt_hi)
-    s += arr("P_SLOT", pslot)
+    s = f"    // {prefix}: {W} waves, {frames} frame(s) per lane; variable tasks (column, outputs [lo, hi)); slot map\n"
+    s += f"    static constexpr int {prefix}W = {W};\n"
+    s += arr(f"{prefix}_CHK_PTR", cp)
+    s += arr(f"{prefix}_CHK_ROWS", cl)
+    s += arr(f"{prefix}_VT_PTR", vt_ptr)
+    s += arr(f"{prefix}_VT_COL", vt_col)
+    s += arr(f"{prefix}_VT_LO", vt_lo)
+    s += arr(f"{prefix}_VT_HI", vt_hi)
+    s += arr(f"{prefix}_SLOT", pslot)
     return s
 
 

@@ -360,13 +360,15 @@ def test_streaming_large_sparse_code_chunked_grid(cuda, oracle_mod):
     assert np.array_equal(bits.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("variant", ["LDPC_FLOOD_PAIR", "LDPC_FLOOD_W6"])
 @pytest.mark.parametrize("z", [4, 32])
 @pytest.mark.parametrize("algo", ["minsum", "bp"])
-def test_pair_kernel_matches_fixed_kernel(cuda, monkeypatch, z, algo):
-    """The frame-pair kernel (two frames per lane, the default without early stopping on the
-    reference's codes) against the one-frame fixed kernel (LDPC_FLOOD_PAIR=0): identical decisions,
-    counters and iteration outputs, for odd batch sizes (a workgroup's second frame of a pair
-    missing), both output dtypes, and zeros / infinities / NaN in some frames (the exact path)."""
+def test_pair_kernel_matches_fixed_kernel(cuda, monkeypatch, z, algo, variant):
+    """The opt-in kernels without early stopping on the reference's codes -- the frame-pair kernel
+    (two frames per lane, LDPC_FLOOD_PAIR=1) and the 6-wave kernel (LDPC_FLOOD_W6=1) -- against the
+    default 4-wave fixed kernel: identical decisions, counters and iteration outputs, for odd batch
+    sizes (a workgroup's last frame(s) missing), both output dtypes, and zeros / infinities / NaN in
+    some frames (the exact path)."""
     H = H_of(z)
     n = H.shape[1]
     rng = np.random.default_rng(100 + z)
@@ -383,7 +385,7 @@ def test_pair_kernel_matches_fixed_kernel(cuda, monkeypatch, z, algo):
         x = torch.from_numpy(llr).to(cuda)
         outs = []
         for pair in ("1", "0"):
-            monkeypatch.setenv("LDPC_FLOOD_PAIR", pair)
+            monkeypatch.setenv(variant, pair)
             cnt = torch.zeros(4, dtype=torch.int64, device=cuda)
             b8, it, fi = mk().decode(x, out_dtype=torch.uint8, counters=cnt, return_frame_iters=True)
             bf, _ = mk().decode(x)
