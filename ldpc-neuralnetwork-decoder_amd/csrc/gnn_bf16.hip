@@ -156,6 +156,9 @@ struct GmArgs {
     GtArgs G;
     __bf16 *Mv, *Mc;
     const uint8_t *active;  // early termination: frames still decoding (null = all)
+    // early termination after the first syndrome pass: the frames still decoding, ascending
+    // (list[0 .. *count)); null = every frame of the range
+    const int32_t *list, *count;
     int Gv, Gc, E, N;
     int64_t B;
 };
@@ -163,8 +166,10 @@ struct GmArgs {
 __global__ __launch_bounds__(256) void gnn_bf16_gm_kernel(GmArgs A) {
     const uint32_t w = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
     const uint32_t nt = (uint32_t)(A.G.n_tiles - A.G.first);
-    if (w >= (uint32_t)A.B * nt) return;
-    const uint32_t b = w / nt, t = w - b * nt + (uint32_t)A.G.first;
+    const uint32_t nact = A.count ? (uint32_t)__builtin_amdgcn_readfirstlane(*A.count) : (uint32_t)A.B;
+    if (w >= nact * nt) return;
+    const uint32_t slot = w / nt, t = w - slot * nt + (uint32_t)A.G.first;
+    const uint32_t b = A.list ? (uint32_t)A.list[slot] : slot;
     if (A.active && !A.active[b]) return;
     const int lane = threadIdx.x & 63, q = lane >> 3, p0 = 8 * (lane & 7);
     const int2 md = A.G.meta[t];
@@ -236,6 +241,7 @@ struct MlpArgs {
     int64_t B;
     float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
     const uint8_t *active;               // early termination: frames still decoding (null = all)
+    const int32_t *list, *count;         // early termination: the frames still decoding (see GmArgs)
     const float *kd_last, *bo_last;      // early termination: the last layer's output projection
 };
 
@@ -316,8 +322,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
 
     const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
     constexpr bool layer0 = (MODE & 1) != 0, last = (MODE & 2) != 0;
-    const int64_t ntiles = A.B * A.tpf;
+    // tiles of the frames still decoding: slot-major (slot s = the s-th listed frame)
+    const int64_t nact = A.count ? (int64_t)__builtin_amdgcn_readfirstlane(*A.count) : A.B;
+    const int64_t ntiles = nact * A.tpf;
     const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
+    auto frame_of = [&](int64_t slot) -> int64_t { return A.list ? (int64_t)A.list[slot] : slot; };
     // frame / in-frame tile counters, advanced without divisions
     const int64_t sb = tw.stride / A.tpf, sk = tw.stride - sb * A.tpf;
     int64_t fb = tw.first / A.tpf, fk = tw.first - fb * A.tpf;
@@ -328,13 +337,15 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         return A.info[m0 < A.E ? m0 : A.E - 1];
     };
     // the frame's "still decoding" flag of tile t (frame b), read ahead of the tile's row loads
-    auto load_on = [&](int64_t t, int64_t b) -> bool { return !A.active || A.active[t < tw.end ? b : fb]; };
+    auto load_on = [&](int64_t t, int64_t b) -> bool {
+        return A.list || !A.active || A.active[t < tw.end ? b : fb];  // listed frames are active
+    };
     auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k) {
         TileIn I;
         const int m0 = (int)k * 32 + j;
         I.ok = m0 < A.E && t < tw.end;
         const int m = m0 < A.E ? m0 : A.E - 1;
-        const int64_t bb = t < tw.end ? b : fb;
+        const int64_t bb = frame_of(t < tw.end ? b : fb);
         I.ty = inf.z;
         I.var = inf.w;
         I.one = !layer0 && A.d1 && inf.x < 0;
@@ -499,10 +510,13 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
                                                                 const int32_t *__restrict__ cg_mem, int Gc,
                                                                 const int32_t *__restrict__ msg_var, int layer,
                                                                 uint8_t *__restrict__ active,
+                                                                const int32_t *__restrict__ list,
+                                                                const int32_t *__restrict__ count,
                                                                 int32_t *__restrict__ iters, float *__restrict__ probs) {
     extern __shared__ uint32_t bits[];
     __shared__ int odd;
-    const int64_t b = blockIdx.x;
+    if (count && (int)blockIdx.x >= *count) return;
+    const int64_t b = list ? list[blockIdx.x] : blockIdx.x;
     if (!active[b]) return;
     const float *mo = msg_out + b * E, *lr = llr + b * N;
     const int32_t *vptr = csr_ptr(csr), *vmem = csr_mem(csr, N);
@@ -534,6 +548,32 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
     for (int v = threadIdx.x; v < N; v += blockDim.x) probs[b * N + v] = 1.0f / (1.0f + expf(-z(v)));
 }
 
+// The frames still decoding, ascending: list[0 .. *count) (one workgroup; a block-wide scan per
+// 1024 frames).  The next layer's kernels walk only these.
+__global__ __launch_bounds__(1024) void gnn_bf16_compact_kernel(const uint8_t *__restrict__ active, int64_t nb,
+                                                                int32_t *__restrict__ list, int32_t *__restrict__ count) {
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int base = 0;
+    for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
+        const int64_t f = c0 + tid;
+        const bool a = f < nb && active[f];
+        const uint64_t m = __ballot(a);
+        const int before = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int q = 0; q < 16; ++q) {
+            off += q < w ? wsum[q] : 0;
+            tot += wsum[q];
+        }
+        if (a) list[base + off + before] = (int32_t)f;
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) *count = base;
+}
+
 __global__ void fill_i32_kernel(int32_t *p, int64_t n, int32_t v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -541,7 +581,7 @@ __global__ void fill_i32_kernel(int32_t *p, int64_t n, int32_t v) {
 
 struct Bf16Ws {
     float *kd, *memb, *msg_out;
-    int32_t *csr;
+    int32_t *csr, *alist, *acount;
     int4 *info;
     uint8_t *active;
     __bf16 *xa, *xb, *Mv, *Mc;
@@ -554,6 +594,7 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
     const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * p->E * 4);
     const int64_t inf = al(p->E * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
+    const int64_t alb = al(B * 4) + 256;  // active list [B] + the two ranges' counts
     char *c = static_cast<char *>(base);
     Bf16Ws w;
     w.info = reinterpret_cast<int4 *>(c + kd + memb + xa + xb + mv + mc + vs);
@@ -566,7 +607,9 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     w.Mv = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb);
     w.Mc = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb + mv);
     w.msg_out = reinterpret_cast<float *>(c + kd + memb + xa + xb + mv + mc);
-    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf + act + cs;
+    w.alist = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs);
+    w.acount = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + al(B * 4));
+    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb;
     return w;
 }
 
@@ -617,6 +660,13 @@ int gnn_streams_bf16() {
         return (e && std::atoi(e) == 1) ? 1 : 2;
     }();
     return t;
+}
+
+// LDPC_GNN_ET_COMPACT=0: after a syndrome pass the kernels still walk every frame and skip the
+// finished ones (A/B); default: they walk the compacted list of frames still decoding
+int compact_env() {
+    const char *e = std::getenv("LDPC_GNN_ET_COMPACT");  // read per call (tests toggle it)
+    return e ? std::atoi(e) : 1;
 }
 
 int mlp_variant() {
@@ -680,9 +730,11 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     const float *bo_last = layer_w(d_weights, T, L - 1).bo;
 
     // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
-    auto run_range = [&](int64_t b0, int64_t nb, hipStream_t st) -> int {
+    auto run_range = [&](int64_t b0, int64_t nb, hipStream_t st, int slot) -> int {
     const int64_t xoff = b0 * p->E * H;
     uint8_t *act = et ? w.active + b0 : nullptr;
+    int32_t *alist = w.alist + b0, *acount = w.acount + slot;
+    bool listed = false;  // after the first syndrome pass the kernels walk the active list
     const __bf16 *x_in = nullptr;
     for (int l = 0; l < L; ++l) {
         const LayerW lw = layer_w(d_weights, T, l);
@@ -703,6 +755,8 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.N = N;
         gm.B = nb;
         gm.active = act;
+        gm.list = listed ? alist : nullptr;
+        gm.count = listed ? acount : nullptr;
         const int64_t gwaves = nb * (gm.G.n_tiles - gm.G.first);
         hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, st, gm);
         LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
@@ -730,6 +784,8 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.B = nb;
         m.msg_out = w.msg_out + b0 * p->E;
         m.active = act;
+        m.list = listed ? alist : nullptr;
+        m.count = listed ? acount : nullptr;
         m.kd_last = et && l < L - 1 ? kd_last : nullptr;
         m.bo_last = bo_last;
         const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0);
@@ -739,8 +795,14 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         if (m.kd_last) {
             hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)nb), dim3(256), (size_t)(N + 31) / 32 * 4, st,
                                w.msg_out + b0 * p->E, w.csr, p->E, d_llr + b0 * N, N, p->cg_ptr, p->cg_mem, p->Gc,
-                               d_msg_var, l, act, d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N);
+                               d_msg_var, l, act, listed ? alist : nullptr, listed ? acount : nullptr,
+                               d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N);
             LDPC_CHECK_LAUNCH("gnn_bf16_syndrome_kernel");
+            if (compact_env()) {
+                hipLaunchKernelGGL(gnn_bf16_compact_kernel, dim3(1), dim3(1024), 0, st, act, nb, alist, acount);
+                LDPC_CHECK_LAUNCH("gnn_bf16_compact_kernel");
+                listed = true;
+            }
         }
         x_in = m.x_out;
     }
@@ -753,11 +815,11 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         const int64_t b1 = B / 2;
         LDPC_HIP(hipEventRecord(fork, s));
         LDPC_HIP(hipStreamWaitEvent(s2, fork, 0));
-        if (int rc = run_range(0, b1, s)) return rc;
-        if (int rc = run_range(b1, B - b1, s2)) return rc;
+        if (int rc = run_range(0, b1, s, 0)) return rc;
+        if (int rc = run_range(b1, B - b1, s2, 1)) return rc;
         LDPC_HIP(hipEventRecord(join, s2));
         LDPC_HIP(hipStreamWaitEvent(s, join, 0));
-    } else if (int rc = run_range(0, B, s)) {
+    } else if (int rc = run_range(0, B, s, 0)) {
         return rc;
     }
     return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s);

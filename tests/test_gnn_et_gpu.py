@@ -51,8 +51,12 @@ def test_no_stop_is_the_full_run(cuda):
     assert torch.equal(p0, p1)
 
 
-@pytest.mark.parametrize("z,layers,B", [(4, 5, 512), (32, 4, 64), (32, 15, 64)])
-def test_stops_exactly_on_codeword_decisions(cuda, oracle_mod, z, layers, B):
+@pytest.mark.parametrize("compact", ["1", "0"])
+@pytest.mark.parametrize("z,layers,B", [(4, 5, 512), (32, 4, 64), (32, 15, 64), (32, 3, 300)])
+def test_stops_exactly_on_codeword_decisions(cuda, oracle_mod, monkeypatch, z, layers, B, compact):
+    """(compact: after a syndrome pass the layers walk the list of frames still decoding, or --
+    LDPC_GNN_ET_COMPACT=0 -- every frame, skipping the finished ones; same results either way)"""
+    monkeypatch.setenv("LDPC_GNN_ET_COMPACT", compact)
     base, H, dec, conv = _decoder(z, layers, cuda, seed=1)
     with torch.no_grad():  # second Linear of every MLP = 0: x = 0 after every layer
         for layer in dec.gnn_layers:

@@ -1,7 +1,7 @@
 # Round 3: the 6-wave kernel and the rebalanced 4-wave schedule vs the previous schedule (A/B), flood tests
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r03d; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_flood_gpu.py -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_flood.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_flood_gpu.py tests/test_gnn_et_gpu.py -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_flood.log 2>&1; rc=$?
 tail -4 $O/pytest_flood.log; [ $rc -eq 0 ] || exit $rc
 V=ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib
 one() {  # name, env...
