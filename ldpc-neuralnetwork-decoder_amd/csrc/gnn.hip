@@ -1144,11 +1144,27 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     };
     add_ptiles(vptr, vmem, n_vgroups, 0);
     const int n_ptiles_v = (int)(pt_meta.size() / 4);
+    int n_ptiles_v1 = 0;  // leading var tiles of degree-1 groups only (padding has degree 0)
+    while (n_ptiles_v1 < n_ptiles_v &&
+           std::all_of(pt_deg.begin() + 32 * n_ptiles_v1, pt_deg.begin() + 32 * (n_ptiles_v1 + 1),
+                       [](int32_t d) { return d <= 1; }))
+        ++n_ptiles_v1;
     add_ptiles(cptr, cmem, n_cgroups, 1);
+    // bf16 projected MLP: degree-1 var groups' messages first, each part padded to whole tiles
+    std::vector<int32_t> mperm;
+    auto vdeg = [&](int64_t m) { return vptr[h_vgroup[m] + 1] - vptr[h_vgroup[m]]; };
+    for (int64_t m = 0; m < E; ++m)
+        if (vdeg(m) == 1) mperm.push_back((int32_t)m);
+    while (mperm.size() % 32) mperm.push_back(-1);
+    const int n_mtiles_v1 = (int)(mperm.size() / 32);
+    for (int64_t m = 0; m < E; ++m)
+        if (vdeg(m) != 1) mperm.push_back((int32_t)m);
+    while (mperm.size() % 32) mperm.push_back(-1);
     pt.insert(pt.end(), pt_meta.begin(), pt_meta.end());
     pt.insert(pt.end(), pt_grp.begin(), pt_grp.end());
     pt.insert(pt.end(), pt_deg.begin(), pt_deg.end());
     pt.insert(pt.end(), pt_mem.begin(), pt_mem.end());
+    pt.insert(pt.end(), mperm.begin(), mperm.end());
     std::vector<int32_t> blob;
     blob.insert(blob.end(), h_vgroup, h_vgroup + E);
     blob.insert(blob.end(), h_cgroup, h_cgroup + E);
@@ -1184,10 +1200,14 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     }
     p->n_ptiles = (int)(pt_meta.size() / 4);
     p->n_ptiles_v = n_ptiles_v;
+    p->n_ptiles_v1 = n_ptiles_v1;
     p->pt_meta = reinterpret_cast<const int4 *>(p->d_pt);
     p->pt_grp = p->d_pt + pt_meta.size();
     p->pt_deg = p->pt_grp + pt_grp.size();
     p->pt_mem = p->pt_deg + pt_deg.size();
+    p->mt_perm = p->pt_mem + pt_mem.size();
+    p->n_mtiles = (int)(mperm.size() / 32);
+    p->n_mtiles_v1 = n_mtiles_v1;
     p->vgroup = p->d_tab;
     p->cgroup = p->vgroup + E;
     p->vg_ptr = p->cgroup + E;

@@ -32,10 +32,16 @@ struct ldpc_gnn_plan {
     // its degree (0 for padding); pt_mem[off + 32 i + j] = i-th member message of lane j's group
     // (message 0 past its degree; max degree + 1 rows per tile).
     int n_ptiles = 0;
-    int n_ptiles_v = 0;  // the leading tiles are the var side's
+    int n_ptiles_v = 0;   // the leading tiles are the var side's
+    int n_ptiles_v1 = 0;  // the leading var tiles whose groups all have degree 1
     int32_t *d_pt = nullptr;
     const int4 *pt_meta = nullptr;
     const int32_t *pt_grp = nullptr, *pt_deg = nullptr, *pt_mem = nullptr;
+    // bf16 projected MLP (gnn_bf16.hip): message order of its 32-message tiles -- the messages of
+    // degree-1 var groups first (ascending), then the rest (ascending), each part padded to whole
+    // tiles with -1, so every tile is either all degree-1 or has none.  mt_perm[32 n_mtiles].
+    int n_mtiles = 0, n_mtiles_v1 = 0;
+    const int32_t *mt_perm = nullptr;
 };
 
 namespace ldpc {

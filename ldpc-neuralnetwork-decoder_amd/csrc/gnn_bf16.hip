@@ -117,6 +117,20 @@ __global__ void gnn_bf16_info_kernel(int E, const int32_t *vgroup, const int32_t
     info[m] = make_int4(one ? ~g : g, cgroup[m], msg_type[m], msg_var[m]);
 }
 
+// Projected MLP: per tile slot i of the plan's message order (gnn.hpp mt_perm),
+// {var group (~ when degree 1 and d1), check group, type | variable << 8, message (-1 = padding)};
+// padding slots carry message 0's groups (valid addresses, nothing written).
+__global__ void gnn_bf16_info_perm_kernel(int n, const int32_t *perm, const int32_t *vgroup, const int32_t *vg_ptr,
+                                          int d1, const int32_t *cgroup, const int32_t *msg_type,
+                                          const int32_t *msg_var, int4 *info) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int mp = perm[i], m = mp < 0 ? 0 : mp;
+    const int g = vgroup[m];
+    const bool one = d1 && vg_ptr[g + 1] - vg_ptr[g] == 1;
+    info[i] = make_int4(one ? ~g : g, cgroup[m], msg_type[m] | (msg_var[m] << 8), mp);
+}
+
 struct GtArgs {
     const int2 *meta;
     const int32_t *grp, *mem;
@@ -214,37 +228,6 @@ __global__ __launch_bounds__(256) void gnn_bf16_gm_kernel(GmArgs A) {
     *reinterpret_cast<bf16x8 *>(dst + p0) = o;
 }
 
-// ------------------------------------------------------------------------ fused MLP
-// LDS image (bytes): W1v, W1c bf16 [64 u][136] (128 stored columns + 8 pad: conflict-free
-// ds_read_b128), W2v, W2c bf16 [64 o][72] (columns in GEMM1-accumulator order), then fp32:
-// K [T + 2][132] (two sides x 64 + 4 pad, so that lanes reading different types' rows spread
-// over the banks), b2 [64], wo [64].
-constexpr int kW1B = 64 * 136 * 2, kW2B = 64 * 72 * 2;
-constexpr int kOffW1v = 0, kOffW1c = kW1B, kOffW2v = 2 * kW1B, kOffW2c = 2 * kW1B + kW2B;
-constexpr int kOffK = 2 * kW1B + 2 * kW2B;
-constexpr int kKStride = 132;
-inline size_t mlp_lds_bytes(int T, bool d1) {
-    return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * 64 : 0)) * 4;
-}
-
-struct MlpArgs {
-    const __bf16 *x_in;  // null at layer 0
-    __bf16 *x_out;       // null at the last layer
-    const __bf16 *Mv, *Mc;
-    const int4 *info;                    // per message {var group, check group, type, variable}
-    const float *llr;
-    const float *w1v, *w1c, *w2v, *w2c;  // this layer, nn.Linear layout, fp32
-    const float *kd;                     // this layer's derived constants
-    const float *bo;                     // output_projection bias (device)
-    int T, Gv, Gc, E, N, tpf;            // tpf = 32-message tiles per frame
-    int d1;                              // degree-1 var groups use D1 (info.x < 0), layers >= 1
-    int64_t B;
-    float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
-    const uint8_t *active;               // early termination: frames still decoding (null = all)
-    const int32_t *list, *count;         // early termination: the frames still decoding (see GmArgs)
-    const float *kd_last, *bo_last;      // early termination: the last layer's output projection
-};
-
 __device__ __forceinline__ bf16x8 ld8(const char *p) { return *reinterpret_cast<const bf16x8 *>(p); }
 __device__ __forceinline__ f32x16 ld16(const float *p) {
     f32x16 v;
@@ -281,35 +264,223 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16 &a, int half) {
     return o;
 }
 
+// ------------------------------------------------------------------------ projected group rows
+// (default; LDPC_GNN_BF16_PROJ=0 keeps the group-mean rows above).  As the fp32 path (gnn.hip):
+// W1_s,right g is one row per GROUP, so it is computed here once per group and the MLP starts
+// GEMM1 from it: the MLP's GEMM1 runs over x alone, 32 instead of 48 MFMAs per 32-message tile.
+// One wave per (frame, projection tile of 32 groups of one side): lane (q, c) sums stored
+// positions 8c .. 8c+7 of the tile's groups 8p + q (p < 4, ascending members, two members of all
+// four in flight), x 1/|group| + the group's mean type embedding, rounded to bf16 -- the same row
+// the group-mean kernel writes -- into the wave's LDS tile; lane (j, h) then reads group j's row
+// as the B operand of 2 x 4 v_mfma_f32_32x32x16_bf16 against W1_right (bf16, LDS) and writes the
+// product in bf16, in the features' stored order, to Pv / Pc (the Mv / Mc buffers).  No bias:
+// b1 is in the type constants.
+constexpr int kPjRow = 144;  // bytes per LDS row: 64 bf16 + 8 pad
+inline size_t proj_lds_bytes_bf16(int waves) { return (size_t)(2 + waves / 2) * 64 * kPjRow; }
+
+struct PjArgs {
+    const __bf16 *x_in;  // null at layer 0
+    const float *llr;
+    const int32_t *msg_var;
+    const float *w_in, *b_in;
+    const float *memb;  // this layer, (Gv + Gc, 64) fp32 stored order
+    const float *w1v, *w1c;
+    const int4 *meta;
+    const int32_t *grp, *deg, *mem;
+    int n_tiles, first;
+    __bf16 *Pv, *Pc;
+    const uint8_t *active;
+    const int32_t *list, *count;
+    int Gv, Gc, E, N;
+    int64_t B;
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void gnn_bf16_proj_kernel(PjArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 64 * 64; i += NT) {
+        const int u = i >> 6, p = i & 63, k = 64 + pi_unit(p);
+        reinterpret_cast<__bf16 *>(smem)[u * (kPjRow / 2) + p] = (__bf16)A.w1v[u * 128 + k];
+        reinterpret_cast<__bf16 *>(smem + 64 * kPjRow)[u * (kPjRow / 2) + p] = (__bf16)A.w1c[u * 128 + k];
+    }
+    __syncthreads();
+    const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
+    const int q = lane >> 3, c8 = 8 * (lane & 7);
+    char *tile = smem + 2 * 64 * kPjRow + wave * 32 * kPjRow;
+    const int nt = A.n_tiles - A.first;
+    const int64_t nact = A.count ? (int64_t)__builtin_amdgcn_readfirstlane(*A.count) : A.B;
+    const TileWalk tw = xcd_tiles(nact * nt, NT / 64, wave);
+    for (int64_t tt = tw.first; tt < tw.end; tt += tw.stride) {
+        const int64_t slot = tt / nt;
+        const int t = A.first + (int)(tt - slot * nt);
+        const int64_t b = A.list ? (int64_t)A.list[slot] : slot;
+        if (A.active && !A.active[b]) continue;
+        const int4 md = A.meta[t];  // {side, max degree, member offset, 0}
+        int dg[4];
+        float acc[4][8];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            dg[p] = A.deg[32 * t + 8 * p + q];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[p][k] = 0.0f;
+        }
+        const int32_t *mem = A.mem + md.z + q;
+        if (A.x_in) {
+            const __bf16 *xb = A.x_in + b * A.E * H + c8;
+            for (int i = 0; i < md.y; i += 2) {  // the table holds max degree + 1 rows
+                bf16x8 v[4], w[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    v[p] = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)mem[32 * i + 8 * p] * H);
+                    w[p] = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)mem[32 * (i + 1) + 8 * p] * H);
+                }
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    if (i < dg[p]) {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) acc[p][k] += (float)v[p][k];
+                    }
+                    if (i + 1 < dg[p]) {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) acc[p][k] += (float)w[p][k];
+                    }
+                }
+            }
+        } else {
+            float ls[4] = {};
+            for (int i = 0; i < md.y; ++i) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    if (i < dg[p]) ls[p] += A.llr[b * A.N + A.msg_var[mem[32 * i + 8 * p]]];
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int u = pi_unit(c8 + k);
+                    acc[p][k] = fmaf(A.w_in[u], ls[p], (float)dg[p] * A.b_in[u]);
+                }
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int s = 8 * p + q, g = A.grp[32 * t + s];
+            bf16x8 o;
+            if (g >= 0) {
+                const float *e = A.memb + (int64_t)(md.x ? A.Gv + g : g) * H + c8;
+                const float inv = 1.0f / (float)dg[p];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o[k] = (__bf16)fmaf(acc[p][k], inv, e[k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o[k] = (__bf16)0.0f;
+            }
+            *reinterpret_cast<bf16x8 *>(tile + s * kPjRow + 2 * c8) = o;
+        }
+        __builtin_amdgcn_wave_barrier();
+        bf16x8 gb[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) gb[s] = ld8(tile + j * kPjRow + 16 * h + 32 * s);
+        __builtin_amdgcn_wave_barrier();
+        const char *W = smem + (md.x ? 64 * kPjRow : 0);
+        f32x16 h0 = {}, h1 = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W + j * kPjRow + 16 * h + 32 * s), gb[s], h0, 0, 0, 0);
+            h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W + (32 + j) * kPjRow + 16 * h + 32 * s), gb[s], h1, 0, 0, 0);
+        }
+        const int g = A.grp[32 * t + j];
+        if (g < 0) continue;
+        char *dst = reinterpret_cast<char *>(md.x ? A.Pc + (b * A.Gc + g) * H : A.Pv + (b * A.Gv + g) * H) + 16 * h;
+        *reinterpret_cast<bf16x8 *>(dst) = pack8(h0, 0);
+        *reinterpret_cast<bf16x8 *>(dst + 32) = pack8(h0, 1);
+        *reinterpret_cast<bf16x8 *>(dst + 64) = pack8(h1, 0);
+        *reinterpret_cast<bf16x8 *>(dst + 96) = pack8(h1, 1);
+    }
+}
+
+// ------------------------------------------------------------------------ fused MLP
+// LDS image (bytes): W1v, W1c bf16 [64 u][136] (128 stored columns + 8 pad: conflict-free
+// ds_read_b128), W2v, W2c bf16 [64 o][72] (columns in GEMM1-accumulator order), then fp32:
+// K [T + 2][132] (two sides x 64 + 4 pad, so that lanes reading different types' rows spread
+// over the banks), b2 [64], wo [64].
+constexpr int kW1B = 64 * 136 * 2, kW2B = 64 * 72 * 2;
+constexpr int kOffW1v = 0, kOffW1c = kW1B, kOffW2v = 2 * kW1B, kOffW2c = 2 * kW1B + kW2B;
+constexpr int kOffK = 2 * kW1B + 2 * kW2B;
+// projected MLP (MODE bit 2): W1v,left, W1c,left, W1v,left + W1v,right (degree-1 tiles) bf16
+// [64 u][72], W2v, W2c [64 o][72], then the fp32 part as above
+constexpr int kPOffW1v = 0, kPOffW1c = kW2B, kPOffW1s = 2 * kW2B, kPOffW2v = 3 * kW2B, kPOffW2c = 4 * kW2B;
+constexpr int kPOffK = 5 * kW2B;
+constexpr int kKStride = 132;
+inline size_t mlp_lds_bytes(int T, bool d1, bool proj) {
+    return (size_t)(proj ? kPOffK : kOffK) + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * 64 : 0)) * 4;
+}
+
+struct MlpArgs {
+    const __bf16 *x_in;  // null at layer 0
+    __bf16 *x_out;       // null at the last layer
+    const __bf16 *Mv, *Mc;               // group-mean rows, or (projected) W1_right g rows
+    const int4 *info;                    // per message {var group, check group, type, variable};
+                                         // projected: per tile slot (gnn_bf16_info_perm_kernel)
+    const float *llr;
+    const float *w1v, *w1c, *w2v, *w2c;  // this layer, nn.Linear layout, fp32
+    const float *kd;                     // this layer's derived constants
+    const float *bo;                     // output_projection bias (device)
+    int T, Gv, Gc, E, N, tpf;            // tpf = 32-message tiles per frame
+    int tpf1;                            // projected: the leading tiles of degree-1 messages
+    int d1;                              // degree-1 var groups use D1 (info.x < 0), layers >= 1
+    int64_t B;
+    float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
+    const uint8_t *active;               // early termination: frames still decoding (null = all)
+    const int32_t *list, *count;         // early termination: the frames still decoding (see GmArgs)
+    const float *kd_last, *bo_last;      // early termination: the last layer's output projection
+};
+
 // Per-tile inputs of one lane (message j of the tile, lane half h).
 struct TileIn {
     bf16x8 xf[4], af[4], cf[4];
     float l;
     int ty, var;
     bool one;  // degree-1 var group (D1 constant instead of K[ty][var side])
+    bool t1;   // projected: a tile of degree-1 messages (uniform over the wave)
     int64_t row, b;
     bool ok, on;  // on: the frame is still decoding (early termination)
 };
 
 // MODE bit 0: layer 0 (x from the LLRs, no GEMM1 over x, no residual); bit 1: last layer
-// (output projection + per-variable sum instead of writing x)
+// (output projection + per-variable sum instead of writing x); bit 2: projected group rows
+// (GEMM1 over x only, started from K + the group's W1_right g row; tiles in the plan's message
+// order, whose degree-1 tiles run GEMM1 over x with W1v,left + W1v,right and D1)
 template <int NT, int WPS, bool PF, int MODE>
 __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
-    for (int i = tid; i < 64 * 128; i += NT) {
-        const int u = i >> 7, p = i & 127;
-        const int k = p < 64 ? pi_unit(p) : 64 + pi_unit(p - 64);
-        reinterpret_cast<__bf16 *>(smem + kOffW1v)[u * 136 + p] = (__bf16)A.w1v[u * 128 + k];
-        reinterpret_cast<__bf16 *>(smem + kOffW1c)[u * 136 + p] = (__bf16)A.w1c[u * 128 + k];
+    constexpr bool proj = (MODE & 4) != 0;
+    constexpr int oW1v = proj ? kPOffW1v : kOffW1v, oW1c = proj ? kPOffW1c : kOffW1c;
+    constexpr int oW2v = proj ? kPOffW2v : kOffW2v, oW2c = proj ? kPOffW2c : kOffW2c;
+    constexpr int w1row = proj ? 144 : 272;  // bytes per W1 image row
+    if constexpr (proj) {
+        for (int i = tid; i < 64 * 64; i += NT) {
+            const int u = i >> 6, p = i & 63, k = pi_unit(p);
+            reinterpret_cast<__bf16 *>(smem + kPOffW1v)[u * 72 + p] = (__bf16)A.w1v[u * 128 + k];
+            reinterpret_cast<__bf16 *>(smem + kPOffW1c)[u * 72 + p] = (__bf16)A.w1c[u * 128 + k];
+            reinterpret_cast<__bf16 *>(smem + kPOffW1s)[u * 72 + p] = (__bf16)(A.w1v[u * 128 + k] + A.w1v[u * 128 + 64 + k]);
+        }
+    } else {
+        for (int i = tid; i < 64 * 128; i += NT) {
+            const int u = i >> 7, p = i & 127;
+            const int k = p < 64 ? pi_unit(p) : 64 + pi_unit(p - 64);
+            reinterpret_cast<__bf16 *>(smem + kOffW1v)[u * 136 + p] = (__bf16)A.w1v[u * 128 + k];
+            reinterpret_cast<__bf16 *>(smem + kOffW1c)[u * 136 + p] = (__bf16)A.w1c[u * 128 + k];
+        }
     }
     for (int i = tid; i < 64 * 64; i += NT) {
         const int o = i >> 6, q = i & 63;
         const int u = pi_unit(q);  // GEMM2's k index = GEMM1 accumulator registers (see header)
-        reinterpret_cast<__bf16 *>(smem + kOffW2v)[o * 72 + q] = (__bf16)A.w2v[o * 64 + u];
-        reinterpret_cast<__bf16 *>(smem + kOffW2c)[o * 72 + q] = (__bf16)A.w2c[o * 64 + u];
+        reinterpret_cast<__bf16 *>(smem + oW2v)[o * 72 + q] = (__bf16)A.w2v[o * 64 + u];
+        reinterpret_cast<__bf16 *>(smem + oW2c)[o * 72 + q] = (__bf16)A.w2c[o * 64 + u];
     }
-    float *Ks = reinterpret_cast<float *>(smem + kOffK);
+    float *Ks = reinterpret_cast<float *>(smem + (proj ? kPOffK : kOffK));
     const int nk = (A.T + 2) * 128;
     for (int i = tid; i < nk; i += NT) Ks[(i >> 7) * kKStride + (i & 127)] = A.kd[i];
     float *tail = Ks + (A.T + 2) * kKStride;  // b2 [64], wo [64]
@@ -334,6 +505,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     // per-message static info {var group, check group, type, variable} of this lane's message
     auto load_info = [&](int64_t k) {
         const int m0 = (int)k * 32 + j;
+        if constexpr (proj) return A.info[m0];  // one entry per tile slot
         return A.info[m0 < A.E ? m0 : A.E - 1];
     };
     // the frame's "still decoding" flag of tile t (frame b), read ahead of the tile's row loads
@@ -343,12 +515,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k) {
         TileIn I;
         const int m0 = (int)k * 32 + j;
-        I.ok = m0 < A.E && t < tw.end;
-        const int m = m0 < A.E ? m0 : A.E - 1;
+        I.ok = (proj ? inf.w >= 0 : m0 < A.E) && t < tw.end;
+        const int m = proj ? (inf.w < 0 ? 0 : inf.w) : m0 < A.E ? m0 : A.E - 1;
         const int64_t bb = frame_of(t < tw.end ? b : fb);
-        I.ty = inf.z;
-        I.var = inf.w;
+        I.ty = proj ? (inf.z & 255) : inf.z;
+        I.var = proj ? (inf.z >> 8) : inf.w;
         I.one = !layer0 && A.d1 && inf.x < 0;
+        I.t1 = proj && !layer0 && A.d1 && k < A.tpf1;
         I.row = bb * A.E + m;
         I.b = bb;
         I.on = on;
@@ -367,7 +540,12 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         } else {
             I.l = A.llr[lb * A.N + I.var];
         }
-        if (layer0 || !A.d1 || inf.x >= 0) {
+        if constexpr (proj) {
+            if (!I.t1) {  // degree-1 tiles need no W1_right g row (D1 + W1v,left+right x)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
+            }
+        } else if (layer0 || !A.d1 || inf.x >= 0) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
         } else {  // degree-1 var group: g = x, its emb part is in D1
@@ -383,14 +561,25 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         if (!I.on) return;
         const float *Kt = Ks + I.ty * kKStride;
         f32x16 y0 = ld16(tail + 16 * h), y1 = ld16(tail + 32 + 16 * h);  // b2v + b2c
-        int wbase = j * 272 + 16 * h, w2base = j * 144 + 16 * h;
+        int wbase = j * w1row + 16 * h, w2base = j * 144 + 16 * h;
         asm volatile("" : "+v"(wbase), "+v"(w2base));
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-            const char *W1 = smem + (side == 0 ? kOffW1v : kOffW1c);
-            const char *W2 = smem + (side == 0 ? kOffW2v : kOffW2c);
-            const float *K0 = side == 0 && I.one ? D1s + I.ty * 64 : Kt + side * 64;
+            const char *W1 = smem + (side == 0 ? (proj && I.t1 ? kPOffW1s : oW1v) : oW1c);
+            const char *W2 = smem + (side == 0 ? oW2v : oW2c);
+            const bool d1k = proj ? I.t1 : I.one;
+            const float *K0 = side == 0 && d1k ? D1s + I.ty * 64 : Kt + side * 64;
             f32x16 h0 = ld16(K0 + 16 * h), h1 = ld16(K0 + 32 + 16 * h);
+            if (proj && !(side == 0 && I.t1)) {  // + the group's W1_right g row (bf16)
+                const bf16x8 *P = side == 0 ? I.af : I.cf;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    h0[i] += (float)P[0][i];
+                    h0[8 + i] += (float)P[1][i];
+                    h1[i] += (float)P[2][i];
+                    h1[8 + i] += (float)P[3][i];
+                }
+            }
             if constexpr (layer0) {  // + llr * (W1 w_in) + W1 b_in
                 const float *U = Ks + A.T * kKStride + side * 64 + 16 * h, *V = U + kKStride;
 #pragma unroll
@@ -402,14 +591,16 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + wbase + 32 * s), I.xf[s], h0, 0, 0, 0);
-                    h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * s), I.xf[s], h1, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * w1row + wbase + 32 * s), I.xf[s], h1, 0, 0, 0);
                 }
             }
+            if constexpr (!proj) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const bf16x8 g = side == 0 ? I.af[s] : I.cf[s];
-                h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + wbase + 32 * (4 + s)), g, h0, 0, 0, 0);
-                h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * (4 + s)), g, h1, 0, 0, 0);
+                for (int s = 0; s < 4; ++s) {
+                    const bf16x8 g = side == 0 ? I.af[s] : I.cf[s];
+                    h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + wbase + 32 * (4 + s)), g, h0, 0, 0, 0);
+                    h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * (4 + s)), g, h1, 0, 0, 0);
+                }
             }
             const bf16x8 p00 = relu8(h0, 0), p01 = relu8(h0, 1), p10 = relu8(h1, 0), p11 = relu8(h1, 1);
 #pragma unroll
@@ -593,7 +784,7 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4);
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
     const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * p->E * 4);
-    const int64_t inf = al(p->E * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
+    const int64_t inf = al(std::max<int64_t>(p->E, (int64_t)p->n_mtiles * 32) * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
     const int64_t alb = al(B * 4) + 256;  // active list [B] + the two ranges' counts
     char *c = static_cast<char *>(base);
     Bf16Ws w;
@@ -631,7 +822,11 @@ int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpAr
         case 0: return launch_mlp_t<NT, WPS, PF, 0>(tiles, lds, s, m);
         case 1: return launch_mlp_t<NT, WPS, PF, 1>(tiles, lds, s, m);
         case 2: return launch_mlp_t<NT, WPS, PF, 2>(tiles, lds, s, m);
-        default: return launch_mlp_t<NT, WPS, PF, 3>(tiles, lds, s, m);
+        case 3: return launch_mlp_t<NT, WPS, PF, 3>(tiles, lds, s, m);
+        case 4: return launch_mlp_t<NT, WPS, PF, 4>(tiles, lds, s, m);
+        case 5: return launch_mlp_t<NT, WPS, PF, 5>(tiles, lds, s, m);
+        case 6: return launch_mlp_t<NT, WPS, PF, 6>(tiles, lds, s, m);
+        default: return launch_mlp_t<NT, WPS, PF, 7>(tiles, lds, s, m);
     }
 }
 
@@ -669,6 +864,15 @@ int compact_env() {
     return e ? std::atoi(e) : 1;
 }
 
+// LDPC_GNN_BF16_PROJ=0: group-mean rows and GEMM1 over [x; g] (A/B); default: projected rows
+int proj_env() {
+    static int v = [] {
+        const char *e = std::getenv("LDPC_GNN_BF16_PROJ");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
 int mlp_variant() {
     static int v = [] {
         const char *e = std::getenv("LDPC_GNN_BF16_MLP");
@@ -691,8 +895,12 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     Bf16Ws w = carve_bf16(p, N, B, T, L, d_work);
     if (!d_work || work_bytes < w.bytes)
         return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
-    const int64_t tpf = (p->E + 31) / 32;
-    if (B * tpf >= (1LL << 31) || B * p->n_gtiles >= (1LL << 31) || p->E >= (1LL << 31))
+    // projected group rows (see gnn_bf16_proj_kernel): needs the plan's projection tiles and a
+    // variable index that fits the packed per-slot info (type | variable << 8)
+    const bool proj = proj_env() && p->n_ptiles > 0 && p->n_mtiles > 0 && N < (1 << 23);
+    const int64_t tpf = proj ? p->n_mtiles : (p->E + 31) / 32;
+    if (B * tpf >= (1LL << 31) || B * p->n_gtiles >= (1LL << 31) || B * p->n_ptiles >= (1LL << 31) ||
+        p->E >= (1LL << 31))
         return fail(LDPC_EUNSUPPORTED, "batch too large for one launch (chunk it)");
     // degree-1 skip when its D1 table still lets two 256-thread workgroups share a CU's LDS
     // (LDPC_GNN_BF16_D1=0 disables it, for A/B runs)
@@ -700,8 +908,8 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         const char *e = std::getenv("LDPC_GNN_BF16_D1");
         return e ? std::atoi(e) : 1;
     }();
-    const bool d1 = d1_env && p->n_gtiles_v1 > 0 && 2 * mlp_lds_bytes(T, true) <= 160 * 1024;
-    const size_t lds = mlp_lds_bytes(T, d1);
+    const bool d1 = d1_env && p->n_gtiles_v1 > 0 && 2 * mlp_lds_bytes(T, true, proj) <= 160 * 1024;
+    const size_t lds = mlp_lds_bytes(T, d1, proj);
     if (T > kBf16MaxTypes || lds > 160 * 1024)
         return fail(LDPC_EUNSUPPORTED, "too many message types for the bf16 LDS image");
     if (!g_cus) {
@@ -711,9 +919,16 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     }
     const GtArgs G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles, 0};
     const int Gtot = p->Gv + p->Gc;
-    hipLaunchKernelGGL(gnn_bf16_info_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, (int)p->E,
-                       p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, d_msg_type, d_msg_var, w.info);
-    LDPC_CHECK_LAUNCH("gnn_bf16_info_kernel");
+    if (proj) {
+        const int n = p->n_mtiles * 32;
+        hipLaunchKernelGGL(gnn_bf16_info_perm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, p->mt_perm,
+                           p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, d_msg_type, d_msg_var, w.info);
+        LDPC_CHECK_LAUNCH("gnn_bf16_info_perm_kernel");
+    } else {
+        hipLaunchKernelGGL(gnn_bf16_info_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, (int)p->E,
+                           p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, d_msg_type, d_msg_var, w.info);
+        LDPC_CHECK_LAUNCH("gnn_bf16_info_kernel");
+    }
     hipLaunchKernelGGL(gnn_bf16_kconst_kernel, dim3(L, T + 2), dim3(128), 0, s, d_weights, T, w.kd);
     LDPC_CHECK_LAUNCH("gnn_bf16_kconst_kernel");
     hipLaunchKernelGGL(gnn_bf16_memb_kernel, dim3((unsigned)(((int64_t)L * p->n_gtiles + 3) / 4)), dim3(256), 0, s,
@@ -757,9 +972,41 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.active = act;
         gm.list = listed ? alist : nullptr;
         gm.count = listed ? acount : nullptr;
-        const int64_t gwaves = nb * (gm.G.n_tiles - gm.G.first);
-        hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, st, gm);
-        LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
+        if (proj) {
+            PjArgs pj{};
+            pj.x_in = x_in;
+            pj.llr = gm.llr;
+            pj.msg_var = d_msg_var;
+            pj.w_in = gm.w_in;
+            pj.b_in = gm.b_in;
+            pj.memb = gm.memb;
+            pj.w1v = lw.w1v;
+            pj.w1c = lw.w1c;
+            pj.meta = p->pt_meta;
+            pj.grp = p->pt_grp;
+            pj.deg = p->pt_deg;
+            pj.mem = p->pt_mem;
+            pj.n_tiles = p->n_ptiles;
+            pj.first = d1 && l > 0 ? p->n_ptiles_v1 : 0;
+            pj.Pv = gm.Mv;
+            pj.Pc = gm.Mc;
+            pj.active = gm.active;
+            pj.list = gm.list;
+            pj.count = gm.count;
+            pj.Gv = p->Gv;
+            pj.Gc = p->Gc;
+            pj.E = (int)p->E;
+            pj.N = N;
+            pj.B = nb;
+            const int64_t pw = nb * (pj.n_tiles - pj.first);  // waves of work
+            const unsigned pgrid = (unsigned)std::min<int64_t>((pw + 3) / 4, (int64_t)g_cus * 8);
+            hipLaunchKernelGGL(gnn_bf16_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds_bytes_bf16(4), st, pj);
+            LDPC_CHECK_LAUNCH("gnn_bf16_proj_kernel");
+        } else {
+            const int64_t gwaves = nb * (gm.G.n_tiles - gm.G.first);
+            hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, st, gm);
+            LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
+        }
 
         MlpArgs m{};
         m.x_in = x_in;
@@ -780,6 +1027,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.E = (int)p->E;
         m.N = N;
         m.tpf = (int)tpf;
+        m.tpf1 = p->n_mtiles_v1;
         m.d1 = d1 ? 1 : 0;
         m.B = nb;
         m.msg_out = w.msg_out + b0 * p->E;
@@ -788,7 +1036,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.count = listed ? acount : nullptr;
         m.kd_last = et && l < L - 1 ? kd_last : nullptr;
         m.bo_last = bo_last;
-        const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0);
+        const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0) | (proj ? 4 : 0);
         const int rc = launch_mlp(mlp_variant(), mode, nb * tpf, lds, st, m);
         if (rc != LDPC_OK) return rc;
         LDPC_CHECK_LAUNCH("gnn_bf16_mlp_kernel");

@@ -285,6 +285,9 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
     (csrc/gnn.hip).  Oracle: oracle/oracle.py custom_variable_forward."""
 
     def __init__(self, num_messages, num_iterations=5, hidden_dim=64, num_message_types=1, depth_L=3):
+        if hidden_dim != 64:  # refused up front rather than at the first forward
+            raise ValueError(f"CustomVariableMessageGNNDecoder: this build's kernels run the hybrid GNN at "
+                             f"hidden_dim 64 only (got hidden_dim={hidden_dim})")
         super().__init__(num_messages, num_iterations, hidden_dim, num_message_types)
         self.gnn_layers = nn.ModuleList([
             CustomVariableMessageGNNLayer(num_message_types, hidden_dim, depth_L) for _ in range(num_iterations)])
@@ -319,8 +322,6 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
             if isinstance(cspec[0], str) and cspec[0] == "csr":
                 raise NotImplementedError("the hybrid GNN runs with clique (TannerToMessageGraph) or identity "
                                           "check adjacencies")
-        if self.hidden_dim != 64:
-            raise NotImplementedError("the hybrid GNN runs at hidden_dim 64")
         plan = self._plan(vspec, cspec, dev)
         blob = self._weights_blob(dev)
         L = len(self.gnn_layers)

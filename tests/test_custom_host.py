@@ -9,6 +9,7 @@ The reference's decoder cannot run.  What pins this build'
     restatement is the definition, cross-checked below against an independent numpy restatement;
   * the module's state_dict layout against the reference's constructor (fixture sd_keys)."""
 import numpy as np
+import pytest
 import torch
 
 from conftest import golden
@@ -148,3 +149,11 @@ def test_variable_decoder_state_dict_layout_matches_reference():
     sd = dec.state_dict()
     assert sorted(sd) == list(d["sdv_keys"])
     assert [len(sd[k].shape) and sd[k].numel() for k in sorted(sd)] == list(d["sdv_numel"])
+
+
+def test_variable_decoder_refuses_other_hidden_dims():
+    """The hybrid GNN's kernels are built for hidden_dim 64: other sizes are refused when the
+    decoder is constructed, with a message that says so (not at the first forward)."""
+    from ldpc_neural_decoder.models import CustomVariableMessageGNNDecoder
+    with pytest.raises(ValueError, match="hidden_dim 64"):
+        CustomVariableMessageGNNDecoder(40, 3, 32, 1, 3)
