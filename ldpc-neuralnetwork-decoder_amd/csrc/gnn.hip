@@ -113,6 +113,9 @@ struct GnnLayer {
     // are x = (v2c w_in + b_in) + F, formed where a row is read (custom_combine_kernel's exact
     // float sequence) instead of being written back between the layers
     const float *hv2c = nullptr;  // (B, E)
+    // training backward (gnn_project_groups): the projection kernel also writes the group means
+    // it projects, (B, Gv, H) / (B, Gc, H)
+    float *gsave_v = nullptr, *gsave_c = nullptr;
 };
 __device__ __forceinline__ float4 hyb_x(float4 f, float v, float4 w, float4 c) {
     return make_float4((v * w.x + c.x) + f.x, (v * w.y + c.y) + f.y, (v * w.z + c.z) + f.z, (v * w.w + c.w) + f.w);
@@ -572,8 +575,11 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         for (int p = 0; p < 8; ++p) {
             const int slot = 4 * p + r4, g = T.grp[32 * t + slot];
             const float inv = g >= 0 ? (md.x ? P.inv_c : P.inv_v)[g] : 0.0f;
-            *reinterpret_cast<float4 *>(gm + slot * kPS + c4) =
-                make_float4(acc[p].x * inv, acc[p].y * inv, acc[p].z * inv, acc[p].w * inv);
+            const float4 mean = make_float4(acc[p].x * inv, acc[p].y * inv, acc[p].z * inv, acc[p].w * inv);
+            *reinterpret_cast<float4 *>(gm + slot * kPS + c4) = mean;
+            if (P.gsave_v && g >= 0)
+                *reinterpret_cast<float4 *>((md.x ? P.gsave_c + ((int64_t)b * P.Gc + g) * 64
+                                                  : P.gsave_v + ((int64_t)b * P.Gv + g) * 64) + c4) = mean;
         }
         __builtin_amdgcn_wave_barrier();
         // B operand: lane (j, half) <- group j's units 8 q + 4 half + i (q < 8)
@@ -1463,6 +1469,61 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         return rc;
     }
     if (int rc = gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, nullptr, d_probs, s)) return rc;
+    return LDPC_OK;
+}
+
+int ldpc::gnn_project_groups(const ldpc_gnn_plan *p, int types, const float *d_weights, int layer, const float *d_x,
+                             const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                             int64_t B, float *d_pv, float *d_pc, float *d_gv, float *d_gc, hipStream_t s) {
+    constexpr int H = kMfmaH;
+    if (p->weighted || p->n_ptiles <= 0) return fail(LDPC_EUNSUPPORTED, "group projection needs a group plan");
+    if (!g_num_cus) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    GnnLayer L{};
+    L.x_in = d_x;
+    L.llr = d_llr;
+    L.msg_var = d_msg_var;
+    L.w_in = d_weights;
+    L.b_in = d_weights + H;
+    L.N = N;
+    L.T = types;
+    L.msg_type = d_msg_type;
+    L.vgroup = p->vgroup; L.cgroup = p->cgroup;
+    L.vg_ptr = p->vg_ptr; L.vg_mem = p->vg_mem; L.cg_ptr = p->cg_ptr; L.cg_mem = p->cg_mem;
+    L.inv_v = p->inv_v; L.inv_c = p->inv_c;
+    L.Gv = p->Gv; L.Gc = p->Gc;
+    L.E = p->E; L.B = B;
+    L.Mv = d_pv; L.Mc = d_pc;
+    L.gsave_v = d_gv; L.gsave_c = d_gc;
+    L.vside = 1;
+    const float *lw = d_weights + 2 * H + (int64_t)layer * layer_floats(H, types);
+    L.emb = lw;
+    L.w1v = L.emb + (int64_t)types * H;
+    L.b1v = L.w1v + 2LL * H * H;
+    L.w2v = L.b1v + H;
+    L.b2v = L.w2v + (int64_t)H * H;
+    L.w1c = L.b2v + H;
+    L.b1c = L.w1c + 2LL * H * H;
+    L.w2c = L.b1c + H;
+    const int proj_nt = LDPC_PROJ_NT == 768 && proj_lds_bytes(types, 12) <= 160 * 1024 ? 768 : 256;
+    const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64);
+    if (proj_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
+    const void *proj_fn = proj_nt == 768 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<768>)
+                                         : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
+    LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
+    const int per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
+    const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, 0};
+    const int64_t ptiles = B * (int64_t)p->n_ptiles;
+    const int pw = proj_nt / 64;
+    const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * per_cu);
+    if (proj_nt == 768)
+        hipLaunchKernelGGL(gnn_group_proj_kernel<768>, dim3(pgrid), dim3(768), proj_lds, s, L, T);
+    else
+        hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds, s, L, T);
+    LDPC_CHECK_LAUNCH("gnn_group_proj_kernel (training backward)");
     return LDPC_OK;
 }
 

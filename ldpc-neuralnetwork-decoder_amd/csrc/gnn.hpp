@@ -64,6 +64,13 @@ int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, 
                      const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
                      float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s);
 
+// Layer `layer`'s projected group rows W1_s,right g + b1_s (d_pv / d_pc, (B, G, 64)) and, when
+// d_gv is set, the group means g themselves (d_gv / d_gc) of c = x + emb (x = d_x, or the LLR
+// embedding when d_x is null): the fp32 forward's projection kernel, for the training backward.
+int gnn_project_groups(const ldpc_gnn_plan *p, int types, const float *d_weights, int layer, const float *d_x,
+                       const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
+                       float *d_pv, float *d_pc, float *d_gv, float *d_gc, hipStream_t s);
+
 // The per-device side stream and the calling thread's fork/join events the forwards split their
 // frames over (thread-safe: see gnn.hip).
 int gnn_side_stream(hipStream_t *side, hipEvent_t *fork, hipEvent_t *join);

@@ -339,7 +339,12 @@ struct F64 {
 };
 __device__ __forceinline__ int crow_t(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
-template <int NT>
+// PJ (projected groups, the default): Mv / Mc hold the side's projected group rows W1_right g + b1
+// (gnn_project_groups), so GEMM1 runs over c alone (lane half h carries c[32 h + kk]) from that
+// row, and GEMM3' computes only the c part of dz: the group part's mean over a group is
+// W1_right^T (mean of dh over the group), formed per group afterwards (train_group_back_kernel).
+// Per side 64 + 64 + 64 MFMAs instead of 64 + 128 + 128.
+template <int NT, bool PJ = false>
 __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd_mfma_kernel(MlpT A) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr int H = 64;
@@ -373,6 +378,35 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
         // half 1 lanes the side's group mean
         auto load_in = [&](int side) {
             F64 in;
+            if (PJ) {  // c[32 half + kk], kk < 32
+                const float4 *e = reinterpret_cast<const float4 *>(A.emb + A.msg_type[m] * H + 32 * half);
+                if (A.x) {
+                    const float4 *xr = reinterpret_cast<const float4 *>(A.x + rr * H + 32 * half);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float4 v = xr[q], ev = e[q];
+                        in[4 * q] = v.x + ev.x; in[4 * q + 1] = v.y + ev.y;
+                        in[4 * q + 2] = v.z + ev.z; in[4 * q + 3] = v.w + ev.w;
+                    }
+                } else {
+                    const float l = A.llr[b * A.N + A.msg_var[m]];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float4 ev = e[q];
+                        const float4 w = reinterpret_cast<const float4 *>(A.w_in + 32 * half)[q];
+                        const float4 bi = reinterpret_cast<const float4 *>(A.b_in + 32 * half)[q];
+                        in[4 * q] = (w.x * l + bi.x) + ev.x; in[4 * q + 1] = (w.y * l + bi.y) + ev.y;
+                        in[4 * q + 2] = (w.z * l + bi.z) + ev.z; in[4 * q + 3] = (w.w * l + bi.w) + ev.w;
+                    }
+                }
+                if (side == 0 && ok) {
+                    float4 *cb = reinterpret_cast<float4 *>(A.cbuf + row * H + 32 * half);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        cb[q] = make_float4(in[4 * q], in[4 * q + 1], in[4 * q + 2], in[4 * q + 3]);
+                }
+                return in;
+            }
             if (half == 0) {
                 const float4 *e = reinterpret_cast<const float4 *>(A.emb + A.msg_type[m] * H);
                 if (A.x) {
@@ -437,7 +471,24 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
             }
             // GEMM1: u[32 rt + i][msg]; A = W1[32 rt + j][64 half + kk]
             f32x16 u0 = {}, u1 = {};
-            {
+            if constexpr (PJ) {  // from the projected row (b1 included); A = W1[32 rt + j][32 half + kk]
+                const float *pr = side == 0 ? A.Mv + (b * A.Gv + A.vgroup[m]) * H : A.Mc + (b * A.Gc + A.cgroup[m]) * H;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 p0 = *reinterpret_cast<const float4 *>(pr + 8 * q + 4 * half);
+                    const float4 p1 = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q + 4 * half);
+                    u0[4 * q] = p0.x; u0[4 * q + 1] = p0.y; u0[4 * q + 2] = p0.z; u0[4 * q + 3] = p0.w;
+                    u1[4 * q] = p1.x; u1[4 * q + 1] = p1.y; u1[4 * q + 2] = p1.z; u1[4 * q + 3] = p1.w;
+                }
+                const F64 in = load_in(side);
+                const int lp = j * kS1 + 32 * half;
+#pragma unroll
+                for (int kk = 0; kk < 32; ++kk) {
+                    const float *wr = W1 + lp + kk;
+                    u0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[0], in[kk], u0, 0, 0, 0);
+                    u1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32 * kS1], in[kk], u1, 0, 0, 0);
+                }
+            } else {
                 const F64 in = load_in(side);
 #pragma unroll
                 for (int kk = 0; kk < 64; ++kk) {
@@ -449,7 +500,8 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
             // bias, relu, mask: lane holds units 32 rt + crow(r, half)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float a0 = u0[r] + bs[crow_t(r, half)], a1 = u1[r] + bs[32 + crow_t(r, half)];
+                const float a0 = PJ ? u0[r] : u0[r] + bs[crow_t(r, half)];
+                const float a1 = PJ ? u1[r] : u1[r] + bs[32 + crow_t(r, half)];
                 u0[r] = fmaxf(a0, 0.0f);
                 u1[r] = fmaxf(a1, 0.0f);
                 d0[r] = a0 > 0.0f ? d0[r] : 0.0f;
@@ -471,7 +523,7 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
             }
             // GEMM3': dz[k][msg] = sum_u W1[u][k] dh[u]; A = W1[32 rt + crow(r, half)][32 kt + j]
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt) {
+            for (int kt = 0; kt < (PJ ? 2 : 4); ++kt) {
                 f32x16 acc = kt == 0 ? dco0 : kt == 1 ? dco1 : f32x16{};
 #pragma unroll
                 for (int rt = 0; rt < 2; ++rt)
@@ -502,6 +554,51 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
                     *reinterpret_cast<float4 *>(co + 32 * rt + 8 * q + 4 * half) =
                         make_float4(cc[4 * q], cc[4 * q + 1], cc[4 * q + 2], cc[4 * q + 3]);
                 }
+        }
+    }
+}
+
+// PJ backward: the group part of dz averaged over a group, formed per group --
+// Mda[b][g][k] = inv[g] sum_u W1v[u][64 + k] S_v[b][g][u] with S the group sums of dh (Mdb: the
+// check side with W1c).  One wave per 4 rows of a side, lanes = k, W1_right in LDS.
+__global__ __launch_bounds__(256) void train_group_back_kernel(const float *__restrict__ Sv, const float *__restrict__ Sc,
+                                                               const float *__restrict__ w1v, const float *__restrict__ w1c,
+                                                               const float *__restrict__ inv_v,
+                                                               const float *__restrict__ inv_c, int Gv, int Gc, int64_t B,
+                                                               float *__restrict__ Mda, float *__restrict__ Mdb) {
+    __shared__ float W[2 * 64 * 64];
+    for (int i = threadIdx.x; i < 2 * 4096; i += 256) {
+        const int side = i >> 12, u = (i >> 6) & 63, k = i & 63;
+        W[i] = (side ? w1c : w1v)[u * 128 + 64 + k];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    for (int side = 0; side < 2; ++side) {
+        const int G = side ? Gc : Gv;
+        const int64_t rows = B * G, quads = (rows + 3) / 4;
+        const float *S = side ? Sc : Sv, *inv = side ? inv_c : inv_v;
+        float *out = side ? Mdb : Mda;
+        const float *Ws = W + side * 4096 + lane;
+        for (int64_t q = wave; q < quads; q += nw) {
+            int sv[4];
+            float acc[4] = {};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = 4 * q + r;
+                sv[r] = __float_as_int(row < rows ? S[row * 64 + lane] : 0.0f);
+            }
+#pragma unroll 8
+            for (int u = 0; u < 64; ++u) {
+                const float w = Ws[u * 64];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[r] = fmaf(w, __int_as_float(__builtin_amdgcn_readlane(sv[r], u)), acc[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = 4 * q + r;
+                if (row < rows) out[row * 64 + lane] = acc[r] * inv[row % G];
+            }
         }
     }
 }
@@ -553,6 +650,10 @@ struct OuterT {
     int H, J, Gn;
     int ld = 0, col0 = 0;  // out[i * ld + col0 + j] (ld 0 = J): one half of a [H][2H] gradient
     int64_t E, R;
+    // MFMA kernel, two gradients of one A (J = 2H): Z columns j >= H come from zsrc2 and go to
+    // out2 [H][H] (+ bias2, the same row sums as bias)
+    const float *zsrc2 = nullptr;
+    float *out2 = nullptr, *bias2 = nullptr;
 };
 constexpr int kRB = 16;  // rows staged per step
 
@@ -631,6 +732,7 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     auto zval = [&](int64_t r, int64_t b, int64_t m, int j) -> float {
         if (j >= J) return 0.0f;
         if (j < H) return P.zsrc[r * H + j];
+        if (P.zsrc2) return P.zsrc2[r * H + (j - H)];
         return P.G[(b * P.Gn + P.grp[m]) * H + (j - H)];
     };
     // (frame, message) of row r0 + k, stepped along with r0 (no 64-bit division per row)
@@ -688,9 +790,13 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     __syncthreads();
     for (int e = threadIdx.x; e < NIT * 32 * NJT * 32; e += 256) {
         const int i = e / (NJT * 32), j = e - i * (NJT * 32);
-        if (i < H && j < J) atomicAdd(&P.out[i * (P.ld ? P.ld : J) + P.col0 + j], red[e]);
+        if (i < H && j < J) {
+            if (P.out2 && j >= H) atomicAdd(&P.out2[i * H + (j - H)], red[e]);
+            else atomicAdd(&P.out[i * (P.ld ? P.ld : J) + P.col0 + j], red[e]);
+        }
     }
     if (P.bias && threadIdx.x < H) atomicAdd(&P.bias[threadIdx.x], bred[threadIdx.x]);
+    if (P.bias2 && threadIdx.x < H) atomicAdd(&P.bias2[threadIdx.x], bred[threadIdx.x]);
 }
 
 int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
@@ -811,6 +917,13 @@ TrainWs carve_train(const ldpc_gnn_plan *p, int H, int N, int64_t B, void *base)
 
 int g_cus_t = 0;
 
+// LDPC_GNN_TRAIN_PROJ=0: the backward recomputes group means and runs GEMM1 / GEMM3' over
+// [c; g] per message (A/B); default: projected group rows (train_mlp_bwd_mfma_kernel PJ)
+int bwd_proj() {
+    const char *e = std::getenv("LDPC_GNN_TRAIN_PROJ");  // read per call (tests toggle it)
+    return e ? std::atoi(e) : 1;
+}
+
 int bwd_mfma() {
     static const int v = [] {
         const char *e = std::getenv("LDPC_GNN_TRAIN_MFMA");
@@ -878,6 +991,14 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<256>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
+    // projected groups (see train_mlp_bwd_mfma_kernel): H = 64 on MFMA with the plan's projection tiles
+    const bool pj = H == 64 && bwd_mfma() && bwd_proj() && p->n_ptiles > 0;
+    if (pj) {
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<512, true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<256, true>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
+    }
     auto blocks = [](int64_t work, int per) { return dim3((unsigned)((work + per - 1) / per)); };
     const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * 4);
 
@@ -908,15 +1029,22 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         float *Gw[11];
         t_layer(d_grad_weights, H, T, l, Gw);
         const float *x = l > 0 ? d_saved + (int64_t)(l - 1) * n : nullptr;
-        // group means of c (forward recompute)
-        GmT g{};
-        g.src = x; g.emb = W[0]; g.llr = d_llr; g.w_in = d_weights; g.b_in = d_weights + H;
-        g.msg_type = d_msg_type; g.msg_var = d_msg_var;
-        g.src_mode = x ? 1 : 2; g.H = H; g.N = N; g.E = E; g.B = B;
-        g.ptr = p->vg_ptr; g.mem = p->vg_mem; g.inv = p->inv_v; g.G = p->Gv; g.dst = w.Mv;
-        if (int rc = launch_group_mean(g, s)) return rc;
-        g.ptr = p->cg_ptr; g.mem = p->cg_mem; g.inv = p->inv_c; g.G = p->Gc; g.dst = w.Mc;
-        if (int rc = launch_group_mean(g, s)) return rc;
+        // PJ: the group means of c go to da / db (free in this mode: no per-message group part)
+        float *Gsv = w.da, *Gsc = w.db;
+        if (pj) {  // forward recompute: projected rows (Mv / Mc) and the group means (Gsv / Gsc)
+            if (int rc = gnn_project_groups(p, T, d_weights, l, x, d_msg_type, d_msg_var, d_llr, N, B, w.Mv, w.Mc,
+                                            Gsv, Gsc, s))
+                return rc;
+        } else {  // group means of c (forward recompute)
+            GmT g{};
+            g.src = x; g.emb = W[0]; g.llr = d_llr; g.w_in = d_weights; g.b_in = d_weights + H;
+            g.msg_type = d_msg_type; g.msg_var = d_msg_var;
+            g.src_mode = x ? 1 : 2; g.H = H; g.N = N; g.E = E; g.B = B;
+            g.ptr = p->vg_ptr; g.mem = p->vg_mem; g.inv = p->inv_v; g.G = p->Gv; g.dst = w.Mv;
+            if (int rc = launch_group_mean(g, s)) return rc;
+            g.ptr = p->cg_ptr; g.mem = p->cg_mem; g.inv = p->inv_c; g.G = p->Gc; g.dst = w.Mc;
+            if (int rc = launch_group_mean(g, s)) return rc;
+        }
         // MLP backward
         MlpT m{};
         m.x = x; m.llr = d_llr; m.w_in = d_weights; m.b_in = d_weights + H;
@@ -929,7 +1057,11 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         if (H == 64 && bwd_mfma()) {  // LDPC_GNN_TRAIN_MFMA=0 selects the VALU kernel (A/B runs)
             const int nt = bwd_mfma() == 2 ? 256 : 512;  // =2: 256 threads, 1 wave per SIMD
             const unsigned grid = (unsigned)std::min<int64_t>((R + 32 * (nt / 64) - 1) / (32 * (nt / 64)), (int64_t)g_cus_t);
-            if (nt == 256)
+            if (pj && nt == 256)
+                hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<256, true>), dim3(grid), dim3(256), mlp_bwd_mfma_lds(), s, m);
+            else if (pj)
+                hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<512, true>), dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);
+            else if (nt == 256)
                 hipLaunchKernelGGL(train_mlp_bwd_mfma_kernel<256>, dim3(grid), dim3(256), mlp_bwd_mfma_lds(), s, m);
             else
                 hipLaunchKernelGGL(train_mlp_bwd_mfma_kernel<512>, dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);
@@ -939,13 +1071,30 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
             hipLaunchKernelGGL(train_mlp_bwd_kernel, dim3(mgrid), dim3(256), lds_mlp, s, m);
             LDPC_CHECK_LAUNCH("train_mlp_bwd_kernel");
         }
-        // group means of the aggregated-input gradients (the mean operator is symmetric)
-        GmT d{};
-        d.src_mode = 0; d.H = H; d.N = N; d.E = E; d.B = B;
-        d.src = w.da; d.ptr = p->vg_ptr; d.mem = p->vg_mem; d.inv = p->inv_v; d.G = p->Gv; d.dst = w.Mda;
-        if (int rc = launch_group_mean(d, s)) return rc;
-        d.src = w.db; d.ptr = p->cg_ptr; d.mem = p->cg_mem; d.inv = p->inv_c; d.G = p->Gc; d.dst = w.Mdb;
-        if (int rc = launch_group_mean(d, s)) return rc;
+        if (pj) {
+            // group sums of dh (into Mv / Mc: the projected rows are consumed), then the group part of
+            // dz per group: Mda = W1v_right^T (sum dh) / |group|, Mdb likewise
+            for (int side = 0; side < 2; ++side) {
+                GmT gs{};
+                gs.src = side ? w.dhc : w.dhv; gs.src_mode = 0; gs.sum_only = 1; gs.H = H; gs.N = N; gs.E = E; gs.B = B;
+                gs.ptr = side ? p->cg_ptr : p->vg_ptr; gs.mem = side ? p->cg_mem : p->vg_mem;
+                gs.inv = side ? p->inv_c : p->inv_v; gs.G = side ? p->Gc : p->Gv; gs.dst = side ? w.Mc : w.Mv;
+                if (int rc = launch_group_mean(gs, s)) return rc;
+            }
+            const int64_t quads = (B * p->Gv + 3) / 4 + (B * p->Gc + 3) / 4;
+            const unsigned ggrid = (unsigned)std::min<int64_t>((quads + 3) / 4, (int64_t)g_cus_t * 8);
+            hipLaunchKernelGGL(train_group_back_kernel, dim3(ggrid), dim3(256), 0, s, w.Mv, w.Mc, W[1], W[5], p->inv_v,
+                               p->inv_c, p->Gv, p->Gc, B, w.Mda, w.Mdb);
+            LDPC_CHECK_LAUNCH("train_group_back_kernel");
+        } else {
+            // group means of the aggregated-input gradients (the mean operator is symmetric)
+            GmT d{};
+            d.src_mode = 0; d.H = H; d.N = N; d.E = E; d.B = B;
+            d.src = w.da; d.ptr = p->vg_ptr; d.mem = p->vg_mem; d.inv = p->inv_v; d.G = p->Gv; d.dst = w.Mda;
+            if (int rc = launch_group_mean(d, s)) return rc;
+            d.src = w.db; d.ptr = p->cg_ptr; d.mem = p->cg_mem; d.inv = p->inv_c; d.G = p->Gc; d.dst = w.Mdb;
+            if (int rc = launch_group_mean(d, s)) return rc;
+        }
         if (H % 4 == 0)
             hipLaunchKernelGGL(train_combine4_kernel, blocks(n / 4, 256), dim3(256), 0, s,
                                reinterpret_cast<float4 *>(w.dco), reinterpret_cast<const float4 *>(w.Mda),
@@ -960,25 +1109,34 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         OuterT o{};
         o.H = H; o.E = E; o.R = R;
         o.A = w.dX; o.zsrc = w.hv; o.J = H; o.out = Gw[3]; o.bias = Gw[4];
-        if (int rc = launch_outer(o, red_grid, s)) return rc;
-        o.zsrc = w.hc; o.out = Gw[7]; o.bias = Gw[8];
-        if (int rc = launch_outer(o, red_grid, s)) return rc;
+        if (H == 64) {  // dW2v and dW2c in one pass over dX
+            o.J = 2 * H; o.ld = H; o.zsrc2 = w.hc; o.out2 = Gw[7]; o.bias2 = Gw[8];
+            if (int rc = launch_outer(o, red_grid, s)) return rc;
+        } else {
+            if (int rc = launch_outer(o, red_grid, s)) return rc;
+            o.zsrc = w.hc; o.out = Gw[7]; o.bias = Gw[8];
+            if (int rc = launch_outer(o, red_grid, s)) return rc;
+        }
         // dW1_s = sum_m dh_s[m] (x) [c_m; g_s(group(m))]: the c half row by row; the group half as
         // sum_groups (sum_{m in group} dh_s[m]) (x) g_s(group) -- contiguous group rows instead of
         // a gathered group row per message (Mda / Mdb are free again after the combine step)
         for (int side = 0; side < 2; ++side) {
-            const float *dh = side ? w.dhc : w.dhv, *Gs = side ? w.Mc : w.Mv;
-            float *dhsum = side ? w.Mdb : w.Mda, *gw = side ? Gw[5] : Gw[1], *gb = side ? Gw[6] : Gw[2];
+            // PJ: the group means are in Gsv / Gsc and the group sums of dh already in Mv / Mc
+            const float *dh = side ? w.dhc : w.dhv, *Gs = pj ? (side ? Gsc : Gsv) : side ? w.Mc : w.Mv;
+            float *dhsum = pj ? (side ? w.Mc : w.Mv) : side ? w.Mdb : w.Mda;
+            float *gw = side ? Gw[5] : Gw[1], *gb = side ? Gw[6] : Gw[2];
             const int Gn = side ? p->Gc : p->Gv;
             OuterT c{};
             c.H = H; c.E = E; c.R = R; c.A = dh; c.zsrc = w.cbuf; c.J = H; c.ld = 2 * H; c.col0 = 0;
             c.out = gw; c.bias = gb;
             if (int rc = launch_outer(c, red_grid, s)) return rc;
-            GmT gs{};
-            gs.src = dh; gs.src_mode = 0; gs.sum_only = 1; gs.H = H; gs.N = N; gs.E = E; gs.B = B;
-            gs.ptr = side ? p->cg_ptr : p->vg_ptr; gs.mem = side ? p->cg_mem : p->vg_mem;
-            gs.inv = side ? p->inv_c : p->inv_v; gs.G = Gn; gs.dst = dhsum;
-            if (int rc = launch_group_mean(gs, s)) return rc;
+            if (!pj) {
+                GmT gs{};
+                gs.src = dh; gs.src_mode = 0; gs.sum_only = 1; gs.H = H; gs.N = N; gs.E = E; gs.B = B;
+                gs.ptr = side ? p->cg_ptr : p->vg_ptr; gs.mem = side ? p->cg_mem : p->vg_mem;
+                gs.inv = side ? p->inv_c : p->inv_v; gs.G = Gn; gs.dst = dhsum;
+                if (int rc = launch_group_mean(gs, s)) return rc;
+            }
             OuterT g{};
             g.H = H; g.E = (int64_t)Gn; g.R = B * Gn; g.A = dhsum; g.zsrc = Gs; g.J = H; g.ld = 2 * H; g.col0 = H;
             g.out = gw; g.bias = nullptr;
