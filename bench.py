@@ -104,6 +104,13 @@ def valu_roofline(B, n, kern_ms, traffic, pmc, pmc_path, alg_bytes):
     return achieved, notes
 
 
+# mangled-name prefix of the kernel a workload's PMC summary counts (flood_fixed_kernel<G, ALGO, ES>)
+PMC_KERNEL_SYMBOL = {
+    "minsum-z32": "_ZN4ldpc18flood_fixed_kernelINS_5fixed7BG2_Z32ELi0ELi0E",
+    "bp-z32": "_ZN4ldpc18flood_fixed_kernelINS_5fixed7BG2_Z32ELi1ELi0E",
+}
+
+
 def sha256_file(path):
     import hashlib
     h = hashlib.sha256()
@@ -561,7 +568,16 @@ def main():
             # a PMC summary describes the library build it profiled (tools/gpu_profile.sh stamps the
             # sha256 of the .so it loaded): from any other build its counts are not this run's
             lib_sha = sha256_file(N.LIB_PATH)
-            if tjd.get("lib_sha256") != lib_sha:
+            # ... or of the gfx950 code object that holds the benched kernel (tools/code_object_sha.py):
+            # a rebuild after a change in another translation unit leaves that one untouched
+            needle = PMC_KERNEL_SYMBOL.get(a.workload)
+            code_sha = None
+            if needle:
+                sys.path.insert(0, os.path.join(ROOT, "tools"))
+                from code_object_sha import kernel_code_sha
+                code_sha = kernel_code_sha(N.LIB_PATH, needle)
+            if tjd.get("lib_sha256") != lib_sha and (code_sha is None
+                                                     or code_sha not in tjd.get("code_objects_sha256", [])):
                 pmc_stale = {"pmc_source": os.path.relpath(tj, ROOT), "pmc_lib_sha256": tjd.get("lib_sha256"),
                              "loaded_lib_sha256": lib_sha,
                              "note": "the PMC summary was measured on another libldpc_amd.so build: its "

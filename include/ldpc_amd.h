@@ -216,6 +216,25 @@ int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                       const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
                       int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
                       float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream);
+/* Deep supervision (training extension, no reference counterpart; it is what makes the cfg5
+ * per-frame early termination fire: the syndrome check decodes every layer's output through the
+ * last layer's output_projection, so a model trained on the last layer's loss alone never yields a
+ * codeword before the end).
+ * ldpc_gnn_layer_probs: probs of every layer l < L - 1 through the LAST layer's output_projection,
+ *   p_l[b][v] = sigmoid(llr + sum_{m -> v} (wo_L . x_{l+1}[b][m] + bo_L)) from d_saved, into
+ *   d_layer_probs (L - 1, B, N); the output stage's own variable sums (ascending messages).
+ *   Workspace: ldpc_gnn_train_workspace_size(...) bytes suffice.
+ * ldpc_gnn_backward_ds: ldpc_gnn_backward plus dLoss/d(layer probs) (L - 1, B, N): each layer's
+ *   head gradient is added to the feature gradient that arrives from above and to dwo_L / dbo_L.
+ *   Both layer pointers null = ldpc_gnn_backward. */
+int ldpc_gnn_layer_probs(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                         const int32_t *d_msg_var, const float *d_llr, int N, int64_t B, const float *d_saved,
+                         float *d_layer_probs, void *d_work, int64_t work_bytes, void *stream);
+int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                         const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                         int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
+                         const float *d_layer_probs, const float *d_grad_layer_probs, float *d_grad_weights,
+                         void *d_work, int64_t work_bytes, void *stream);
 
 /* ---- index-gather neural-BP layers (models/layers.py) ------------------
  * d_idx is the reference's (n_out, K) index tensor transposed to (K, n_out) int32, -1 = padding

@@ -70,16 +70,34 @@ __global__ void train_head_kernel(const float *__restrict__ p, const float *__re
     if (i < n) dz[i] = g[i] * (p[i] * (1.0f - p[i]));  // d sigmoid
 }
 
-// dX_L[r][u] = dz[b][var(m)] * wo[u]
+// dX_L[r][u] = dz[b][var(m)] * wo[u]   (acc: dX[r][u] += that -- a deep-supervision head on an
+// intermediate layer's output, added to the gradient that arrives from the layers above)
 __global__ void train_dx_last_kernel(const float *__restrict__ dz, const int32_t *__restrict__ msg_var,
                                      const float *__restrict__ wo, int H, int64_t E, int N, int64_t n,
-                                     float *__restrict__ dX) {
+                                     float *__restrict__ dX, int acc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t r = i / H;
     const int u = (int)(i - r * H);
     const int64_t b = r / E, m = r - b * E;
-    dX[i] = dz[b * N + msg_var[m]] * wo[u];
+    const float d = dz[b * N + msg_var[m]] * wo[u];
+    dX[i] = acc ? dX[i] + d : d;
+}
+
+// Deep-supervision head (training only, no reference counterpart): out_m = wo . x_m + bo for every
+// message row of one layer's saved output features (16 lanes per row, H <= 64); the variable sums
+// and the sigmoid are the decoder's own output stage (gnn_output)
+__global__ __launch_bounds__(256) void train_msg_head_kernel(const float *__restrict__ x, int H, int64_t R,
+                                                             const float *__restrict__ wo, const float *__restrict__ bo,
+                                                             float *__restrict__ msg_out) {
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int q = threadIdx.x & 15;
+    if (r >= R) return;  // whole 16-lane groups leave together
+    const float *xr = x + r * H;
+    float part = 0.0f;
+    for (int u = q; u < H; u += 16) part = fmaf(xr[u], wo[u], part);
+    for (int off = 8; off > 0; off >>= 1) part += __shfl_xor(part, off, 16);
+    if (q == 0) msg_out[r] = part + bo[0];
 }
 
 // ------------------------------------------------------------------------ group means
@@ -960,10 +978,12 @@ extern "C" int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int ty
                             d_work, work_bytes, static_cast<hipStream_t>(stream));
 }
 
-extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
-                                 const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
-                                 int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
-                                 float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream) {
+extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                                    const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                                    const float *d_llr, int N, int64_t B, const float *d_probs,
+                                    const float *d_grad_probs, const float *d_saved, const float *d_layer_probs,
+                                    const float *d_grad_layer_probs, float *d_grad_weights, void *d_work,
+                                    int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     const int H = hidden, T = types, L = layers;
@@ -971,6 +991,9 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 64)");
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_grad_probs || !d_saved || !d_grad_weights)
         return fail(LDPC_EINVAL, "NULL tensor");
+    if ((d_layer_probs == nullptr) != (d_grad_layer_probs == nullptr))
+        return fail(LDPC_EINVAL, "d_layer_probs and d_grad_layer_probs go together");
+    const bool ds = d_layer_probs != nullptr && L > 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t wfloats = 2LL * H + (int64_t)L * tl_floats(H, T);
     LDPC_HIP(hipMemsetAsync(d_grad_weights, 0, (size_t)wfloats * 4, s));
@@ -1010,7 +1033,7 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
     hipLaunchKernelGGL(train_head_kernel, blocks(B * N, 256), dim3(256), 0, s, d_probs, d_grad_probs, B * N, w.dz);
     LDPC_CHECK_LAUNCH("train_head_kernel");
     hipLaunchKernelGGL(train_dx_last_kernel, blocks(n, 256), dim3(256), 0, s, w.dz, d_msg_var, WL[9], H, E, N, n,
-                       w.dX);
+                       w.dX, 0);
     LDPC_CHECK_LAUNCH("train_dx_last_kernel");
     {
         VecT v{};
@@ -1028,6 +1051,19 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
         t_layer(d_weights, H, T, l, W);
         float *Gw[11];
         t_layer(d_grad_weights, H, T, l, Gw);
+        if (ds && l < L - 1) {  // deep supervision: layer l's output through the last layer's head
+            const float *pl = d_layer_probs + (int64_t)l * B * N, *gl = d_grad_layer_probs + (int64_t)l * B * N;
+            hipLaunchKernelGGL(train_head_kernel, blocks(B * N, 256), dim3(256), 0, s, pl, gl, B * N, w.dz);
+            LDPC_CHECK_LAUNCH("train_head_kernel");
+            hipLaunchKernelGGL(train_dx_last_kernel, blocks(n, 256), dim3(256), 0, s, w.dz, d_msg_var, WL[9], H, E, N,
+                               n, w.dX, 1);
+            LDPC_CHECK_LAUNCH("train_dx_last_kernel");
+            VecT v{};
+            v.src = d_saved + (int64_t)l * n;
+            v.dz = w.dz; v.msg_type = d_msg_type; v.msg_var = d_msg_var; v.g0 = GL[9]; v.g1 = GL[10];
+            v.H = H; v.T = T; v.N = N; v.mode = 2; v.E = E; v.R = R;
+            if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
+        }
         const float *x = l > 0 ? d_saved + (int64_t)(l - 1) * n : nullptr;
         // PJ: the group means of c go to da / db (free in this mode: no per-message group part)
         float *Gsv = w.da, *Gsc = w.db;
@@ -1153,6 +1189,41 @@ extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, 
             if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
         }
         std::swap(w.dX, w.dXp);
+    }
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                                 const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                                 int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
+                                 float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream) {
+    return ldpc_gnn_backward_ds(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
+                                d_grad_probs, d_saved, nullptr, nullptr, d_grad_weights, d_work, work_bytes, stream);
+}
+
+extern "C" int ldpc_gnn_layer_probs(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                                    const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
+                                    const float *d_saved, float *d_layer_probs, void *d_work, int64_t work_bytes,
+                                    void *stream) {
+    if (!p) return fail(LDPC_EINVAL, "plan is NULL");
+    const int H = hidden, T = types, L = layers;
+    if (H <= 0 || H > kMaxH || T <= 0 || L <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
+    if (L < 2 || B == 0) return LDPC_OK;
+    if (!d_weights || !d_msg_var || !d_llr || !d_saved || !d_layer_probs) return fail(LDPC_EINVAL, "NULL tensor");
+    const int64_t E = p->E, R = B * E, mo = (R + 63) / 64 * 64;
+    const int64_t need = (mo + gnn_csr_ints(E, N)) * 4;
+    if (!d_work || work_bytes < need) return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    float *msg_out = static_cast<float *>(d_work);
+    int32_t *csr = reinterpret_cast<int32_t *>(msg_out + mo);
+    if (int rc = gnn_build_var_csr(d_msg_var, E, N, csr, s)) return rc;
+    const float *WL[11];
+    t_layer(d_weights, H, T, L - 1, WL);
+    for (int l = 0; l < L - 1; ++l) {
+        hipLaunchKernelGGL(train_msg_head_kernel, dim3((unsigned)((R * 16 + 255) / 256)), dim3(256), 0, s,
+                           d_saved + (int64_t)l * R * H, H, R, WL[9], WL[10], msg_out);
+        LDPC_CHECK_LAUNCH("train_msg_head_kernel");
+        if (int rc = gnn_output(msg_out, csr, d_llr, E, N, B, nullptr, d_layer_probs + (int64_t)l * B * N, s)) return rc;
     }
     return LDPC_OK;
 }

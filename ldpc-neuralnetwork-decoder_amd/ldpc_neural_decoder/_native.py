@@ -71,6 +71,10 @@ SIGNATURES = {
                                               _P]),
     "ldpc_gnn_backward": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                          ctypes.c_int, _I64, _P, _P, _P, _P, _P, _I64, _P]),
+    "ldpc_gnn_layer_probs": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P,
+                                            ctypes.c_int, _I64, _P, _P, _P, _I64, _P]),
+    "ldpc_gnn_backward_ds": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
+                                            ctypes.c_int, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
 }
 
 _lib = None

@@ -308,7 +308,7 @@ class MessageGNNDecoder(nn.Module):
             if plan.weighted:
                 raise NotImplementedError("training through a general (non-clique) adjacency is not supported; "
                                           "use the TannerToMessageGraph adjacencies")
-            probs = _NativeGnnTrain.apply(self, llr, io_map, types, plan, *params)
+            probs, _ = _NativeGnnTrain.apply(self, llr, io_map, types, plan, False, *params)
         else:
             with torch.no_grad():
                 probs = self.native_forward(llr, io_map, types, vg, cg)
@@ -318,6 +318,30 @@ class MessageGNNDecoder(nn.Module):
             loss = F.binary_cross_entropy(probs, ground_truth.to(probs.device).float())
             return probs, loss
         return probs
+
+    def forward_all_layers(self, input_llr, message_to_var_mapping, message_types=None,
+                           var_to_check_adjacency=None, check_to_var_adjacency=None):
+        """Training extension (no reference counterpart): the soft decisions after EVERY layer,
+        (L, B, N), each layer's output features through the last layer's output_projection and the
+        decoder's output stage; the last entry is forward()'s probs.  A loss on all of them (deep
+        supervision) trains the intermediate layers to decode, which is what lets the bf16 path's
+        per-frame early termination (cfg5) stop before the last layer -- its syndrome check reads
+        exactly these decisions.  fp32, group (clique) adjacencies, with autograd through the HIP
+        backward (ldpc_gnn_backward_ds)."""
+        dev = N.device_of(input_llr)
+        E = self.num_messages
+        vg, cg = _aggregation_specs(var_to_check_adjacency, check_to_var_adjacency, E)
+        llr = input_llr.to(dev, torch.float32).contiguous()
+        io_map = _io_mapping(message_to_var_mapping, E, llr.shape[1], dev)
+        T = self.gnn_layers[0].message_type_embeddings.shape[0]
+        types = _types_for(message_types, E, T, dev)
+        plan = self._plan(vg, cg, dev)
+        if plan.weighted:
+            raise NotImplementedError("forward_all_layers needs the TannerToMessageGraph adjacencies")
+        if self.precision != "fp32":
+            raise NotImplementedError("forward_all_layers runs the fp32 training forward")
+        probs, layer_probs = _NativeGnnTrain.apply(self, llr, io_map, types, plan, True, *self._blob_params())
+        return torch.cat([layer_probs, probs.unsqueeze(0)], 0).to(input_llr.device)
 
     def decode(self, input_llr, message_to_var_mapping, message_types=None,
                var_to_check_adjacency=None, check_to_var_adjacency=None):
@@ -336,7 +360,8 @@ class _NativeGnnTrain(torch.autograd.Function):
     autograd graph through the reference's forward for loss.backward() (trainer.py:93-99)."""
 
     @staticmethod
-    def forward(ctx, dec, llr, io_map, types, plan, *params):
+    def forward(ctx, dec, llr, io_map, types, plan, all_layers, *params):
+        ctx.set_materialize_grads(False)
         dev = llr.device
         H, L = dec.hidden_dim, len(dec.gnn_layers)
         T = dec.gnn_layers[0].message_type_embeddings.shape[0]
@@ -362,23 +387,33 @@ class _NativeGnnTrain(torch.autograd.Function):
             N.check(N.lib().ldpc_gnn_forward_train(
                 plan.handle, H, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr), Nv, B,
                 N.ptr(probs), N.ptr(saved), N.ptr(ws), wsb, N.stream_ptr(dev)))
-        ctx.save_for_backward(llr, io_map, types, blob, probs, saved)
+        layer_probs = torch.empty((max(L - 1, 0) if all_layers else 0, B, Nv), dtype=torch.float32, device=dev)
+        if all_layers and B and L > 1:
+            N.check(N.lib().ldpc_gnn_layer_probs(
+                plan.handle, H, T, L, N.ptr(blob), N.ptr(io_map), N.ptr(llr), Nv, B, N.ptr(saved),
+                N.ptr(layer_probs), N.ptr(ws), wsb, N.stream_ptr(dev)))
+        ctx.save_for_backward(llr, io_map, types, blob, probs, saved, layer_probs)
         ctx.meta = (plan, H, T, L, [p.shape for p in params])
-        return probs
+        return probs, layer_probs
 
     @staticmethod
-    def backward(ctx, grad_probs):
-        llr, io_map, types, blob, probs, saved = ctx.saved_tensors
+    def backward(ctx, grad_probs, grad_layer_probs):
+        llr, io_map, types, blob, probs, saved, layer_probs = ctx.saved_tensors
         plan, H, T, L, shapes = ctx.meta
         dev = llr.device
         B, Nv = llr.shape
         grad = torch.empty_like(blob)
         wsb = N.check(N.lib().ldpc_gnn_train_workspace_size(plan.handle, H, Nv, B, L))
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-        g = grad_probs.to(dev, torch.float32).contiguous()
-        N.check(N.lib().ldpc_gnn_backward(
+        g = (grad_probs.to(dev, torch.float32).contiguous() if grad_probs is not None
+             else torch.zeros_like(probs))
+        gl = None
+        if grad_layer_probs is not None and layer_probs.numel():
+            gl = grad_layer_probs.to(dev, torch.float32).contiguous()
+        N.check(N.lib().ldpc_gnn_backward_ds(
             plan.handle, H, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr), Nv, B,
-            N.ptr(probs), N.ptr(g), N.ptr(saved), N.ptr(grad), N.ptr(ws), wsb, N.stream_ptr(dev)))
+            N.ptr(probs), N.ptr(g), N.ptr(saved), N.ptr(layer_probs) if gl is not None else None,
+            N.ptr(gl) if gl is not None else None, N.ptr(grad), N.ptr(ws), wsb, N.stream_ptr(dev)))
         grads, off = [], 0
         for s in shapes:
             n = int(torch.Size(s).numel())
@@ -389,7 +424,7 @@ class _NativeGnnTrain(torch.autograd.Function):
         for layer in range(L - 1):
             grads[2 + layer * 11 + 9] = None
             grads[2 + layer * 11 + 10] = None
-        return (None, None, None, None, None, *grads)
+        return (None, None, None, None, None, None, *grads)
 
 
 class TannerToMessageGraph:

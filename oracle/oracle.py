@@ -144,8 +144,12 @@ def message_types(graph, base, z):
 
 # --------------------------------------------------------------------------- GNN (torch fp32)
 def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, types=None,
-                ground_truth=None):
+                ground_truth=None, all_layers=False):
     """MessageGNNDecoder.forward restated (message_gnn_decoder.py:190-317).
+
+    all_layers  (training extension, no reference counterpart) return the (L, B, N) probs of every
+                layer's output through the LAST layer's output_projection (the decoder's
+                forward_all_layers / deep supervision); the last entry is the reference's probs.
 
     sd          state_dict (tensors) in the reference's key schema
     msg_var_io  (E,) int64 message->variable index used for the LLR gather and the output sum
@@ -174,6 +178,14 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
         h = torch.relu(z @ sd[p + ".0.weight"].T + sd[p + ".0.bias"])
         return h @ sd[p + ".2.weight"].T + sd[p + ".2.bias"]
 
+    last = f"gnn_layers.{n_layers - 1}.output_projection."
+
+    def head(x):
+        out = (x @ sd[last + "weight"][0]) + sd[last + "bias"][0]
+        var_llrs = torch.zeros(B, num_vars).index_add_(1, mv, out)
+        return torch.sigmoid(var_llrs + llr)
+
+    per_layer = []
     for i in range(n_layers):
         p = f"gnn_layers.{i}."
         emb = sd[p + "message_type_embeddings"]
@@ -183,10 +195,11 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
         y = mlp(p + "var_to_check_update", torch.cat([c, a], 2)) + \
             mlp(p + "check_to_var_update", torch.cat([c, b], 2))
         x = y + x if i > 0 else y
-    last = f"gnn_layers.{n_layers - 1}.output_projection."
-    out = (x @ sd[last + "weight"][0]) + sd[last + "bias"][0]
-    var_llrs = torch.zeros(B, num_vars).index_add_(1, mv, out)
-    probs = torch.sigmoid(var_llrs + llr)
+        if all_layers and i < n_layers - 1:
+            per_layer.append(head(x))
+    probs = head(x)
+    if all_layers:
+        return torch.stack(per_layer + [probs])
     if ground_truth is not None:
         return probs, F.binary_cross_entropy(probs, torch.as_tensor(ground_truth).float())
     return probs

@@ -119,3 +119,34 @@ def test_no_grad_path_unchanged(cuda):
     p1 = dec(*args)
     assert not p0.requires_grad and p1.requires_grad
     np.testing.assert_allclose(p0.cpu().numpy(), p1.detach().cpu().numpy(), atol=1e-6)
+
+
+@pytest.mark.parametrize("z,layers,hidden,B", [(4, 3, 64, 8), (4, 2, 32, 5), (32, 3, 64, 2)])
+def test_deep_supervision_matches_autograd(cuda, oracle_mod, z, layers, hidden, B):
+    """forward_all_layers (every layer's output through the last output_projection) and the
+    backward of a loss over all of them (ldpc_gnn_layer_probs / ldpc_gnn_backward_ds) vs torch
+    autograd through the oracle's all_layers forward.  Same tolerance as above.  Parity unpinned:
+    the reference has no per-layer loss; the oracle restates its forward and head."""
+    base, H, dec, conv, types, llr, gt = _setup(z, layers, hidden, B, seed=3)
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in dec.state_dict().items()}
+    ev, ec = conv.edge_var, conv.edge_chk
+    wts = torch.linspace(0.5, 1.0, layers)
+    ref_p = oracle_mod.gnn_forward(sd, llr, ev, ev, ec, H.shape[1], H.shape[0], types, all_layers=True)
+    ref_loss = sum(w * F.binary_cross_entropy(ref_p[i], gt) for i, w in enumerate(wts))
+    ref_loss.backward()
+    ref_g = {k: v.grad for k, v in sd.items()}
+    dec = dec.to(cuda)
+    p = dec.forward_all_layers(llr.to(cuda), conv.message_to_var_index(), types, conv.var_to_check_adjacency,
+                               conv.check_to_var_adjacency)
+    assert p.shape == (layers, B, H.shape[1])
+    np.testing.assert_allclose(p.detach().cpu().numpy(), ref_p.detach().numpy(), atol=2e-5)
+    g = gt.to(cuda)
+    loss = sum(w * F.binary_cross_entropy(p[i], g) for i, w in enumerate(wts.tolist()))
+    assert abs(loss.item() - ref_loss.item()) < 1e-4
+    loss.backward()
+    assert _check(dec, ref_g) == 2 + 9 * layers + 2
+    # the same final probs as forward()
+    with torch.no_grad():
+        q = dec(llr.to(cuda), conv.message_to_var_index(), types, conv.var_to_check_adjacency,
+                conv.check_to_var_adjacency)
+    np.testing.assert_allclose(q.cpu().numpy(), p[-1].detach().cpu().numpy(), atol=2e-6)

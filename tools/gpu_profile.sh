@@ -8,6 +8,8 @@ OUT=$R/gpurun_out/prof_${TAG}_${W}
 mkdir -p $OUT
 # stamp: the library build these counters describe (bench.py refuses PMC figures of another build)
 sha256sum ${LDPC_AMD_LIB:-$R/ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib/libldpc_amd.so} > $OUT/lib_sha256.txt || exit 1
+# and of each of its gfx950 code objects (bench.py also accepts a stamp on the benched kernel's one)
+python3 $R/tools/code_object_sha.py --all ${LDPC_AMD_LIB:-$R/ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib/libldpc_amd.so} > $OUT/code_objects_sha256.txt || exit 1
 cd /tmp && export TMPDIR=/tmp
 ok() { rc=$1; if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "fatal rc=$rc"; exit $rc; fi; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --workload $W --steps 10 --warmup 2 --cpu-baseline-seconds 0 $EXTRA > $OUT/trace_bench.log 2>&1; ok $?; echo "trace rc=$rc"

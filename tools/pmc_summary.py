@@ -45,6 +45,9 @@ def main(d, kern, out, expected_read=None, per_call=None):
     stamp = os.path.join(d, "lib_sha256.txt")
     if os.path.exists(stamp):
         out_d["lib_sha256"] = open(stamp).read().split()[0]
+    cos = os.path.join(d, "code_objects_sha256.txt")
+    if os.path.exists(cos):
+        out_d["code_objects_sha256"] = open(cos).read().split()
     if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
         read_b = 2 * res["FETCH_SIZE"] * 1024
         write_b = res["WRITE_SIZE"] * 1024
