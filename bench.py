@@ -505,7 +505,8 @@ def main():
         elif kind == "gnn-bf16":
             # HBM-bound; per frame-layer 3 passes over the bf16 features
             # (group-mean read, MLP read + write) + the fp32-sized group-mean rows written + read
-            per_launch_alg = iters * (3 * E * 64 * 2 + 2 * (g_n + g_m) * 64 * 4) * B
+            bf16_layer_bytes = (3 * E * 64 * 2 + 2 * (g_n + g_m) * 64 * 4) * B  # all frames, one layer
+            per_launch_alg = iters * bf16_layer_bytes
             bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
         elif kind == "gnn-train":
             # forward 12 H^2 E + backward 24 H^2 E (recomputed GEMM1, W2^T, W1^T, 4 weight-grad
@@ -549,6 +550,9 @@ def main():
         avg_layers = float(gdec.last_iterations.double().mean())  # this rank's last step
     be, fe, fr, itsum = tot.tolist()
 
+    if kind == "gnn-bf16" and avg_layers is not None:
+        # early termination: the layers actually run (the frames' mean), not the maximum
+        per_launch_alg = avg_layers * bf16_layer_bytes
     if rank == 0:
         total_frames = B * world * a.steps * (7 if kind == "gnn-sweep" else 1)
         value = total_frames / elapsed

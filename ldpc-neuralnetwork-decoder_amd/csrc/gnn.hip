@@ -773,6 +773,191 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
     }
 }
 
+// ------------------------------------------------------------------------ MLP over projected groups, fp32 by bf16x6
+// gnn_mlp2_kernel's math with every fp32 product on v_mfma_f32_32x32x16_bf16: each fp32 operand is
+// split into three bf16 terms, v = v0 + v1 + v2 (v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 -
+// v1): 24 significant bits, every subtraction exact), and a product a b is the six terms
+// a2 b0 + a1 b1 + a0 b2 + a1 b0 + a0 b1 + a0 b0 (the dropped ones are below 2^-24 |a b|), each exact
+// in the fp32 accumulator.  The result is an fp32 GEMM up to summation order -- the same class of
+// difference as between any two fp32 GEMMs -- at 6 x 32 instead of 8 x 64 MFMA cycles per K = 16
+// (2.67x less matrix time).  Weights: three split images per matrix in LDS (bf16, 72-element rows,
+// conflict-free ds_read_b128); activations (c for GEMM1, relu(h) for GEMM2) are split in registers.
+// K order: GEMM1's k-step s, lane half h, element i is unit pi16(16 s + 8 h + i) =
+// 32 (s>>1) + 16 (s&1) + 8 (i>>2) + 4 h + (i&3), which is the unit that lane owns in register
+// 8 (s&1) + i of accumulator tile s>>1: so GEMM2's B operand is GEMM1's accumulator as it stands,
+// and the x values loaded for GEMM1 are the residual the lane adds to its output registers.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__host__ __device__ constexpr int pi16(int p) {
+    return 32 * (p >> 5) + 16 * ((p >> 4) & 1) + 8 * ((p >> 2) & 1) + 4 * ((p >> 3) & 1) + (p & 3);
+}
+constexpr int kS6Row = 72;                                         // bf16 per image row
+constexpr int kS6Img = 64 * kS6Row;                                // bf16 per split image
+constexpr int kS6OffW2 = 6 * kS6Img;                               // W1L (side, split), then W2
+constexpr int kS6Bytes = 12 * kS6Img * 2;                          // 12 images
+constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo
+constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][64]
+inline size_t mlp2s_lds_bytes(int T) { return (size_t)(kS6OffEmb + T * 64) * 4; }
+
+__device__ __forceinline__ void split3(const float *v, bf16x8_t &a, bf16x8_t &b, bf16x8_t &c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const __bf16 h0 = (__bf16)v[i];
+        const float r1 = v[i] - (float)h0;
+        const __bf16 h1 = (__bf16)r1;
+        const float r2 = r1 - (float)h1;
+        a[i] = h0;
+        b[i] = h1;
+        c[i] = (__bf16)r2;
+    }
+}
+__device__ __forceinline__ bf16x8_t lds8(const __bf16 *p) { return *reinterpret_cast<const bf16x8_t *>(p); }
+// acc += A B over one K = 16 step, A from the three LDS images at img (+ kS6Img, + 2 kS6Img)
+__device__ __forceinline__ f32x16 mfma6(const __bf16 *img, const bf16x8_t &b0, const bf16x8_t &b1,
+                                        const bf16x8_t &b2, f32x16 acc) {
+    const bf16x8_t a0 = lds8(img), a1 = lds8(img + kS6Img), a2 = lds8(img + 2 * kS6Img);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
+}
+
+template <int NT, int WPS, bool HYB = false>
+__global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __bf16 *img = reinterpret_cast<__bf16 *>(lds);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 64 * 64; i += NT) {
+        const int o = i >> 6, p = i & 63, u = pi16(p);
+        const float w[4] = {P.w1v[o * 128 + u], P.w1c[o * 128 + u], P.w2v[o * 64 + u], P.w2c[o * 64 + u]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // q: W1v, W1c, W2v, W2c -> images 3q .. 3q + 2
+            const __bf16 h0 = (__bf16)w[q];
+            const float r1 = w[q] - (float)h0;
+            const __bf16 h1 = (__bf16)r1;
+            __bf16 *d = img + 3 * q * kS6Img + o * kS6Row + p;
+            d[0] = h0;
+            d[kS6Img] = h1;
+            d[2 * kS6Img] = (__bf16)(r1 - (float)h1);
+        }
+    }
+    if (tid < 64) {
+        lds[kS6OffB + tid] = P.vside ? P.b2v[tid] : 0.0f;
+        lds[kS6OffB + 64 + tid] = P.b2c[tid];
+        lds[kS6OffB + 128 + tid] = P.last ? P.wo[tid] : 0.0f;
+    }
+    for (int i = tid; i < P.T * 64; i += NT) lds[kS6OffEmb + i] = P.emb[i];
+    __syncthreads();
+
+    const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
+    const int64_t R = P.B * P.E;
+    const int64_t ntiles = (R + 31) / 32;
+    const float bo = P.last ? P.bo[0] : 0.0f;
+    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
+    const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
+    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+        const int64_t row = t * 32 + j;
+        const bool ok = row < R;
+        const int64_t rr = ok ? row : R - 1;
+        const int64_t b = rr / P.E, m = rr - b * P.E;
+        // x[s][i] = feature pi16(16 s + 8 h + i) before the type embedding (float4 pairs)
+        float x[4][8];
+        if (P.x_in) {
+            const float *xr = P.x_in + rr * 64 + 4 * half;
+            const float hv = HYB && P.hv2c ? P.hv2c[rr] : 0.0f;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int u0 = 32 * (s >> 1) + 16 * (s & 1) + 8 * q;  // + 4 half (in xr)
+                    float4 v = *reinterpret_cast<const float4 *>(xr + u0);
+                    if (HYB && P.hv2c)
+                        v = hyb_x(v, hv, *reinterpret_cast<const float4 *>(P.w_in + u0 + 4 * half),
+                                  *reinterpret_cast<const float4 *>(P.b_in + u0 + 4 * half));
+                    x[s][4 * q] = v.x; x[s][4 * q + 1] = v.y; x[s][4 * q + 2] = v.z; x[s][4 * q + 3] = v.w;
+                }
+            }
+        } else {
+            const float l = P.llr[b * P.N + P.msg_var[m]];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int u = pi16(16 * s + 8 * half + i);
+                    x[s][i] = l * P.w_in[u] + P.b_in[u];
+                }
+        }
+        const float *e = lds + kS6OffEmb + P.msg_type[m] * 64;
+        const float *pv = P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
+        const float *pc = P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
+        f32x16 y0 = {}, y1 = {};
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            if (side == 0 && !P.vside) continue;
+            const float *pr = side == 0 ? pv : pc;
+            f32x16 h0, h1;  // from the projected group row W1_right g + b1
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 a = *reinterpret_cast<const float4 *>(pr + 8 * q);
+                const float4 c = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q);
+                h0[4 * q] = a.x; h0[4 * q + 1] = a.y; h0[4 * q + 2] = a.z; h0[4 * q + 3] = a.w;
+                h1[4 * q] = c.x; h1[4 * q + 1] = c.y; h1[4 * q + 2] = c.z; h1[4 * q + 3] = c.w;
+            }
+            const __bf16 *W1 = img + 3 * side * kS6Img + abase, *W2 = img + kS6OffW2 + 3 * side * kS6Img + abase;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {  // GEMM1: h += W1_left c, c = x + emb[type]
+                float c[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) c[i] = x[s][i] + e[pi16(16 * s + 8 * half + i)];
+                bf16x8_t c0, c1, c2;
+                split3(c, c0, c1, c2);
+                h0 = mfma6(W1 + 16 * s, c0, c1, c2, h0);
+                h1 = mfma6(W1 + 32 * kS6Row + 16 * s, c0, c1, c2, h1);
+                __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {  // GEMM2: y += W2 relu(h); k-step s = registers 8 (s&1) .. of h_{s>>1}
+                float hr[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) hr[i] = fmaxf(s < 2 ? h0[8 * (s & 1) + i] : h1[8 * (s & 1) + i], 0.0f);
+                bf16x8_t r0, r1, r2;
+                split3(hr, r0, r1, r2);
+                y0 = mfma6(W2 + 16 * s, r0, r1, r2, y0);
+                y1 = mfma6(W2 + 32 * kS6Row + 16 * s, r0, r1, r2, y1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        const float *b2v = lds + kS6OffB, *b2c = lds + kS6OffB + 64, *wo = lds + kS6OffB + 128;
+        float part = 0.0f;
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int o0 = 32 * ot + 8 * q + 4 * half;
+                float4 v;
+                float *vv = reinterpret_cast<float *>(&v);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float acc = ot == 0 ? y0[4 * q + i] : y1[4 * q + i];
+                    vv[i] = (acc + b2v[o0 + i]) + b2c[o0 + i];
+                    // residual: register 4 q + i of tile ot is x[2 ot + (q >> 1)][4 (q & 1) + i]
+                    if (P.residual) vv[i] += x[2 * ot + (q >> 1)][4 * (q & 1) + i];
+                }
+                if (P.last) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) part += vv[i] * wo[o0 + i];
+                }
+                if (ok && P.x_out) *reinterpret_cast<float4 *>(P.x_out + row * 64 + o0) = v;
+            }
+        }
+        if (P.last) {
+            part += __shfl_xor(part, 32, 64);
+            if (ok && half == 0) P.msg_out[b * P.E + m] = part + bo;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------ fused MLP, any H
 // one wave per message, lanes = output units (H <= 64 per pass); VALU fp32.
 __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H) {
@@ -984,6 +1169,21 @@ __global__ void custom_output_kernel(const float *__restrict__ msg_out, const in
 int g_num_cus = 0;
 
 constexpr int kMlp2Wps = LDPC_MLP2_WPS, kMlp2Nt = LDPC_MLP2_NT;
+#ifndef LDPC_MLP2S_WPS
+#define LDPC_MLP2S_WPS 3
+#endif
+#ifndef LDPC_MLP2S_NT
+#define LDPC_MLP2S_NT 768
+#endif
+constexpr int kMlp2sWps = LDPC_MLP2S_WPS, kMlp2sNt = LDPC_MLP2S_NT;
+// LDPC_GNN_SPLIT=0: the projected-group MLP on v_mfma_f32_32x32x2_f32 (gnn_mlp2_kernel); default:
+// the same fp32 products as three-term bf16 splits on the bf16 MFMA (gnn_mlp2s_kernel).  Read per
+// call (tests compare the two).
+bool split_path() {
+    const char *e = std::getenv("LDPC_GNN_SPLIT");
+    return !(e && std::atoi(e) == 0);
+}
+
 // LDPC_GNN_PROJ=0 keeps the per-message [c; g] GEMM1 (gnn_mlp_mfma_kernel) for A/B runs
 bool proj_path() {
     static bool t = [] {
@@ -1357,7 +1557,9 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     // projection workgroups of 12 waves (one LDS weight image for 12 waves' gathers) when the
     // type table leaves room, else 4
     const int proj_nt = LDPC_PROJ_NT == 768 && proj_lds_bytes(types, 12) <= 160 * 1024 ? 768 : 256;
-    const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64), mlp2_lds = mlp2_lds_bytes(types);
+    const bool split = split_path() && mlp2s_lds_bytes(types) <= 160 * 1024;
+    const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
+                 mlp2_lds = split ? mlp2s_lds_bytes(types) : mlp2_lds_bytes(types);
     const void *proj_fn = proj_nt == 768 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<768>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
     int mlp2_per_cu = 1, proj_per_cu = 1;
@@ -1369,7 +1571,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
-        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
+        LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps>)
+                                           : reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
     }
     // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
@@ -1417,7 +1620,12 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             const int64_t tiles = (nb * p->E + 31) / 32;
             constexpr int wpb = kMlp2Nt / 64;
             const unsigned grid = (unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu);
-            hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>), dim3(grid), dim3(kMlp2Nt), mlp2_lds, st, L);
+            if (split)
+                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps>),
+                                   dim3((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus)),
+                                   dim3(kMlp2sNt), mlp2_lds, st, L);
+            else
+                hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>), dim3(grid), dim3(kMlp2Nt), mlp2_lds, st, L);
             LDPC_CHECK_LAUNCH("gnn_mlp2_kernel");
             x_in = L.x_out;
             continue;
@@ -1591,11 +1799,13 @@ extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, i
         LDPC_HIP(hipGetDevice(&dev));
         LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    const size_t proj_lds = proj_lds_bytes(types, 4), mlp2_lds = mlp2_lds_bytes(types);
+    const bool split = split_path() && mlp2s_lds_bytes(types) <= 160 * 1024;
+    const size_t proj_lds = proj_lds_bytes(types, 4), mlp2_lds = split ? mlp2s_lds_bytes(types) : mlp2_lds_bytes(types);
     if (proj_lds > 160 * 1024 || mlp2_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_group_proj_kernel<256, true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
-    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps, true>),
+    LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, true>)
+                                       : reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps, true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
     const int mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
     const int proj_per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
@@ -1626,9 +1836,13 @@ extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, i
         LDPC_CHECK_LAUNCH("gnn_group_proj_kernel (check side)");
         constexpr int wpb = kMlp2Nt / 64;
         const int64_t tiles = (R + 31) / 32;
-        hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps, true>),
-                           dim3((unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu)),
-                           dim3(kMlp2Nt), mlp2_lds, s, L);
+        const dim3 mgrid((unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu));
+        if (split)
+            hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, true>),
+                               dim3((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus)),
+                               dim3(kMlp2sNt), mlp2_lds, s, L);
+        else
+            hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps, true>), mgrid, dim3(kMlp2Nt), mlp2_lds, s, L);
         LDPC_CHECK_LAUNCH("gnn_mlp2_kernel (check side)");
         hipLaunchKernelGGL(custom_var_llr_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, w.msg_out, w.csr,
                            d_llr, p->E, N, B, v2c);

@@ -144,12 +144,14 @@ def message_types(graph, base, z):
 
 # --------------------------------------------------------------------------- GNN (torch fp32)
 def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, types=None,
-                ground_truth=None, all_layers=False):
+                ground_truth=None, all_layers=False, dtype=None):
     """MessageGNNDecoder.forward restated (message_gnn_decoder.py:190-317).
 
     all_layers  (training extension, no reference counterpart) return the (L, B, N) probs of every
                 layer's output through the LAST layer's output_projection (the decoder's
                 forward_all_layers / deep supervision); the last entry is the reference's probs.
+    dtype       None: float32, the reference's arithmetic; torch.float64 gives the exact-arithmetic
+                yardstick the fp32 kernels' errors are measured against
 
     sd          state_dict (tensors) in the reference's key schema
     msg_var_io  (E,) int64 message->variable index used for the LLR gather and the output sum
@@ -159,7 +161,10 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
     import torch
     import torch.nn.functional as F
 
-    llr = torch.as_tensor(llr, dtype=torch.float32)
+    dt = dtype or torch.float32
+    llr = torch.as_tensor(llr).to(dt)
+    if dtype is not None:
+        sd = {k: v.to(dt) for k, v in sd.items()}
     B, E = llr.shape[0], len(edge_var)
     mv = torch.as_tensor(msg_var_io, dtype=torch.long)
     ev = torch.as_tensor(edge_var, dtype=torch.long)
@@ -167,11 +172,11 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
     n_layers = len({k.split(".")[1] for k in sd if k.startswith("gnn_layers.")})
     x = llr[:, mv].unsqueeze(-1) * sd["input_embedding.weight"][:, 0] + sd["input_embedding.bias"]
     t = torch.zeros(E, dtype=torch.long) if types is None else torch.as_tensor(types).long()
-    deg_v = torch.bincount(ev, minlength=num_vars).float()
-    deg_c = torch.bincount(ec, minlength=num_checks).float()
+    deg_v = torch.bincount(ev, minlength=num_vars).to(dt)
+    deg_c = torch.bincount(ec, minlength=num_checks).to(dt)
 
     def seg_mean(c, idx, deg, n):
-        s = torch.zeros(B, n, c.shape[-1]).index_add_(1, idx, c)
+        s = torch.zeros(B, n, c.shape[-1], dtype=dt).index_add_(1, idx, c)
         return (s / deg.clamp(min=1).view(1, -1, 1))[:, idx]
 
     def mlp(p, z):
@@ -182,7 +187,7 @@ def gnn_forward(sd, llr, msg_var_io, edge_var, edge_chk, num_vars, num_checks, t
 
     def head(x):
         out = (x @ sd[last + "weight"][0]) + sd[last + "bias"][0]
-        var_llrs = torch.zeros(B, num_vars).index_add_(1, mv, out)
+        var_llrs = torch.zeros(B, num_vars, dtype=dt).index_add_(1, mv, out)
         return torch.sigmoid(var_llrs + llr)
 
     per_layer = []

@@ -54,9 +54,13 @@ def _native(dec, conv, types, llr, cuda, chunk=None):
         return dec.native_forward(llr, io, t, conv.var_groups, conv.check_groups, chunk=chunk)
 
 
-def test_cfg4_depth_fp32_vs_oracle(cuda, oracle_mod):
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_cfg4_depth_fp32_vs_oracle(cuda, oracle_mod, monkeypatch, split):
     """10-layer fp32 forward at Z=32, H=64 through native_forward, forward() under no_grad and
-    decode() (which must take the inference path even with grad enabled)."""
+    decode() (which must take the inference path even with grad enabled).  split: the MLP's fp32
+    products as three-term bf16 splits on the bf16 MFMA (default) or on the fp32 MFMA
+    (LDPC_GNN_SPLIT=0); same bar."""
+    monkeypatch.setenv("LDPC_GNN_SPLIT", split)
     base, H, dec, conv, types = _model(10, cuda)
     llr = (torch.randn(8, H.shape[1], generator=torch.Generator().manual_seed(4)) * 2 + 1.5).to(cuda)
     ref = _oracle(oracle_mod, dec, conv, H, types, llr)
@@ -149,3 +153,21 @@ def test_bf16_projected_rows_vs_group_means(cuda, oracle_mod, monkeypatch, layer
         assert d.mean() <= 5e-3 and d.max() <= 0.1 and agree >= 0.995
     assert not np.array_equal(out["1"], out["0"])
     assert np.abs(out["1"] - out["0"]).mean() <= 5e-3
+
+
+def test_split_mlp_is_fp32_accurate(cuda, oracle_mod, monkeypatch):
+    """The bf16x6 MLP (gnn_mlp2s_kernel) is an fp32 GEMM up to summation order: against the
+    float64 oracle its error is within 2x (+1e-7) of the fp32-MFMA kernel's and of the float32
+    oracle's own, at 10 layers, Z=32."""
+    base, H, dec, conv, types = _model(10, cuda, seed=5)
+    llr = awgn_llr(16, H.shape[1], 1.0, seed=9, device=cuda)
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    args = (sd, llr.cpu(), conv.edge_var, conv.edge_var, conv.edge_chk, H.shape[1], H.shape[0], types)
+    exact = oracle_mod.gnn_forward(*args, dtype=torch.float64).numpy()
+    f32 = oracle_mod.gnn_forward(*args).numpy()
+    err = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("LDPC_GNN_SPLIT", split)
+        err[split] = float(np.abs(_native(dec, conv, types, llr, cuda).cpu().numpy() - exact).max())
+    ref_err = float(np.abs(f32 - exact).max())
+    assert err["1"] <= 2 * max(err["0"], ref_err) + 1e-7, (err, ref_err)
