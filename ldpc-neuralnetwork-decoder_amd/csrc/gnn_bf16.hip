@@ -451,7 +451,9 @@ struct TileIn {
 // (output projection + per-variable sum instead of writing x); bit 2: projected group rows
 // (GEMM1 over x only, started from K + the group's W1_right g row; tiles in the plan's message
 // order, whose degree-1 tiles run GEMM1 over x with W1v,left + W1v,right and D1)
-template <int NT, int WPS, bool PF, int MODE>
+// PF: 0 no register prefetch; 1 the next tile's rows one tile ahead; 2 (non-projected, layers >= 1)
+// as 1, and the feature rows -- the HBM part of a tile -- two tiles ahead
+template <int NT, int WPS, int PF, int MODE>
 __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
@@ -512,7 +514,19 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     auto load_on = [&](int64_t t, int64_t b) -> bool {
         return A.list || !A.active || A.active[t < tw.end ? b : fb];  // listed frames are active
     };
-    auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k) {
+    // the feature rows of tile t (frame slot b, in-frame tile k) alone: PF 2 issues them a tile
+    // before the rest of the tile's loads (a terminated frame's rows are loaded too: harmless)
+    struct XRows { bf16x8 v[4]; };
+    auto load_x = [&](int64_t t, int64_t b, int64_t k) {
+        XRows X;
+        const int m0 = (int)k * 32 + j;
+        const int64_t bb = frame_of(t < tw.end ? b : fb);
+        const char *xr = reinterpret_cast<const char *>(A.x_in + (bb * A.E + (m0 < A.E ? m0 : A.E - 1)) * H) + 16 * h;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) X.v[s] = ld8(xr + 32 * s);
+        return X;
+    };
+    auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k, const XRows *xpre = nullptr) {
         TileIn I;
         const int m0 = (int)k * 32 + j;
         I.ok = (proj ? inf.w >= 0 : m0 < A.E) && t < tw.end;
@@ -533,9 +547,14 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         const char *ma = reinterpret_cast<const char *>(A.Mv + (lb * A.Gv + vg) * H) + 16 * h;
         const char *mc = reinterpret_cast<const char *>(A.Mc + (lb * A.Gc + inf.y) * H) + 16 * h;
         if constexpr (!layer0) {
-            const char *xr = reinterpret_cast<const char *>(A.x_in + (lb * A.E + m) * H) + 16 * h;
+            if (xpre) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s) I.xf[s] = ld8(xr + 32 * s);
+                for (int s = 0; s < 4; ++s) I.xf[s] = xpre->v[s];
+            } else {
+                const char *xr = reinterpret_cast<const char *>(A.x_in + (lb * A.E + m) * H) + 16 * h;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) I.xf[s] = ld8(xr + 32 * s);
+            }
             I.l = 0.0f;
         } else {
             I.l = A.llr[lb * A.N + I.var];
@@ -652,7 +671,31 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     };
 
     if (tw.first >= tw.end) return;
-    if constexpr (PF) {
+    if constexpr (PF == 2 && !proj && !layer0) {
+        // feature rows two tiles ahead, everything else one tile ahead, message info and frame
+        // flags as in PF 1
+        TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
+        int64_t nb = fb + sb, nk = fk + sk;
+        if (nk >= A.tpf) { nk -= A.tpf; ++nb; }
+        int4 inf_n = load_info(nk);
+        bool on_n = load_on(tw.first + tw.stride, nb);
+        XRows x_n = load_x(tw.first + tw.stride, nb, nk);
+        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+            int64_t nb2 = nb + sb, nk2 = nk + sk;
+            if (nk2 >= A.tpf) { nk2 -= A.tpf; ++nb2; }
+            const int4 inf_nn = load_info(nk2);
+            const bool on_nn = load_on(t + 2 * tw.stride, nb2);
+            const XRows x_nn = load_x(t + 2 * tw.stride, nb2, nk2);
+            const TileIn nxt = load(inf_n, on_n, t + tw.stride, nb, nk, &x_n);
+            compute(cur);
+            cur = nxt;
+            x_n = x_nn;
+            inf_n = inf_nn;
+            on_n = on_nn;
+            nb = nb2;
+            nk = nk2;
+        }
+    } else if constexpr (PF != 0) {
         // rows are prefetched one tile ahead; the small per-tile items (message info, frame
         // flag) two tiles ahead, so the row loads never wait behind an index load
         TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
@@ -806,7 +849,7 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
 
 int g_cus = 0;
 
-template <int NT, int WPS, bool PF, int MODE>
+template <int NT, int WPS, int PF, int MODE>
 int launch_mlp_t(int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     const void *fn = reinterpret_cast<const void *>(gnn_bf16_mlp_kernel<NT, WPS, PF, MODE>);
     LDPC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -816,7 +859,7 @@ int launch_mlp_t(int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     return LDPC_OK;
 }
 
-template <int NT, int WPS, bool PF>
+template <int NT, int WPS, int PF>
 int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (mode) {
         case 0: return launch_mlp_t<NT, WPS, PF, 0>(tiles, lds, s, m);
@@ -836,14 +879,16 @@ int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpAr
 //   2 = 512 threads, 4 waves/SIMD, no prefetch (spills at 128 VGPRs)
 //   3 = 512 threads, 2 waves/SIMD, prefetch: one workgroup (one LDS weight copy) per CU
 //   4 = 768 threads, 3 waves/SIMD, prefetch; 5 = 1024 threads, 4 waves/SIMD, no prefetch
+//   6 = as 1, feature rows two tiles ahead (PF 2)
 int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (variant) {
-        case 0: return launch_mlp_v<768, 3, false>(mode, tiles, lds, s, m);
-        case 2: return launch_mlp_v<512, 4, false>(mode, tiles, lds, s, m);
-        case 3: return launch_mlp_v<512, 2, true>(mode, tiles, lds, s, m);
-        case 4: return launch_mlp_v<768, 3, true>(mode, tiles, lds, s, m);
-        case 5: return launch_mlp_v<1024, 4, false>(mode, tiles, lds, s, m);
-        default: return launch_mlp_v<256, 2, true>(mode, tiles, lds, s, m);
+        case 0: return launch_mlp_v<768, 3, 0>(mode, tiles, lds, s, m);
+        case 2: return launch_mlp_v<512, 4, 0>(mode, tiles, lds, s, m);
+        case 3: return launch_mlp_v<512, 2, 1>(mode, tiles, lds, s, m);
+        case 4: return launch_mlp_v<768, 3, 1>(mode, tiles, lds, s, m);
+        case 5: return launch_mlp_v<1024, 4, 0>(mode, tiles, lds, s, m);
+        case 6: return launch_mlp_v<256, 2, 2>(mode, tiles, lds, s, m);
+        default: return launch_mlp_v<256, 2, 1>(mode, tiles, lds, s, m);
     }
 }
 
@@ -872,11 +917,8 @@ int proj_env() {
 }
 
 int mlp_variant() {
-    static int v = [] {
-        const char *e = std::getenv("LDPC_GNN_BF16_MLP");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
+    const char *e = std::getenv("LDPC_GNN_BF16_MLP");  // read per call (tests compare variants)
+    return e ? std::atoi(e) : 1;
 }
 
 }  // namespace

@@ -83,3 +83,18 @@ def test_fp32_early_termination_is_refused(cuda):
     llr = awgn_llr(4, H.shape[1], 3.0, device=cuda)
     with pytest.raises(NotImplementedError):
         _run(dec, conv, base, 4, llr, True)
+
+
+@pytest.mark.parametrize("variant", ["0", "6"])
+@pytest.mark.parametrize("et", [False, True])
+def test_mlp_variants_are_bitwise_equal(cuda, monkeypatch, variant, et):
+    """The bf16 MLP kernel's occupancy / prefetch variants (LDPC_GNN_BF16_MLP: 1 default, 0 = 3
+    waves without register prefetch, 6 = feature rows two tiles ahead) run the same arithmetic in
+    the same order: bitwise equal probs and layer counts, with and without early termination."""
+    base, H, dec, conv = _decoder(32, 6, cuda, seed=2)
+    llr = awgn_llr(300, H.shape[1], 4.0, seed=21, device=cuda)
+    monkeypatch.setenv("LDPC_GNN_BF16_MLP", "1")
+    p1, it1 = _run(dec, conv, base, 32, llr, et)
+    monkeypatch.setenv("LDPC_GNN_BF16_MLP", variant)
+    p2, it2 = _run(dec, conv, base, 32, llr, et)
+    assert torch.equal(p1, p2) and torch.equal(it1, it2)
