@@ -595,11 +595,21 @@ def main():
         notes = None
         if kind in ("gnn", "gnn-sweep"):
             reps = len(sweep_snrs) if kind == "gnn-sweep" else 1
+            split = os.environ.get("LDPC_GNN_SPLIT", "1") != "0"
             notes = {"flop_model": "achieved = SURVEY 8(d)'s algorithmic FLOPs, the reference's per-message MLPs: "
-                                   "12 H^2 E per frame-layer. This build executes 8 H^2 E + 2 H^2 (N + M) "
-                                   "(W1's group half applied once per group): executed_frac is that rate",
+                                   "12 H^2 E per frame-layer, against the fp32 MFMA peak. This build executes "
+                                   "8 H^2 E + 2 H^2 (N + M) fp32-equivalent FLOPs (W1's group half applied once per "
+                                   "group): executed_frac is that rate",
                      "executed_flops_per_launch": fwd_flops * B * iters * reps,
                      "executed_frac": fwd_flops / nominal_flops * achieved / peak}
+            if split:
+                # gnn_mlp2s_kernel: the per-message products (8 H^2 E) as six bf16 products each on the
+                # bf16 MFMA; the group projection (2 H^2 (N + M)) stays on the fp32 MFMA
+                mlp_bf16 = 6 * 8 * 64 * 64 * E * B * iters * reps
+                notes["mlp_products"] = ("bf16x6 split (fp32-accurate, tests/test_gnn_depth_gpu.py::"
+                                         "test_split_mlp_is_fp32_accurate)")
+                notes["mlp_bf16_mfma_flops_per_launch"] = mlp_bf16
+                notes["mlp_bf16_mfma_frac_whole_forward"] = mlp_bf16 / (kern_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFS
         if bound == "valu":
             achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg)
             if tjd is None:

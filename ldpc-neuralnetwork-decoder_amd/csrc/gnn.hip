@@ -1556,11 +1556,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     const bool proj = mfma && !p->weighted && p->n_ptiles > 0 && proj_path();
     // projection workgroups of 12 waves (one LDS weight image for 12 waves' gathers) when the
     // type table leaves room, else 4
-    const int proj_nt = LDPC_PROJ_NT == 768 && proj_lds_bytes(types, 12) <= 160 * 1024 ? 768 : 256;
+    const int proj_nt = LDPC_PROJ_NT != 256 && proj_lds_bytes(types, LDPC_PROJ_NT / 64) <= 160 * 1024 ? LDPC_PROJ_NT : 256;
     const bool split = split_path() && mlp2s_lds_bytes(types) <= 160 * 1024;
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
                  mlp2_lds = split ? mlp2s_lds_bytes(types) : mlp2_lds_bytes(types);
-    const void *proj_fn = proj_nt == 768 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<768>)
+    const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
     int mlp2_per_cu = 1, proj_per_cu = 1;
     if (proj) {
@@ -1612,8 +1612,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;
             const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
-            if (proj_nt == 768)
-                hipLaunchKernelGGL(gnn_group_proj_kernel<768>, dim3(pgrid), dim3(768), proj_lds, st, L, T);
+            if (proj_nt != 256)
+                hipLaunchKernelGGL(gnn_group_proj_kernel<LDPC_PROJ_NT>, dim3(pgrid), dim3(LDPC_PROJ_NT), proj_lds, st, L, T);
             else
                 hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds, st, L, T);
             LDPC_CHECK_LAUNCH("gnn_group_proj_kernel");
@@ -1716,10 +1716,10 @@ int ldpc::gnn_project_groups(const ldpc_gnn_plan *p, int types, const float *d_w
     L.w1c = L.b2v + H;
     L.b1c = L.w1c + 2LL * H * H;
     L.w2c = L.b1c + H;
-    const int proj_nt = LDPC_PROJ_NT == 768 && proj_lds_bytes(types, 12) <= 160 * 1024 ? 768 : 256;
+    const int proj_nt = LDPC_PROJ_NT != 256 && proj_lds_bytes(types, LDPC_PROJ_NT / 64) <= 160 * 1024 ? LDPC_PROJ_NT : 256;
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64);
     if (proj_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
-    const void *proj_fn = proj_nt == 768 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<768>)
+    const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
     LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
     const int per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
@@ -1727,8 +1727,8 @@ int ldpc::gnn_project_groups(const ldpc_gnn_plan *p, int types, const float *d_w
     const int64_t ptiles = B * (int64_t)p->n_ptiles;
     const int pw = proj_nt / 64;
     const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * per_cu);
-    if (proj_nt == 768)
-        hipLaunchKernelGGL(gnn_group_proj_kernel<768>, dim3(pgrid), dim3(768), proj_lds, s, L, T);
+    if (proj_nt != 256)
+        hipLaunchKernelGGL(gnn_group_proj_kernel<LDPC_PROJ_NT>, dim3(pgrid), dim3(LDPC_PROJ_NT), proj_lds, s, L, T);
     else
         hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds, s, L, T);
     LDPC_CHECK_LAUNCH("gnn_group_proj_kernel (training backward)");
