@@ -386,7 +386,9 @@ def main():
             N.check(N.lib().ldpc_custom_minsum_decode(g.handle, N.ptr(llr), B, iters, N.ptr(probs), N.ptr(ws), wsb,
                                                       stream))
             if count:
-                count_errors((probs > 0.5).to(torch.uint8), ref=ref_bits, counters=counters)
+                # probs = sigmoid(llr + S) (MGD:1214-1240) is P(bit = 0) for a channel LLR log P(0)/P(1):
+                # counted with the flooding decoders' rule, bit = 1 where the APP is negative (TD:101)
+                count_errors((probs < 0.5).to(torch.uint8), ref=ref_bits, counters=counters)
 
         dtype = "f32"
         # per frame-iteration, messages in HBM: variable phase reads + writes every edge message and

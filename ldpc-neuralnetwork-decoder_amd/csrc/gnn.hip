@@ -786,10 +786,6 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
 // 32 (s>>1) + 16 (s&1) + 8 (i>>2) + 4 h + (i&3), which is the unit that lane owns in register
 // 8 (s&1) + i of accumulator tile s>>1: so GEMM2's B operand is GEMM1's accumulator as it stands,
 // and the x values loaded for GEMM1 are the residual the lane adds to its output registers.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-__host__ __device__ constexpr int pi16(int p) {
-    return 32 * (p >> 5) + 16 * ((p >> 4) & 1) + 8 * ((p >> 2) & 1) + 4 * ((p >> 3) & 1) + (p & 3);
-}
 constexpr int kS6Row = 72;                                         // bf16 per image row
 constexpr int kS6Img = 64 * kS6Row;                                // bf16 per split image
 constexpr int kS6OffW2 = 6 * kS6Img;                               // W1L (side, split), then W2
@@ -797,31 +793,6 @@ constexpr int kS6Bytes = 12 * kS6Img * 2;                          // 12 images
 constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo
 constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][64]
 inline size_t mlp2s_lds_bytes(int T) { return (size_t)(kS6OffEmb + T * 64) * 4; }
-
-__device__ __forceinline__ void split3(const float *v, bf16x8_t &a, bf16x8_t &b, bf16x8_t &c) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const __bf16 h0 = (__bf16)v[i];
-        const float r1 = v[i] - (float)h0;
-        const __bf16 h1 = (__bf16)r1;
-        const float r2 = r1 - (float)h1;
-        a[i] = h0;
-        b[i] = h1;
-        c[i] = (__bf16)r2;
-    }
-}
-__device__ __forceinline__ bf16x8_t lds8(const __bf16 *p) { return *reinterpret_cast<const bf16x8_t *>(p); }
-// acc += A B over one K = 16 step, A from the three LDS images at img (+ kS6Img, + 2 kS6Img)
-__device__ __forceinline__ f32x16 mfma6(const __bf16 *img, const bf16x8_t &b0, const bf16x8_t &b1,
-                                        const bf16x8_t &b2, f32x16 acc) {
-    const bf16x8_t a0 = lds8(img), a1 = lds8(img + kS6Img), a2 = lds8(img + 2 * kS6Img);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
-}
 
 template <int NT, int WPS, bool HYB = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
@@ -832,15 +803,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         const int o = i >> 6, p = i & 63, u = pi16(p);
         const float w[4] = {P.w1v[o * 128 + u], P.w1c[o * 128 + u], P.w2v[o * 64 + u], P.w2c[o * 64 + u]};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {  // q: W1v, W1c, W2v, W2c -> images 3q .. 3q + 2
-            const __bf16 h0 = (__bf16)w[q];
-            const float r1 = w[q] - (float)h0;
-            const __bf16 h1 = (__bf16)r1;
-            __bf16 *d = img + 3 * q * kS6Img + o * kS6Row + p;
-            d[0] = h0;
-            d[kS6Img] = h1;
-            d[2 * kS6Img] = (__bf16)(r1 - (float)h1);
-        }
+        for (int q = 0; q < 4; ++q)  // q: W1v, W1c, W2v, W2c -> images 3q .. 3q + 2
+            split_store(w[q], img + 3 * q * kS6Img + o * kS6Row + p, kS6Img);
     }
     if (tid < 64) {
         lds[kS6OffB + tid] = P.vside ? P.b2v[tid] : 0.0f;
@@ -912,8 +876,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 for (int i = 0; i < 8; ++i) c[i] = x[s][i] + e[pi16(16 * s + 8 * half + i)];
                 bf16x8_t c0, c1, c2;
                 split3(c, c0, c1, c2);
-                h0 = mfma6(W1 + 16 * s, c0, c1, c2, h0);
-                h1 = mfma6(W1 + 32 * kS6Row + 16 * s, c0, c1, c2, h1);
+                h0 = mfma6(W1 + 16 * s, c0, c1, c2, h0, kS6Img);
+                h1 = mfma6(W1 + 32 * kS6Row + 16 * s, c0, c1, c2, h1, kS6Img);
                 __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
             }
 #pragma unroll
@@ -923,8 +887,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 for (int i = 0; i < 8; ++i) hr[i] = fmaxf(s < 2 ? h0[8 * (s & 1) + i] : h1[8 * (s & 1) + i], 0.0f);
                 bf16x8_t r0, r1, r2;
                 split3(hr, r0, r1, r2);
-                y0 = mfma6(W2 + 16 * s, r0, r1, r2, y0);
-                y1 = mfma6(W2 + 32 * kS6Row + 16 * s, r0, r1, r2, y1);
+                y0 = mfma6(W2 + 16 * s, r0, r1, r2, y0, kS6Img);
+                y1 = mfma6(W2 + 32 * kS6Row + 16 * s, r0, r1, r2, y1, kS6Img);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }

@@ -107,4 +107,47 @@ __device__ __forceinline__ TileWalk xcd_tiles(int64_t ntiles, int waves_per_bloc
     return {t0 + i * waves_per_block + wave, nbx * waves_per_block, t1};
 }
 
+
+// ---- fp32 products as three-term bf16 splits on v_mfma_f32_32x32x16_bf16 (gnn.hip gnn_mlp2s_kernel,
+// gnn_train.hip train_mlp_bwd_split_kernel): see gnn_mlp2s_kernel's comment
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__host__ __device__ constexpr int pi16(int p) {
+    return 32 * (p >> 5) + 16 * ((p >> 4) & 1) + 8 * ((p >> 2) & 1) + 4 * ((p >> 3) & 1) + (p & 3);
+}
+__device__ __forceinline__ void split3(const float *v, bf16x8_t &a, bf16x8_t &b, bf16x8_t &c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const __bf16 h0 = (__bf16)v[i];
+        const float r1 = v[i] - (float)h0;
+        const __bf16 h1 = (__bf16)r1;
+        const float r2 = r1 - (float)h1;
+        a[i] = h0;
+        b[i] = h1;
+        c[i] = (__bf16)r2;
+    }
+}
+// one fp32 value's three split terms at d, d + stride, d + 2 stride (the weight images)
+__device__ __forceinline__ void split_store(float w, __bf16 *d, int stride) {
+    const __bf16 h0 = (__bf16)w;
+    const float r1 = w - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    d[0] = h0;
+    d[stride] = h1;
+    d[2 * stride] = (__bf16)(r1 - (float)h1);
+}
+__device__ __forceinline__ bf16x8_t lds8(const __bf16 *p) { return *reinterpret_cast<const bf16x8_t *>(p); }
+// acc += A B over one K = 16 step, A from the three split images at img (+ img_stride, + 2 img_stride)
+__device__ __forceinline__ f32x16_t mfma6(const __bf16 *img, const bf16x8_t &b0, const bf16x8_t &b1,
+                                        const bf16x8_t &b2, f32x16_t acc, int img_stride) {
+    const bf16x8_t a0 = lds8(img), a1 = lds8(img + img_stride), a2 = lds8(img + 2 * img_stride);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
+}
+
+
 }  // namespace ldpc

@@ -5,7 +5,7 @@ cd $R
 run() {  # name, args...
   local n=$1; shift
   timeout -k 10 400 python3 bench.py "$@" > $OUT/$n.json 2> $OUT/$n.err || { rc=$?; echo "bench $n rc=$rc"; tail -5 $OUT/$n.err; exit $rc; }
-  python3 -c "import json; d=json.load(open('$OUT/$n.json')); r=d['roofline']; c=d['cpu_baseline'] or {}; print('$n', round(d['value']), d['unit'], 'frac', round(r['frac'],3), 'kern_ms', round(r['kernel_ms'],2), 'cpu', c.get('value'))"
+  python3 -c "import json; d=json.load(open('$OUT/$n.json')); r=d['roofline']; c=d['cpu_baseline'] or {}; print('$n', round(d['value']), d['unit'], 'frac', None if r['frac'] is None else round(r['frac'],3), 'kern_ms', round(r['kernel_ms'],2), 'cpu', c.get('value'))"
 }
 run minsum-z32 --steps 20 --warmup 3
 run bp-z4 --workload bp-z4 --batch 65536 --steps 10 --warmup 3 --cpu-baseline-seconds 5
