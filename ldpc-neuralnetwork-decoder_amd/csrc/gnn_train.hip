@@ -1097,11 +1097,13 @@ int bwd_proj() {
     return e ? std::atoi(e) : 1;
 }
 
-// LDPC_GNN_SPLIT=0: the backward MLP on the fp32 MFMA alone; default: GEMM1 and GEMM3' as bf16x6
-// splits (train_mlp_bwd_split_kernel), like the forward's MLP (gnn.hip).  Read per call.
+// LDPC_GNN_TRAIN_SPLIT=1: GEMM1 and GEMM3' of the backward MLP as bf16x6 splits
+// (train_mlp_bwd_split_kernel), like the forward's MLP (gnn.hip); default 0: the fp32-MFMA kernel.
+// Measured 1.27 vs 1.24 ms per layer at B = 256 (profiles/r03n): the kernel is bound by its six
+// (B, E, H) outputs, not by the matrix pipe.  Read per call.
 int bwd_split() {
-    const char *e = std::getenv("LDPC_GNN_SPLIT");
-    return !(e && std::atoi(e) == 0);
+    const char *e = std::getenv("LDPC_GNN_TRAIN_SPLIT");
+    return e && std::atoi(e) == 1;
 }
 
 int bwd_mfma() {
