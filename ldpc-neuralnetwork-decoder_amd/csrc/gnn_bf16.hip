@@ -430,7 +430,9 @@ struct MlpArgs {
     int tpf1;                            // projected: the leading tiles of degree-1 messages
     int d1;                              // degree-1 var groups use D1 (info.x < 0), layers >= 1
     int64_t B;
-    float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
+    float *msg_out;                      // last layer / early termination: (B, E) projected LLRs,
+    const int32_t *vpos;                 // ... stored variable-major: message m at vpos[m] (the
+                                         // position of m in the per-call CSR of msg_var)
     const uint8_t *active;               // early termination: frames still decoding (null = all)
     const int32_t *list, *count;         // early termination: the frames still decoding (see GmArgs)
     const float *kd_last, *bo_last;      // early termination: the last layer's output projection
@@ -444,6 +446,7 @@ struct TileIn {
     bool one;  // degree-1 var group (D1 constant instead of K[ty][var side])
     bool t1;   // projected: a tile of degree-1 messages (uniform over the wave)
     int64_t row, b;
+    int mpos;     // the message's slot in the variable-major msg_out row
     bool ok, on;  // on: the frame is still decoding (early termination)
 };
 
@@ -538,6 +541,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         I.t1 = proj && !layer0 && A.d1 && k < A.tpf1;
         I.row = bb * A.E + m;
         I.b = bb;
+        I.mpos = (!last && !A.kd_last) ? 0 : A.vpos[m];
         I.on = on;
         // A terminated frame (uniform over the tile) loads frame 0's rows instead of its own:
         // L2 hits, and no branch around the loads -- a branch here makes the compiler wait for
@@ -648,7 +652,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                 part = fmaf(y1[r], wo[32 + 16 * h + r], part);
             }
             part += __shfl_xor(part, 32, 64);
-            if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo[0];
+            if (I.ok && h == 0) A.msg_out[I.b * A.E + I.mpos] = part + A.bo[0];
         } else {
             if (A.kd_last) {  // early termination: project with the last layer's output head
                 const float *wo = tail + 128;
@@ -659,7 +663,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                     part = fmaf(y1[r], wo[32 + 16 * h + r], part);
                 }
                 part += __shfl_xor(part, 32, 64);
-                if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo_last[0];
+                if (I.ok && h == 0) A.msg_out[I.b * A.E + I.mpos] = part + A.bo_last[0];
             }
             if (!I.ok) return;
             char *xo = reinterpret_cast<char *>(A.x_out + I.row * H) + 16 * h;
@@ -736,76 +740,70 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
 // after layer `layer` < L - 1: bit_v = [llr_v + sum_{m -> v} (wo_L . x_m + bo_L) > 0] (the
 // decoder's P(bit = 1) > 0.5, message_gnn_decoder.py:298-307, with the last layer's head as the
 // output stage, :270); if every check group has even parity the frame is done: its probs are
-// written now, its layer count recorded, and every later kernel skips it.
+// written now, its layer count recorded, and every later kernel skips it.  A frame that goes on is
+// appended to out_list (one atomic per frame): the next layer's kernels walk that list, so no
+// separate compaction pass is needed (the list order varies run to run; no result depends on it).
 __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__restrict__ msg_out,
                                                                 const int32_t *__restrict__ csr, int64_t E,
                                                                 const float *__restrict__ llr, int N,
                                                                 const int32_t *__restrict__ cg_ptr,
-                                                                const int32_t *__restrict__ cg_mem, int Gc,
-                                                                const int32_t *__restrict__ msg_var, int layer,
+                                                                const int32_t *__restrict__ cg_var, int Gc, int layer,
                                                                 uint8_t *__restrict__ active,
                                                                 const int32_t *__restrict__ list,
                                                                 const int32_t *__restrict__ count,
-                                                                int32_t *__restrict__ iters, float *__restrict__ probs) {
-    extern __shared__ uint32_t bits[];
+                                                                int32_t *__restrict__ iters, float *__restrict__ probs,
+                                                                int32_t *__restrict__ out_list,
+                                                                int32_t *__restrict__ out_count) {
+    extern __shared__ uint32_t bits[];  // [(N + 31) / 32] decision bits, then zs [N]
+    float *zs = reinterpret_cast<float *>(bits + (N + 31) / 32);
     __shared__ int odd;
     if (count && (int)blockIdx.x >= *count) return;
     const int64_t b = list ? list[blockIdx.x] : blockIdx.x;
     if (!active[b]) return;
     const float *mo = msg_out + b * E, *lr = llr + b * N;
-    const int32_t *vptr = csr_ptr(csr), *vmem = csr_mem(csr, N);
-    auto z = [&](int v) {  // the output stage's own sum order (gnn_output)
-        float s = 0.0f;
-        for (int q = vptr[v]; q < vptr[v + 1]; ++q) s += mo[vmem[q]];
-        return s + lr[v];
-    };
+    const int32_t *vptr = csr_ptr(csr);
     for (int i = threadIdx.x; i < (N + 31) / 32; i += blockDim.x) bits[i] = 0u;
     if (threadIdx.x == 0) odd = 0;
     __syncthreads();
-    for (int v = threadIdx.x; v < N; v += blockDim.x)
-        if (z(v) > 0.0f) atomicOr(&bits[v >> 5], 1u << (v & 31));
+    for (int v = threadIdx.x; v < N; v += blockDim.x) {
+        float sum = 0.0f;  // the output stage's own sum order (gnn_output): msg_out is variable-major
+        for (int q = vptr[v]; q < vptr[v + 1]; ++q) sum += mo[q];
+        const float zv = sum + lr[v];
+        zs[v] = zv;
+        if (zv > 0.0f) atomicOr(&bits[v >> 5], 1u << (v & 31));
+    }
     __syncthreads();
     for (int g = threadIdx.x; g < Gc; g += blockDim.x) {
         uint32_t p = 0;
-        for (int q = cg_ptr[g]; q < cg_ptr[g + 1]; ++q) {
-            const int v = msg_var[cg_mem[q]];
+        for (int q = cg_ptr[g]; q < cg_ptr[g + 1]; ++q) {  // cg_var[q] = the variable of member q
+            const int v = cg_var[q];
             p ^= bits[v >> 5] >> (v & 31);
         }
         if (p & 1u) odd = 1;
     }
     __syncthreads();
-    if (odd) return;
+    if (odd) {  // still decoding: onto the next layer's list (any order: frames are independent)
+        if (out_list && threadIdx.x == 0) out_list[atomicAdd(out_count, 1)] = (int32_t)b;
+        return;
+    }
     if (threadIdx.x == 0) {
         active[b] = 0;
         if (iters) iters[b] = layer + 1;
     }
-    for (int v = threadIdx.x; v < N; v += blockDim.x) probs[b * N + v] = 1.0f / (1.0f + expf(-z(v)));
+    for (int v = threadIdx.x; v < N; v += blockDim.x) probs[b * N + v] = 1.0f / (1.0f + expf(-zs[v]));
 }
 
-// The frames still decoding, ascending: list[0 .. *count) (one workgroup; a block-wide scan per
-// 1024 frames).  The next layer's kernels walk only these.
-__global__ __launch_bounds__(1024) void gnn_bf16_compact_kernel(const uint8_t *__restrict__ active, int64_t nb,
-                                                                int32_t *__restrict__ list, int32_t *__restrict__ count) {
-    __shared__ int wsum[16];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    int base = 0;
-    for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
-        const int64_t f = c0 + tid;
-        const bool a = f < nb && active[f];
-        const uint64_t m = __ballot(a);
-        const int before = __popcll(m & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[w] = __popcll(m);
-        __syncthreads();
-        int off = 0, tot = 0;
-        for (int q = 0; q < 16; ++q) {
-            off += q < w ? wsum[q] : 0;
-            tot += wsum[q];
-        }
-        if (a) list[base + off + before] = (int32_t)f;
-        base += tot;
-        __syncthreads();
-    }
-    if (tid == 0) *count = base;
+// vpos[mem[q]] = q: each message's slot in the variable-major msg_out rows (mem = the CSR of msg_var)
+__global__ void gnn_bf16_vpos_kernel(const int32_t *__restrict__ csr, int N, int64_t E, int32_t *__restrict__ vpos) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < E) vpos[csr_mem(csr, N)[q]] = (int32_t)q;
+}
+
+// cg_var[q] = msg_var[cg_mem[q]]: the variable of every check-group member (syndrome tables)
+__global__ void gnn_bf16_cgvar_kernel(const int32_t *__restrict__ cg_mem, const int32_t *__restrict__ msg_var,
+                                      int64_t n, int32_t *__restrict__ cg_var) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) cg_var[q] = msg_var[cg_mem[q]];
 }
 
 __global__ void fill_i32_kernel(int32_t *p, int64_t n, int32_t v) {
@@ -815,7 +813,7 @@ __global__ void fill_i32_kernel(int32_t *p, int64_t n, int32_t v) {
 
 struct Bf16Ws {
     float *kd, *memb, *msg_out;
-    int32_t *csr, *alist, *acount;
+    int32_t *csr, *alist, *acount, *cg_var, *vpos;
     int4 *info;
     uint8_t *active;
     __bf16 *xa, *xb, *Mv, *Mc;
@@ -828,7 +826,7 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
     const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * p->E * 4);
     const int64_t inf = al(std::max<int64_t>(p->E, (int64_t)p->n_mtiles * 32) * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
-    const int64_t alb = al(B * 4) + 256;  // active list [B] + the two ranges' counts
+    const int64_t alb = al(2 * B * 4) + 256;  // two active lists [B] + the two ranges' two counts
     char *c = static_cast<char *>(base);
     Bf16Ws w;
     w.info = reinterpret_cast<int4 *>(c + kd + memb + xa + xb + mv + mc + vs);
@@ -842,8 +840,10 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     w.Mc = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb + mv);
     w.msg_out = reinterpret_cast<float *>(c + kd + memb + xa + xb + mv + mc);
     w.alist = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs);
-    w.acount = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + al(B * 4));
-    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb;
+    w.acount = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + al(2 * B * 4));
+    w.cg_var = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb);
+    w.vpos = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb + al(p->E * 4));
+    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb + 2 * al(p->E * 4);
     return w;
 }
 
@@ -903,7 +903,7 @@ int gnn_streams_bf16() {
 }
 
 // LDPC_GNN_ET_COMPACT=0: after a syndrome pass the kernels still walk every frame and skip the
-// finished ones (A/B); default: they walk the compacted list of frames still decoding
+// finished ones (A/B); default: they walk the list of frames still decoding that the pass appended
 int compact_env() {
     const char *e = std::getenv("LDPC_GNN_ET_COMPACT");  // read per call (tests toggle it)
     return e ? std::atoi(e) : 1;
@@ -975,11 +975,19 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
                        d_weights, T, L, d_msg_type, G, Gtot, w.memb);
     LDPC_CHECK_LAUNCH("gnn_bf16_memb_kernel");
     if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
+    hipLaunchKernelGGL(gnn_bf16_vpos_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, w.csr, N, p->E,
+                       w.vpos);
+    LDPC_CHECK_LAUNCH("gnn_bf16_vpos_kernel");
     if (d_iters) {
         hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, d_iters, B, L);
         LDPC_CHECK_LAUNCH("fill_i32_kernel");
     }
-    if (et) LDPC_HIP(hipMemsetAsync(w.active, 1, (size_t)B, s));
+    if (et) {
+        LDPC_HIP(hipMemsetAsync(w.active, 1, (size_t)B, s));
+        hipLaunchKernelGGL(gnn_bf16_cgvar_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, p->cg_mem,
+                           d_msg_var, p->E, w.cg_var);
+        LDPC_CHECK_LAUNCH("gnn_bf16_cgvar_kernel");
+    }
     const uint8_t *active = et ? w.active : nullptr;
     const float *kd_last = w.kd + (int64_t)(L - 1) * kd_floats(T);
     const float *bo_last = layer_w(d_weights, T, L - 1).bo;
@@ -988,7 +996,11 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     auto run_range = [&](int64_t b0, int64_t nb, hipStream_t st, int slot) -> int {
     const int64_t xoff = b0 * p->E * H;
     uint8_t *act = et ? w.active + b0 : nullptr;
-    int32_t *alist = w.alist + b0, *acount = w.acount + slot;
+    // active lists: the syndrome pass after layer l appends the frames still decoding to one list
+    // while the layer walked the other (double-buffered, counts zeroed before each pass)
+    int32_t *lists[2] = {w.alist + b0, w.alist + B + b0}, *counts[2] = {w.acount + 2 * slot, w.acount + 2 * slot + 1};
+    int cur = 0;
+    int32_t *alist = lists[0], *acount = counts[0];
     bool listed = false;  // after the first syndrome pass the kernels walk the active list
     const __bf16 *x_in = nullptr;
     for (int l = 0; l < L; ++l) {
@@ -1071,6 +1083,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.d1 = d1 ? 1 : 0;
         m.B = nb;
         m.msg_out = w.msg_out + b0 * p->E;
+        m.vpos = w.vpos;
         m.active = act;
         m.list = listed ? alist : nullptr;
         m.count = listed ? acount : nullptr;
@@ -1081,14 +1094,18 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         if (rc != LDPC_OK) return rc;
         LDPC_CHECK_LAUNCH("gnn_bf16_mlp_kernel");
         if (m.kd_last) {
-            hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)nb), dim3(256), (size_t)(N + 31) / 32 * 4, st,
-                               w.msg_out + b0 * p->E, w.csr, p->E, d_llr + b0 * N, N, p->cg_ptr, p->cg_mem, p->Gc,
-                               d_msg_var, l, act, listed ? alist : nullptr, listed ? acount : nullptr,
-                               d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N);
+            const bool cmp = compact_env();
+            int32_t *olist = lists[cur ^ 1], *ocount = counts[cur ^ 1];
+            if (cmp) LDPC_HIP(hipMemsetAsync(ocount, 0, 4, st));
+            hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)nb), dim3(256),
+                               (size_t)((N + 31) / 32 + N) * 4, st, w.msg_out + b0 * p->E, w.csr, p->E,
+                               d_llr + b0 * N, N, p->cg_ptr, w.cg_var, p->Gc, l, act, listed ? alist : nullptr, listed ? acount : nullptr,
+                               d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N, cmp ? olist : nullptr, ocount);
             LDPC_CHECK_LAUNCH("gnn_bf16_syndrome_kernel");
-            if (compact_env()) {
-                hipLaunchKernelGGL(gnn_bf16_compact_kernel, dim3(1), dim3(1024), 0, st, act, nb, alist, acount);
-                LDPC_CHECK_LAUNCH("gnn_bf16_compact_kernel");
+            if (cmp) {
+                cur ^= 1;
+                alist = olist;
+                acount = ocount;
                 listed = true;
             }
         }
@@ -1110,7 +1127,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     } else if (int rc = run_range(0, B, s, 0)) {
         return rc;
     }
-    return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s);
+    return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s, true);
 }
 
 }  // namespace ldpc
