@@ -791,8 +791,8 @@ constexpr int kS6Img = 64 * kS6Row;                                // bf16 per s
 constexpr int kS6OffW2 = 6 * kS6Img;                               // W1L (side, split), then W2
 constexpr int kS6Bytes = 12 * kS6Img * 2;                          // 12 images
 constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo
-constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][64]
-inline size_t mlp2s_lds_bytes(int T) { return (size_t)(kS6OffEmb + T * 64) * 4; }
+constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][kPS]
+inline size_t mlp2s_lds_bytes(int T) { return (size_t)(kS6OffEmb + T * kPS) * 4; }
 
 template <int NT, int WPS, bool HYB = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
@@ -811,7 +811,9 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         lds[kS6OffB + 64 + tid] = P.b2c[tid];
         lds[kS6OffB + 128 + tid] = P.last ? P.wo[tid] : 0.0f;
     }
-    for (int i = tid; i < P.T * 64; i += NT) lds[kS6OffEmb + i] = P.emb[i];
+    // emb rows kPS = 68 floats apart: lanes of different types read different rows (64 apart, every
+    // row would sit on the same banks)
+    for (int i = tid; i < P.T * 64; i += NT) lds[kS6OffEmb + (i >> 6) * kPS + (i & 63)] = P.emb[i];
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
@@ -852,7 +854,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                     x[s][i] = l * P.w_in[u] + P.b_in[u];
                 }
         }
-        const float *e = lds + kS6OffEmb + P.msg_type[m] * 64;
+        const float *e = lds + kS6OffEmb + P.msg_type[m] * kPS;
         const float *pv = P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
         const float *pc = P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
         f32x16 y0 = {}, y1 = {};

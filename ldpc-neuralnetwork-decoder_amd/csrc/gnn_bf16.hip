@@ -412,8 +412,14 @@ constexpr int kOffK = 2 * kW1B + 2 * kW2B;
 constexpr int kPOffW1v = 0, kPOffW1c = kW2B, kPOffW1s = 2 * kW2B, kPOffW2v = 3 * kW2B, kPOffW2c = 4 * kW2B;
 constexpr int kPOffK = 5 * kW2B;
 constexpr int kKStride = 132;
+// D1 rows: 68 floats apart (a row stride of 64 put every type's row on the same LDS banks: the
+// 16-lane groups of a ds_read_b128 with lanes of different types serialised up to 16-way)
+#ifndef LDPC_BF16_D1_STRIDE
+#define LDPC_BF16_D1_STRIDE 68
+#endif
+constexpr int kD1Stride = LDPC_BF16_D1_STRIDE;
 inline size_t mlp_lds_bytes(int T, bool d1, bool proj) {
-    return (size_t)(proj ? kPOffK : kOffK) + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * 64 : 0)) * 4;
+    return (size_t)(proj ? kPOffK : kOffK) + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * kD1Stride : 0)) * 4;
 }
 
 struct MlpArgs {
@@ -491,9 +497,9 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     float *tail = Ks + (A.T + 2) * kKStride;  // b2 [64], wo [64]
     if (tid < 128) tail[tid] = A.kd[nk + tid];
     if (A.kd_last && tid < 64) tail[128 + tid] = A.kd_last[nk + 64 + tid];  // wo of the last layer
-    float *D1s = tail + 192;  // D1 [T][64]
+    float *D1s = tail + 192;  // D1 [T][kD1Stride]
     if (A.d1)
-        for (int i = tid; i < A.T * 64; i += NT) D1s[i] = A.kd[nk + 128 + i];
+        for (int i = tid; i < A.T * 64; i += NT) D1s[(i >> 6) * kD1Stride + (i & 63)] = A.kd[nk + 128 + i];
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
@@ -591,7 +597,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
             const char *W1 = smem + (side == 0 ? (proj && I.t1 ? kPOffW1s : oW1v) : oW1c);
             const char *W2 = smem + (side == 0 ? oW2v : oW2c);
             const bool d1k = proj ? I.t1 : I.one;
-            const float *K0 = side == 0 && d1k ? D1s + I.ty * 64 : Kt + side * 64;
+            const float *K0 = side == 0 && d1k ? D1s + I.ty * kD1Stride : Kt + side * 64;
             f32x16 h0 = ld16(K0 + 16 * h), h1 = ld16(K0 + 32 + 16 * h);
             if (proj && !(side == 0 && I.t1)) {  // + the group's W1_right g row (bf16)
                 const bf16x8 *P = side == 0 ? I.af : I.cf;
