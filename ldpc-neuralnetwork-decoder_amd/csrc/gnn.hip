@@ -794,7 +794,9 @@ constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2
 constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][kPS]
 inline size_t mlp2s_lds_bytes(int T) { return (size_t)(kS6OffEmb + T * kPS) * 4; }
 
-template <int NT, int WPS, bool HYB = false>
+// PF (LDPC_MLP2S_PF=1 builds, with 2 waves per SIMD): the next tile's feature rows are loaded
+// while the current tile computes (32 more VGPRs); layer 0 and the hybrid decoder's rows are not
+template <int NT, int WPS, bool HYB = false, bool PF = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __bf16 *img = reinterpret_cast<__bf16 *>(lds);
@@ -822,6 +824,20 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     const float bo = P.last ? P.bo[0] : 0.0f;
     const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
     const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
+    constexpr bool pf = PF && !HYB;
+    auto load_x = [&](int64_t t, float (&xo)[4][8]) {
+        const int64_t row = t * 32 + j;
+        const float *xr = P.x_in + (row < R ? row : R - 1) * 64 + 4 * half;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float4 v = *reinterpret_cast<const float4 *>(xr + 32 * (s >> 1) + 16 * (s & 1) + 8 * q);
+                xo[s][4 * q] = v.x; xo[s][4 * q + 1] = v.y; xo[s][4 * q + 2] = v.z; xo[s][4 * q + 3] = v.w;
+            }
+    };
+    float xnext[4][8];
+    if (pf && P.x_in && tw.first < tw.end) load_x(tw.first, xnext);
     for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
         const int64_t row = t * 32 + j;
         const bool ok = row < R;
@@ -829,7 +845,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         const int64_t b = rr / P.E, m = rr - b * P.E;
         // x[s][i] = feature pi16(16 s + 8 h + i) before the type embedding (float4 pairs)
         float x[4][8];
-        if (P.x_in) {
+        if (pf && P.x_in) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) x[s][i] = xnext[s][i];
+            if (t + tw.stride < tw.end) load_x(t + tw.stride, xnext);
+        } else if (P.x_in) {
             const float *xr = P.x_in + rr * 64 + 4 * half;
             const float hv = HYB && P.hv2c ? P.hv2c[rr] : 0.0f;
 #pragma unroll
@@ -1140,6 +1162,9 @@ constexpr int kMlp2Wps = LDPC_MLP2_WPS, kMlp2Nt = LDPC_MLP2_NT;
 #endif
 #ifndef LDPC_MLP2S_NT
 #define LDPC_MLP2S_NT 768
+#endif
+#ifndef LDPC_MLP2S_PF
+#define LDPC_MLP2S_PF 0
 #endif
 constexpr int kMlp2sWps = LDPC_MLP2S_WPS, kMlp2sNt = LDPC_MLP2S_NT;
 // LDPC_GNN_SPLIT=0: the projected-group MLP on v_mfma_f32_32x32x2_f32 (gnn_mlp2_kernel); default:
@@ -1537,7 +1562,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
-        LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps>)
+        LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, LDPC_MLP2S_PF != 0>)
                                            : reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
     }
@@ -1587,7 +1612,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             constexpr int wpb = kMlp2Nt / 64;
             const unsigned grid = (unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu);
             if (split)
-                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps>),
+                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, LDPC_MLP2S_PF != 0>),
                                    dim3((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus)),
                                    dim3(kMlp2sNt), mlp2_lds, st, L);
             else
