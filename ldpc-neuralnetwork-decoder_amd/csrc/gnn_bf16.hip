@@ -535,7 +535,24 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         for (int s = 0; s < 4; ++s) X.v[s] = ld8(xr + 32 * s);
         return X;
     };
-    auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k, const XRows *xpre = nullptr) {
+    // the group rows of tile t alone (PF 3 issues them a tile before the rest of the tile's loads)
+    struct GRows { bf16x8 a[4], c[4]; };
+    auto load_g = [&](const int4 &inf, bool on, int64_t t, int64_t b) {
+        GRows G;
+        const int64_t lb = on ? frame_of(t < tw.end ? b : fb) : 0;
+        const int vg = inf.x < 0 ? ~inf.x : inf.x;
+        const char *ma = reinterpret_cast<const char *>(A.Mv + (lb * A.Gv + vg) * H) + 16 * h;
+        const char *mc = reinterpret_cast<const char *>(A.Mc + (lb * A.Gc + inf.y) * H) + 16 * h;
+        if (layer0 || !A.d1 || inf.x >= 0) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) G.a[s] = ld8(ma + 32 * s);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) G.c[s] = ld8(mc + 32 * s);
+        return G;
+    };
+    auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k, const XRows *xpre = nullptr,
+                    const GRows *gpre = nullptr) {
         TileIn I;
         const int m0 = (int)k * 32 + j;
         I.ok = (proj ? inf.w >= 0 : m0 < A.E) && t < tw.end;
@@ -568,6 +585,15 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
             I.l = 0.0f;
         } else {
             I.l = A.llr[lb * A.N + I.var];
+        }
+        if (gpre) {  // PF 3: the group rows came two tiles ahead
+            const bool own = layer0 || !A.d1 || inf.x >= 0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                I.af[s] = own ? gpre->a[s] : I.xf[s];
+                I.cf[s] = gpre->c[s];
+            }
+            return I;
         }
         if constexpr (proj) {
             if (!I.t1) {  // degree-1 tiles need no W1_right g row (D1 + W1v,left+right x)
@@ -704,6 +730,29 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
             on_n = on_nn;
             nb = nb2;
             nk = nk2;
+        }
+    } else if constexpr (PF == 3 && !proj) {
+        // group rows (L2 gathers) two tiles ahead, message info three, feature rows one
+        TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
+        int64_t b1 = fb + sb, k1 = fk + sk;
+        if (k1 >= A.tpf) { k1 -= A.tpf; ++b1; }
+        int64_t b2 = b1 + sb, k2 = k1 + sk;
+        if (k2 >= A.tpf) { k2 -= A.tpf; ++b2; }
+        int4 inf1 = load_info(k1), inf2 = load_info(k2);
+        bool on1 = load_on(tw.first + tw.stride, b1), on2 = load_on(tw.first + 2 * tw.stride, b2);
+        GRows g1 = load_g(inf1, on1, tw.first + tw.stride, b1);
+        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+            int64_t b3 = b2 + sb, k3 = k2 + sk;
+            if (k3 >= A.tpf) { k3 -= A.tpf; ++b3; }
+            const int4 inf3 = load_info(k3);
+            const bool on3 = load_on(t + 3 * tw.stride, b3);
+            const GRows g2 = load_g(inf2, on2, t + 2 * tw.stride, b2);
+            const TileIn nxt = load(inf1, on1, t + tw.stride, b1, k1, nullptr, &g1);
+            compute(cur);
+            cur = nxt;
+            g1 = g2;
+            inf1 = inf2; on1 = on2; b1 = b2; k1 = k2;
+            inf2 = inf3; on2 = on3; b2 = b3; k2 = k3;
         }
     } else if constexpr (PF != 0) {
         // rows are prefetched one tile ahead; the small per-tile items (message info, frame
@@ -885,7 +934,7 @@ int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpAr
 //   2 = 512 threads, 4 waves/SIMD, no prefetch (spills at 128 VGPRs)
 //   3 = 512 threads, 2 waves/SIMD, prefetch: one workgroup (one LDS weight copy) per CU
 //   4 = 768 threads, 3 waves/SIMD, prefetch; 5 = 1024 threads, 4 waves/SIMD, no prefetch
-//   6 = as 1, feature rows two tiles ahead (PF 2)
+//   6 = as 1, feature rows two tiles ahead (PF 2); 7 = as 1, group rows two tiles ahead (PF 3)
 int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (variant) {
         case 0: return launch_mlp_v<768, 3, 0>(mode, tiles, lds, s, m);
@@ -894,6 +943,7 @@ int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, 
         case 4: return launch_mlp_v<768, 3, 1>(mode, tiles, lds, s, m);
         case 5: return launch_mlp_v<1024, 4, 0>(mode, tiles, lds, s, m);
         case 6: return launch_mlp_v<256, 2, 2>(mode, tiles, lds, s, m);
+        case 7: return launch_mlp_v<256, 2, 3>(mode, tiles, lds, s, m);
         default: return launch_mlp_v<256, 2, 1>(mode, tiles, lds, s, m);
     }
 }
