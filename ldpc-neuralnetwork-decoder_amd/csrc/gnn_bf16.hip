@@ -461,7 +461,8 @@ struct TileIn {
 // (GEMM1 over x only, started from K + the group's W1_right g row; tiles in the plan's message
 // order, whose degree-1 tiles run GEMM1 over x with W1v,left + W1v,right and D1)
 // PF: 0 no register prefetch; 1 the next tile's rows one tile ahead; 2 (non-projected, layers >= 1)
-// as 1, and the feature rows -- the HBM part of a tile -- two tiles ahead
+// as 1, and the feature rows -- the HBM part of a tile -- two tiles ahead; 3 as 1, the group rows
+// two tiles ahead; 4 as 1, both sides' GEMM1 before either GEMM2
 template <int NT, int WPS, int PF, int MODE>
 __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -618,13 +619,15 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         f32x16 y0 = ld16(tail + 16 * h), y1 = ld16(tail + 32 + 16 * h);  // b2v + b2c
         int wbase = j * w1row + 16 * h, w2base = j * 144 + 16 * h;
         asm volatile("" : "+v"(wbase), "+v"(w2base));
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
+        // GEMM1 of one side into (h0, h1), then ReLU + GEMM2 into y.  PF 4 runs both sides' GEMM1
+        // before either GEMM2, so one side's ReLU can issue beside the other side's MFMAs (the
+        // same operations in the same order per accumulator: bitwise the same result)
+        auto gemm1 = [&](int side, f32x16 &h0, f32x16 &h1) {
             const char *W1 = smem + (side == 0 ? (proj && I.t1 ? kPOffW1s : oW1v) : oW1c);
-            const char *W2 = smem + (side == 0 ? oW2v : oW2c);
             const bool d1k = proj ? I.t1 : I.one;
             const float *K0 = side == 0 && d1k ? D1s + I.ty * kD1Stride : Kt + side * 64;
-            f32x16 h0 = ld16(K0 + 16 * h), h1 = ld16(K0 + 32 + 16 * h);
+            h0 = ld16(K0 + 16 * h);
+            h1 = ld16(K0 + 32 + 16 * h);
             if (proj && !(side == 0 && I.t1)) {  // + the group's W1_right g row (bf16)
                 const bf16x8 *P = side == 0 ? I.af : I.cf;
 #pragma unroll
@@ -657,6 +660,9 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                     h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * (4 + s)), g, h1, 0, 0, 0);
                 }
             }
+        };
+        auto gemm2 = [&](int side, const f32x16 &h0, const f32x16 &h1) {
+            const char *W2 = smem + (side == 0 ? oW2v : oW2c);
             const bf16x8 p00 = relu8(h0, 0), p01 = relu8(h0, 1), p10 = relu8(h1, 0), p11 = relu8(h1, 1);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -664,6 +670,20 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                 const int qb = w2base + 32 * q;
                 y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W2 + qb), bop, y0, 0, 0, 0);
                 y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W2 + 32 * 144 + qb), bop, y1, 0, 0, 0);
+            }
+        };
+        if constexpr (PF == 4) {
+            f32x16 hv0, hv1, hc0, hc1;
+            gemm1(0, hv0, hv1);
+            gemm1(1, hc0, hc1);
+            gemm2(0, hv0, hv1);
+            gemm2(1, hc0, hc1);
+        } else {
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                f32x16 h0, h1;
+                gemm1(side, h0, h1);
+                gemm2(side, h0, h1);
             }
         }
         if constexpr (!layer0) {  // residual (message_gnn_decoder.py:261): chunk s <-> y_{s>>1}[8 (s&1) ..]
@@ -935,6 +955,7 @@ int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpAr
 //   3 = 512 threads, 2 waves/SIMD, prefetch: one workgroup (one LDS weight copy) per CU
 //   4 = 768 threads, 3 waves/SIMD, prefetch; 5 = 1024 threads, 4 waves/SIMD, no prefetch
 //   6 = as 1, feature rows two tiles ahead (PF 2); 7 = as 1, group rows two tiles ahead (PF 3)
+//   8 = as 1, both sides' GEMM1 before either GEMM2 (PF 4)
 int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (variant) {
         case 0: return launch_mlp_v<768, 3, 0>(mode, tiles, lds, s, m);
@@ -944,6 +965,7 @@ int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, 
         case 5: return launch_mlp_v<1024, 4, 0>(mode, tiles, lds, s, m);
         case 6: return launch_mlp_v<256, 2, 2>(mode, tiles, lds, s, m);
         case 7: return launch_mlp_v<256, 2, 3>(mode, tiles, lds, s, m);
+        case 8: return launch_mlp_v<256, 2, 4>(mode, tiles, lds, s, m);
         default: return launch_mlp_v<256, 2, 1>(mode, tiles, lds, s, m);
     }
 }

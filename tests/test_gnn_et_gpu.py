@@ -85,7 +85,7 @@ def test_fp32_early_termination_is_refused(cuda):
         _run(dec, conv, base, 4, llr, True)
 
 
-@pytest.mark.parametrize("variant", ["0", "6", "7"])
+@pytest.mark.parametrize("variant", ["0", "6", "7", "8"])
 @pytest.mark.parametrize("et", [False, True])
 def test_mlp_variants_are_bitwise_equal(cuda, monkeypatch, variant, et):
     """The bf16 MLP kernel's occupancy / prefetch variants (LDPC_GNN_BF16_MLP: 1 default, 0 = 3
