@@ -889,10 +889,18 @@ __global__ __launch_bounds__(256) void train_outer_kernel(OuterT P) {
 // accumulator register is two 128-B row segments: the full-rate atomic shape).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int NIT, int NJT>
+// LDPC_GNN_OUTER_H64=0: the general weight-gradient kernels for H = 64 too (A/B); read per call
+int outer_h64() {
+    const char *e = std::getenv("LDPC_GNN_OUTER_H64");
+    return !(e && std::atoi(e) == 0);
+}
+
+// H64: H = 64 and J = 64 or 128 from zsrc (+ zsrc2): no per-load bounds or source checks (the
+// column tile decides the source at compile time)
+template <int NIT, int NJT, bool H64 = false>
 __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     const int lane = threadIdx.x & 63, col = lane & 31, k = lane >> 5;
-    const int H = P.H, J = P.J;
+    const int H = H64 ? 64 : P.H, J = H64 ? 32 * NJT : P.J;
     const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t per = ((P.R + nw - 1) / nw + 1) & ~1LL;  // even: whole k-steps
     const int64_t r_begin = w * per, r_end = r_begin + per < P.R ? r_begin + per : P.R;
@@ -903,6 +911,7 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
         for (int jt = 0; jt < NJT; ++jt) acc[it][jt] = f32x16{};
     float bsum[NIT] = {};
     auto zval = [&](int64_t r, int64_t b, int64_t m, int j) -> float {
+        if constexpr (H64) return j < 64 ? P.zsrc[r * 64 + j] : P.zsrc2[r * 64 + (j - 64)];
         if (j >= J) return 0.0f;
         if (j < H) return P.zsrc[r * H + j];
         if (P.zsrc2) return P.zsrc2[r * H + (j - H)];
@@ -924,7 +933,7 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
                 const int i = 32 * it + col;
-                a[u][it] = ok && i < H ? P.A[r * H + i] : 0.0f;
+                a[u][it] = ok && (H64 || i < H) ? P.A[r * H + i] : 0.0f;
             }
 #pragma unroll
             for (int jt = 0; jt < NJT; ++jt) z[u][jt] = ok ? zval(r, bu, mu, 32 * jt + col) : 0.0f;
@@ -974,7 +983,11 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
 
 int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
     const int nit = (o.H + 31) / 32, njt = (o.J + 31) / 32;
-    if (nit == 2 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4>), dim3(grid), dim3(256), 0, s, o);
+    // H = 64 from plain row sources: the specialised kernels (no per-load source / bounds checks)
+    const bool h64 = o.H == 64 && !o.G && ((o.J == 128 && o.zsrc2) || (o.J == 64 && !o.zsrc2)) && outer_h64();
+    if (h64 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4, true>), dim3(grid), dim3(256), 0, s, o);
+    else if (h64 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2, true>), dim3(grid), dim3(256), 0, s, o);
+    else if (nit == 2 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4>), dim3(grid), dim3(256), 0, s, o);
     else if (nit == 2 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2>), dim3(grid), dim3(256), 0, s, o);
     else if (nit == 1 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<1, 2>), dim3(grid), dim3(256), 0, s, o);
     else if (nit == 1 && njt == 1) hipLaunchKernelGGL((train_outer_mfma_kernel<1, 1>), dim3(grid), dim3(256), 0, s, o);
