@@ -889,6 +889,9 @@ __global__ __launch_bounds__(256) void train_outer_kernel(OuterT P) {
 // accumulator register is two 128-B row segments: the full-rate atomic shape).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+#ifndef LDPC_OUTER_PIPE_MIN_NJT
+#define LDPC_OUTER_PIPE_MIN_NJT 2
+#endif
 // LDPC_GNN_OUTER_H64=0: the general weight-gradient kernels for H = 64 too (A/B); read per call
 int outer_h64() {
     const char *e = std::getenv("LDPC_GNN_OUTER_H64");
@@ -922,33 +925,57 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     // KU k-steps (2 KU rows) of fragments are loaded before their MFMAs, so each wave keeps
     // 2 KU (NIT + NJT) independent loads in flight instead of waiting on one k-step at a time
     constexpr int KU = 8;
-    for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * KU) {
-        float a[KU][NIT], z[KU][NJT];
+    struct Batch { float a[KU][NIT], z[KU][NJT]; };
+    auto load_batch = [&](int64_t r0, Batch &B) {
 #pragma unroll
         for (int u = 0; u < KU; ++u) {
             const int64_t r = r0 + 2 * u + k;
             const bool ok = r < r_end;
             int64_t bu = bb, mu = mm + 2 * u;
-            while (mu >= P.E) { mu -= P.E; ++bu; }
+            if constexpr (!H64)
+                while (mu >= P.E) { mu -= P.E; ++bu; }
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
                 const int i = 32 * it + col;
-                a[u][it] = ok && (H64 || i < H) ? P.A[r * H + i] : 0.0f;
+                B.a[u][it] = ok && (H64 || i < H) ? P.A[r * H + i] : 0.0f;
             }
 #pragma unroll
-            for (int jt = 0; jt < NJT; ++jt) z[u][jt] = ok ? zval(r, bu, mu, 32 * jt + col) : 0.0f;
+            for (int jt = 0; jt < NJT; ++jt) B.z[u][jt] = ok ? zval(r, bu, mu, 32 * jt + col) : 0.0f;
         }
-        mm += 2 * KU;
-        while (mm >= P.E) { mm -= P.E; ++bb; }
+        if constexpr (!H64) {
+            mm += 2 * KU;
+            while (mm >= P.E) { mm -= P.E; ++bb; }
+        }
+    };
+    auto mfma_batch = [&](const Batch &B) {
 #pragma unroll
         for (int u = 0; u < KU; ++u)
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
-                bsum[it] += a[u][it];
+                bsum[it] += B.a[u][it];
 #pragma unroll
                 for (int jt = 0; jt < NJT; ++jt)
-                    acc[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][it], z[u][jt], acc[it][jt], 0, 0, 0);
+                    acc[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(B.a[u][it], B.z[u][jt], acc[it][jt], 0, 0, 0);
             }
+    };
+    if constexpr (H64 && NJT >= LDPC_OUTER_PIPE_MIN_NJT) {
+        // software-pipelined: the next batch's rows load while this batch's MFMAs run
+        if (r_begin < r_end) {
+            Batch cur;
+            load_batch(r_begin, cur);
+            for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * KU) {
+                Batch nxt;
+                if (r0 + 2 * KU < r_end) load_batch(r0 + 2 * KU, nxt);
+                mfma_batch(cur);
+                cur = nxt;
+            }
+        }
+    } else {
+        for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * KU) {
+            Batch cur;
+            load_batch(r0, cur);
+            mfma_batch(cur);
+        }
     }
     // D[i][j]: register q of lane l holds i = 8 (q >> 2) + 4 k + (q & 3), j = col.  The four waves'
     // tiles are summed in LDS first, so each workgroup issues one global atomic per gradient entry
