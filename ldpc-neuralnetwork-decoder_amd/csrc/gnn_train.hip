@@ -1008,11 +1008,108 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     if (P.bias2 && threadIdx.x < H) atomicAdd(&P.bias2[threadIdx.x], bred[threadIdx.x]);
 }
 
+// dW2 of both sides in one pass (H = 64, J = 128: Z = [h_v | h_c]) with the fp32 products as bf16x6
+// splits on v_mfma_f32_32x32x16_bf16 (gnn.hpp split3): K = 16 rows per MFMA step, lane (i, half)
+// holding rows r0 + 8 half .. + 7 of column 32 it + i (A) / 32 jt + i (Z); 6 x 32 instead of
+// 8 x 64 MFMA cycles per 16 rows.  Same reduction epilogue as train_outer_mfma_kernel.
+__global__ __launch_bounds__(256, 2) void train_outer_split_kernel(OuterT P) {
+    constexpr int NIT = 2, NJT = 4;
+    const int lane = threadIdx.x & 63, col = lane & 31, hf = lane >> 5;
+    const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t per = ((P.R + nw - 1) / nw + 15) & ~15LL;  // whole 16-row steps
+    const int64_t r_begin = w * per, r_end = r_begin + per < P.R ? r_begin + per : P.R;
+    f32x16 acc[NIT][NJT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it)
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt) acc[it][jt] = f32x16{};
+    float bsum[NIT] = {};
+    struct Step { float a[NIT][8], z[NJT][8]; };
+    auto load = [&](int64_t r0, Step &S) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int64_t r = r0 + 8 * hf + q;
+            const bool ok = r < r_end;
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) S.a[it][q] = ok ? P.A[r * 64 + 32 * it + col] : 0.0f;
+#pragma unroll
+            for (int jt = 0; jt < NJT; ++jt)
+                S.z[jt][q] = ok ? (jt < 2 ? P.zsrc[r * 64 + 32 * jt + col] : P.zsrc2[r * 64 + 32 * (jt - 2) + col]) : 0.0f;
+        }
+    };
+    auto step = [&](const Step &S) {
+        bf16x8_t as[NIT][3];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bsum[it] += S.a[it][q];
+            split3(S.a[it], as[it][0], as[it][1], as[it][2]);
+        }
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt) {  // one column tile's Z split live at a time
+            bf16x8_t z0, z1, z2;
+            split3(S.z[jt], z0, z1, z2);
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                f32x16 c = acc[it][jt];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as[it][2], z0, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as[it][1], z1, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as[it][0], z2, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as[it][1], z0, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as[it][0], z1, c, 0, 0, 0);
+                acc[it][jt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as[it][0], z0, c, 0, 0, 0);
+            }
+        }
+    };
+    if (r_begin < r_end) {
+        Step cur;
+        load(r_begin, cur);
+        for (int64_t r0 = r_begin; r0 < r_end; r0 += 16) {
+            Step nxt;
+            if (r0 + 16 < r_end) load(r0 + 16, nxt);
+            step(cur);
+            cur = nxt;
+        }
+    }
+    // D[i][j]: register q of lane l holds i = 8 (q >> 2) + 4 hf + (q & 3), j = col (as the fp32 kernel)
+    __shared__ float red[NIT * 32 * NJT * 32], bred[NIT * 32];
+    for (int e = threadIdx.x; e < NIT * 32 * NJT * 32; e += 256) red[e] = 0.0f;
+    if (threadIdx.x < NIT * 32) bred[threadIdx.x] = 0.0f;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+#pragma unroll
+        for (int jt = 0; jt < NJT; ++jt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int i = 32 * it + 8 * (q >> 2) + 4 * hf + (q & 3);
+                atomicAdd(&red[i * (NJT * 32) + 32 * jt + col], acc[it][jt][q]);
+            }
+        const float sm = bsum[it] + __shfl_xor(bsum[it], 32, 64);
+        if (hf == 0) atomicAdd(&bred[32 * it + col], sm);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NIT * 32 * NJT * 32; e += 256) {
+        const int i = e / (NJT * 32), j = e - i * (NJT * 32);
+        if (j >= 64) atomicAdd(&P.out2[i * 64 + (j - 64)], red[e]);
+        else atomicAdd(&P.out[i * (P.ld ? P.ld : 128) + P.col0 + j], red[e]);
+    }
+    if (P.bias && threadIdx.x < 64) atomicAdd(&P.bias[threadIdx.x], bred[threadIdx.x]);
+    if (P.bias2 && threadIdx.x < 64) atomicAdd(&P.bias2[threadIdx.x], bred[threadIdx.x]);
+}
+
+// LDPC_GNN_OUTER_SPLIT=0: dW2 on the fp32 MFMA (train_outer_mfma_kernel<2, 4, true>); read per call
+int outer_split() {
+    const char *e = std::getenv("LDPC_GNN_OUTER_SPLIT");
+    return !(e && std::atoi(e) == 0);
+}
+
 int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
     const int nit = (o.H + 31) / 32, njt = (o.J + 31) / 32;
     // H = 64 from plain row sources: the specialised kernels (no per-load source / bounds checks)
     const bool h64 = o.H == 64 && !o.G && ((o.J == 128 && o.zsrc2) || (o.J == 64 && !o.zsrc2)) && outer_h64();
-    if (h64 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4, true>), dim3(grid), dim3(256), 0, s, o);
+    if (h64 && njt == 4 && outer_split()) hipLaunchKernelGGL(train_outer_split_kernel, dim3(grid), dim3(256), 0, s, o);
+    else if (h64 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4, true>), dim3(grid), dim3(256), 0, s, o);
     else if (h64 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2, true>), dim3(grid), dim3(256), 0, s, o);
     else if (nit == 2 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4>), dim3(grid), dim3(256), 0, s, o);
     else if (nit == 2 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2>), dim3(grid), dim3(256), 0, s, o);
