@@ -828,7 +828,7 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
                                                                 const int32_t *__restrict__ count,
                                                                 int32_t *__restrict__ iters, float *__restrict__ probs,
                                                                 int32_t *__restrict__ out_list,
-                                                                int32_t *__restrict__ out_count) {
+                                                                int32_t *__restrict__ out_count, int vm) {
     extern __shared__ uint32_t bits[];  // [(N + 31) / 32] decision bits, then zs [N]
     float *zs = reinterpret_cast<float *>(bits + (N + 31) / 32);
     __shared__ int odd;
@@ -836,13 +836,13 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
     const int64_t b = list ? list[blockIdx.x] : blockIdx.x;
     if (!active[b]) return;
     const float *mo = msg_out + b * E, *lr = llr + b * N;
-    const int32_t *vptr = csr_ptr(csr);
+    const int32_t *vptr = csr_ptr(csr), *vmem = csr_mem(csr, N);
     for (int i = threadIdx.x; i < (N + 31) / 32; i += blockDim.x) bits[i] = 0u;
     if (threadIdx.x == 0) odd = 0;
     __syncthreads();
     for (int v = threadIdx.x; v < N; v += blockDim.x) {
         float sum = 0.0f;  // the output stage's own sum order (gnn_output): msg_out is variable-major
-        for (int q = vptr[v]; q < vptr[v + 1]; ++q) sum += mo[q];
+        for (int q = vptr[v]; q < vptr[v + 1]; ++q) sum += mo[vm ? q : vmem[q]];
         const float zv = sum + lr[v];
         zs[v] = zv;
         if (zv > 0.0f) atomicOr(&bits[v >> 5], 1u << (v & 31));
@@ -869,9 +869,19 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
 }
 
 // vpos[mem[q]] = q: each message's slot in the variable-major msg_out rows (mem = the CSR of msg_var)
-__global__ void gnn_bf16_vpos_kernel(const int32_t *__restrict__ csr, int N, int64_t E, int32_t *__restrict__ vpos) {
+__global__ void gnn_bf16_vpos_kernel(const int32_t *__restrict__ csr, int N, int64_t E, int32_t *__restrict__ vpos,
+                                     int vm) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < E) vpos[csr_mem(csr, N)[q]] = (int32_t)q;
+    if (q < E) {
+        if (vm) vpos[csr_mem(csr, N)[q]] = (int32_t)q;
+        else vpos[q] = (int32_t)q;  // message order
+    }
+}
+
+// LDPC_GNN_MSGOUT_VM=0: msg_out rows in message order (A/B); default variable-major.  Read per call.
+int msgout_vm() {
+    const char *e = std::getenv("LDPC_GNN_MSGOUT_VM");
+    return !(e && std::atoi(e) == 0);
 }
 
 // cg_var[q] = msg_var[cg_mem[q]]: the variable of every check-group member (syndrome tables)
@@ -1053,8 +1063,9 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
                        d_weights, T, L, d_msg_type, G, Gtot, w.memb);
     LDPC_CHECK_LAUNCH("gnn_bf16_memb_kernel");
     if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
+    const int vm = msgout_vm();
     hipLaunchKernelGGL(gnn_bf16_vpos_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, w.csr, N, p->E,
-                       w.vpos);
+                       w.vpos, vm);
     LDPC_CHECK_LAUNCH("gnn_bf16_vpos_kernel");
     if (d_iters) {
         hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, d_iters, B, L);
@@ -1178,7 +1189,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
             hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)nb), dim3(256),
                                (size_t)((N + 31) / 32 + N) * 4, st, w.msg_out + b0 * p->E, w.csr, p->E,
                                d_llr + b0 * N, N, p->cg_ptr, w.cg_var, p->Gc, l, act, listed ? alist : nullptr, listed ? acount : nullptr,
-                               d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N, cmp ? olist : nullptr, ocount);
+                               d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N, cmp ? olist : nullptr, ocount, vm);
             LDPC_CHECK_LAUNCH("gnn_bf16_syndrome_kernel");
             if (cmp) {
                 cur ^= 1;
@@ -1205,7 +1216,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     } else if (int rc = run_range(0, B, s, 0)) {
         return rc;
     }
-    return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s, true);
+    return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s, vm != 0);
 }
 
 }  // namespace ldpc

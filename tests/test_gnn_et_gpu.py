@@ -98,3 +98,16 @@ def test_mlp_variants_are_bitwise_equal(cuda, monkeypatch, variant, et):
     monkeypatch.setenv("LDPC_GNN_BF16_MLP", variant)
     p2, it2 = _run(dec, conv, base, 32, llr, et)
     assert torch.equal(p1, p2) and torch.equal(it1, it2)
+
+
+def test_msg_out_order_is_bitwise_neutral(cuda, monkeypatch):
+    """msg_out rows variable-major (default) or in message order (LDPC_GNN_MSGOUT_VM=0): the output
+    stage and the syndrome pass sum each variable's messages in the same ascending order either
+    way, so probs and layer counts are bitwise equal."""
+    base, H, dec, conv = _decoder(32, 6, cuda, seed=4)
+    llr = awgn_llr(200, H.shape[1], 4.0, seed=23, device=cuda)
+    monkeypatch.setenv("LDPC_GNN_MSGOUT_VM", "1")
+    p1, it1 = _run(dec, conv, base, 32, llr, True)
+    monkeypatch.setenv("LDPC_GNN_MSGOUT_VM", "0")
+    p2, it2 = _run(dec, conv, base, 32, llr, True)
+    assert torch.equal(p1, p2) and torch.equal(it1, it2)
