@@ -177,11 +177,16 @@ struct GmArgs {
     int64_t B;
 };
 
+__device__ __forceinline__ void gm_item(const GmArgs &A, uint32_t w, uint32_t nt);
 __global__ __launch_bounds__(256) void gnn_bf16_gm_kernel(GmArgs A) {
-    const uint32_t w = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+    const uint32_t w0 = (uint32_t)(xcd_block(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
     const uint32_t nt = (uint32_t)(A.G.n_tiles - A.G.first);
     const uint32_t nact = A.count ? (uint32_t)__builtin_amdgcn_readfirstlane(*A.count) : (uint32_t)A.B;
-    if (w >= nact * nt) return;
+    // a grid smaller than the work (listed layers with LDPC_GNN_GM_CAP): waves stride over it
+    for (uint32_t w = w0; w < nact * nt; w += gridDim.x * 4) gm_item(A, w, nt);
+}
+
+__device__ __forceinline__ void gm_item(const GmArgs &A, uint32_t w, uint32_t nt) {
     const uint32_t slot = w / nt, t = w - slot * nt + (uint32_t)A.G.first;
     const uint32_t b = A.list ? (uint32_t)A.list[slot] : slot;
     if (A.active && !A.active[b]) return;
@@ -1006,6 +1011,15 @@ int proj_env() {
     return e ? std::atoi(e) : 0;
 }
 
+// LDPC_GNN_GM_CAP=n: after the first syndrome pass the group-mean kernel runs at most n workgroups
+// per CU, striding over the frames still decoding, instead of one wave per (frame, tile) of the
+// whole range (whose early-exiting waves cost ~0.1 ms per layer once few frames are left).  Default
+// 256 (+2.3 % on cfg5 random codewords; 64: -1.2 %; profiles/r03ah); 0 = the full grid.  Read per call.
+int gm_cap() {
+    const char *e = std::getenv("LDPC_GNN_GM_CAP");
+    return e ? std::atoi(e) : 256;
+}
+
 int mlp_variant() {
     const char *e = std::getenv("LDPC_GNN_BF16_MLP");  // read per call (tests compare variants)
     return e ? std::atoi(e) : 1;
@@ -1147,7 +1161,9 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
             LDPC_CHECK_LAUNCH("gnn_bf16_proj_kernel");
         } else {
             const int64_t gwaves = nb * (gm.G.n_tiles - gm.G.first);
-            hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)((gwaves + 3) / 4)), dim3(256), 0, st, gm);
+            int64_t gblocks = (gwaves + 3) / 4;
+            if (gm.count && gm_cap() > 0) gblocks = std::min<int64_t>(gblocks, (int64_t)g_cus * gm_cap());
+            hipLaunchKernelGGL(gnn_bf16_gm_kernel, dim3((unsigned)gblocks), dim3(256), 0, st, gm);
             LDPC_CHECK_LAUNCH("gnn_bf16_gm_kernel");
         }
 

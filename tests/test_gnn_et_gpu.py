@@ -111,3 +111,15 @@ def test_msg_out_order_is_bitwise_neutral(cuda, monkeypatch):
     monkeypatch.setenv("LDPC_GNN_MSGOUT_VM", "0")
     p2, it2 = _run(dec, conv, base, 32, llr, True)
     assert torch.equal(p1, p2) and torch.equal(it1, it2)
+
+
+def test_group_mean_grid_cap_is_bitwise_neutral(cuda, monkeypatch):
+    """LDPC_GNN_GM_CAP: after the first syndrome pass the group-mean kernel strides a capped grid
+    over the frames still decoding; every (frame, tile) item is computed exactly as before."""
+    base, H, dec, conv = _decoder(32, 5, cuda, seed=6)
+    llr = awgn_llr(300, H.shape[1], 4.0, seed=29, device=cuda)
+    monkeypatch.setenv("LDPC_GNN_GM_CAP", "0")
+    p1, it1 = _run(dec, conv, base, 32, llr, True)
+    monkeypatch.setenv("LDPC_GNN_GM_CAP", "1")
+    p2, it2 = _run(dec, conv, base, 32, llr, True)
+    assert torch.equal(p1, p2) and torch.equal(it1, it2)
