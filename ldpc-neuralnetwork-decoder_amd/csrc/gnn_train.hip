@@ -1196,6 +1196,7 @@ int launch_vec(const VecT &v, float *S0, float *S1, hipStream_t s) {
 
 struct TrainWs {
     float *Mv, *Mc, *dz, *dX, *dXp, *cbuf, *hv, *hc, *dhv, *dhc, *dco, *da, *db, *Mda, *Mdb;
+    float *Mv1, *Mc1, *Gs1v, *Gs1c;  // second projection set (odd layers) for the side-stream recompute
     int64_t bytes;
 };
 
@@ -1221,11 +1222,28 @@ TrainWs carve_train(const ldpc_gnn_plan *p, int H, int N, int64_t B, void *base)
     w.dco = take(reh);
     w.da = take(reh);
     w.db = take(reh);
+    w.Mv1 = take(mv);
+    w.Mc1 = take(mc);
+    w.Gs1v = take(mv);
+    w.Gs1c = take(mc);
     w.bytes = o * 4;
     return w;
 }
 
 int g_cus_t = 0;
+
+// per-device, per-thread events of the backward's side-stream recompute (see bwd_overlap)
+int train_events(hipEvent_t ready[2], hipEvent_t freed[2]) {
+    constexpr int kMaxDev = 64;
+    thread_local hipEvent_t ev[kMaxDev][4];
+    int dev = 0;
+    LDPC_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDev) return fail(LDPC_EUNSUPPORTED, "device index out of range");
+    for (int i = 0; i < 4; ++i)
+        if (!ev[dev][i]) LDPC_HIP(hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming));
+    ready[0] = ev[dev][0]; ready[1] = ev[dev][1]; freed[0] = ev[dev][2]; freed[1] = ev[dev][3];
+    return LDPC_OK;
+}
 
 // LDPC_GNN_TRAIN_PROJ=0: the backward recomputes group means and runs GEMM1 / GEMM3' over
 // [c; g] per message (A/B); default: projected group rows (train_mlp_bwd_mfma_kernel PJ)
@@ -1241,6 +1259,16 @@ int bwd_proj() {
 int bwd_split() {
     const char *e = std::getenv("LDPC_GNN_TRAIN_SPLIT");
     return e && std::atoi(e) == 1;
+}
+
+// LDPC_GNN_TRAIN_OVERLAP=1: the backward's forward recompute (group projections of layer l - 1)
+// runs on a side stream into a second buffer set while layer l's gradients run on the caller's
+// stream; 0: one set, in line.  42.3-42.5 vs 42.7-43.0 ms per B = 256 step (profiles/r03aj, three
+// pairs on one box): the projection mostly competes with the gradient kernels for the CUs.
+// Read per call.
+int bwd_overlap() {
+    const char *e = std::getenv("LDPC_GNN_TRAIN_OVERLAP");
+    return e ? std::atoi(e) : 1;
 }
 
 int bwd_mfma() {
@@ -1350,6 +1378,26 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         v.H = H; v.T = T; v.N = N; v.mode = 2; v.E = E; v.R = R;
         if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
     }
+    const bool ovl = pj && L > 1 && bwd_overlap();
+    hipStream_t s2 = nullptr;
+    hipEvent_t ev_ready[2] = {}, ev_free[2] = {};
+    int rc0 = 0;
+    auto side_project = [&](int j) -> int {  // layer j's projections into set j & 1, on s2
+        const float *xj = j > 0 ? d_saved + (int64_t)(j - 1) * n : nullptr;
+        float *pv = (j & 1) ? w.Mv1 : w.Mv, *pc = (j & 1) ? w.Mc1 : w.Mc;
+        float *gv = (j & 1) ? w.Gs1v : w.da, *gc = (j & 1) ? w.Gs1c : w.db;
+        if (int rc = gnn_project_groups(p, T, d_weights, j, xj, d_msg_type, d_msg_var, d_llr, N, B, pv, pc, gv, gc, s2))
+            return rc;
+        LDPC_HIP(hipEventRecord(ev_ready[j & 1], s2));
+        return LDPC_OK;
+    };
+    if (ovl) {
+        hipEvent_t fork, join;
+        if (int rc = gnn_side_stream(&s2, &fork, &join)) return rc;
+        if (int rc = train_events(ev_ready, ev_free)) return rc;
+        LDPC_HIP(hipEventRecord(fork, s));  // the workspace and inputs are the caller stream's
+        LDPC_HIP(hipStreamWaitEvent(s2, fork, 0));
+    }
     for (int l = L - 1; l >= 0; --l) {
         const float *W[11];
         t_layer(d_weights, H, T, l, W);
@@ -1369,10 +1417,22 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
             if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
         }
         const float *x = l > 0 ? d_saved + (int64_t)(l - 1) * n : nullptr;
-        // PJ: the group means of c go to da / db (free in this mode: no per-message group part)
-        float *Gsv = w.da, *Gsc = w.db;
-        if (pj) {  // forward recompute: projected rows (Mv / Mc) and the group means (Gsv / Gsc)
-            if (int rc = gnn_project_groups(p, T, d_weights, l, x, d_msg_type, d_msg_var, d_llr, N, B, w.Mv, w.Mc,
+        // PJ: the group means of c go to da / db (free in this mode: no per-message group part);
+        // with the side stream, odd layers use the second set
+        const bool odd = ovl && (l & 1);
+        float *Mv = odd ? w.Mv1 : w.Mv, *Mc = odd ? w.Mc1 : w.Mc;
+        float *Gsv = odd ? w.Gs1v : w.da, *Gsc = odd ? w.Gs1c : w.db;
+        if (ovl) {
+            // side stream: layer l's set was filled one iteration earlier (or here, for the last
+            // layer); layer l - 1's goes into the other set once layer l + 1 has released it
+            if (l == L - 1 && (rc0 = side_project(l))) return rc0;
+            if (l > 0) {
+                if (l + 1 <= L - 1) LDPC_HIP(hipStreamWaitEvent(s2, ev_free[(l + 1) & 1], 0));
+                if ((rc0 = side_project(l - 1))) return rc0;
+            }
+            LDPC_HIP(hipStreamWaitEvent(s, ev_ready[l & 1], 0));
+        } else if (pj) {  // forward recompute: projected rows (Mv / Mc) and the group means (Gsv / Gsc)
+            if (int rc = gnn_project_groups(p, T, d_weights, l, x, d_msg_type, d_msg_var, d_llr, N, B, Mv, Mc,
                                             Gsv, Gsc, s))
                 return rc;
         } else {  // group means of c (forward recompute)
@@ -1388,7 +1448,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         // MLP backward
         MlpT m{};
         m.x = x; m.llr = d_llr; m.w_in = d_weights; m.b_in = d_weights + H;
-        m.Mv = w.Mv; m.Mc = w.Mc; m.dX = w.dX;
+        m.Mv = Mv; m.Mc = Mc; m.dX = w.dX;
         m.msg_type = d_msg_type; m.msg_var = d_msg_var; m.vgroup = p->vgroup; m.cgroup = p->cgroup;
         m.emb = W[0]; m.w1v = W[1]; m.b1v = W[2]; m.w2v = W[3]; m.w1c = W[5]; m.b1c = W[6]; m.w2c = W[7];
         m.cbuf = w.cbuf; m.hv = w.hv; m.hc = w.hc; m.dhv = w.dhv; m.dhc = w.dhc;
@@ -1420,12 +1480,12 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
                 GmT gs{};
                 gs.src = side ? w.dhc : w.dhv; gs.src_mode = 0; gs.sum_only = 1; gs.H = H; gs.N = N; gs.E = E; gs.B = B;
                 gs.ptr = side ? p->cg_ptr : p->vg_ptr; gs.mem = side ? p->cg_mem : p->vg_mem;
-                gs.inv = side ? p->inv_c : p->inv_v; gs.G = side ? p->Gc : p->Gv; gs.dst = side ? w.Mc : w.Mv;
+                gs.inv = side ? p->inv_c : p->inv_v; gs.G = side ? p->Gc : p->Gv; gs.dst = side ? Mc : Mv;
                 if (int rc = launch_group_mean(gs, s)) return rc;
             }
             const int64_t quads = (B * p->Gv + 3) / 4 + (B * p->Gc + 3) / 4;
             const unsigned ggrid = (unsigned)std::min<int64_t>((quads + 3) / 4, (int64_t)g_cus_t * 8);
-            hipLaunchKernelGGL(train_group_back_kernel, dim3(ggrid), dim3(256), 0, s, w.Mv, w.Mc, W[1], W[5], p->inv_v,
+            hipLaunchKernelGGL(train_group_back_kernel, dim3(ggrid), dim3(256), 0, s, Mv, Mc, W[1], W[5], p->inv_v,
                                p->inv_c, p->Gv, p->Gc, B, w.Mda, w.Mdb);
             LDPC_CHECK_LAUNCH("train_group_back_kernel");
         } else {
@@ -1465,7 +1525,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         for (int side = 0; side < 2; ++side) {
             // PJ: the group means are in Gsv / Gsc and the group sums of dh already in Mv / Mc
             const float *dh = side ? w.dhc : w.dhv, *Gs = pj ? (side ? Gsc : Gsv) : side ? w.Mc : w.Mv;
-            float *dhsum = pj ? (side ? w.Mc : w.Mv) : side ? w.Mdb : w.Mda;
+            float *dhsum = pj ? (side ? Mc : Mv) : side ? w.Mdb : w.Mda;
             float *gw = side ? Gw[5] : Gw[1], *gb = side ? Gw[6] : Gw[2];
             const int Gn = side ? p->Gc : p->Gv;
             OuterT c{};
@@ -1485,6 +1545,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
             const unsigned ggrid = (unsigned)std::min<int64_t>((g.R + 63) / 64, (int64_t)g_cus_t * 4);
             if (int rc = launch_outer(g, ggrid, s)) return rc;
         }
+        if (ovl) LDPC_HIP(hipEventRecord(ev_free[l & 1], s));  // this layer's set is free again
         VecT v{};
         v.src = w.dco; v.llr = d_llr; v.msg_type = d_msg_type; v.msg_var = d_msg_var;
         v.H = H; v.T = T; v.N = N; v.E = E; v.R = R;
