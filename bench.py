@@ -149,10 +149,12 @@ def parse():
 
 
 def setup_dist():
+    """One process per GPU.  A process group is created for more than one rank, or for one rank
+    with BENCH_DIST=1 (the RCCL branch exercised on a single GPU: tests/test_dist_rccl_gpu.py)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or os.environ.get("BENCH_DIST") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # BENCH_DIST_BACKEND=gloo with more ranks than GPUs is a rehearsal of the multi-rank path
         # on a 1-GPU box (ranks share the card); the measured runs use RCCL ("nccl"), one GPU each
@@ -169,7 +171,7 @@ def setup_dist():
 
 
 def barrier(world):
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
 
 
@@ -338,6 +340,7 @@ def main():
         ref_bits = SystematicEncoder(H, dev).random(B, generator=gen).to(torch.uint8)
     llr = awgn_llr(B, n, snr, seed=20251015, frame_offset=rank * B, bits=ref_bits, device=dev)
     counters = torch.zeros(4, dtype=torch.int64, device=dev)
+    scratch = torch.zeros(4, dtype=torch.int64, device=dev)  # fused counters of a codeword run (iterations only)
 
     weights = None
     if kind in ("minsum", "bp"):
@@ -353,14 +356,17 @@ def main():
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
 
         def step(count):
-            fused = count and ref_bits is None  # the fused counters count against the all-zero codeword
+            # the fused counters count bit errors against the all-zero codeword: a codeword run takes
+            # only their iteration sum (index 3: the iterations actually run, early stop included)
+            # and counts its errors against the transmitted codewords
+            cnt = None if not count else (counters if ref_bits is None else scratch.zero_())
             N.check(N.lib().ldpc_flood_decode(
                 g.handle, algo, N.ptr(llr), B, iters, 0.75, es, N.LDPC_OUT_U8,
-                N.ptr(bits), None, None, N.ptr(counters) if fused else None, N.ptr(ws), wsb, stream))
+                N.ptr(bits), None, None, N.ptr(cnt) if cnt is not None else None, N.ptr(ws), wsb, stream))
             if count and ref_bits is not None:
                 from ldpc_neural_decoder.utils import count_errors
                 count_errors(bits, ref=ref_bits, counters=counters)
-                counters[3] += iters * B
+                counters[3] += scratch[3]
 
         dtype = "f32"
         per_launch_alg = flood_bytes_per_cw(g.E, g.N, iters) * B
@@ -543,7 +549,7 @@ def main():
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     tot = counters.clone()
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed, kern_ms = t.tolist()
@@ -665,9 +671,10 @@ def main():
             "avg_layers": avg_layers,
             "avg_iterations": itsum / max(fr, 1) if kind in ("minsum", "bp") else None,
             "cpu_baseline": cpu,
+            "dist_backend": dist.get_backend() if dist.is_initialized() else None,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

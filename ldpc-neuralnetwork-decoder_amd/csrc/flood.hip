@@ -23,11 +23,13 @@
 // tolerance", not bitwise).
 // Compile with -ffp-contract=off: no a*b+c may fuse on this path.
 // Translation units: flood_dev.hpp (device code shared by all), flood_fixed_ms.hip / flood_fixed_bp.hip
-// (compile-time schedules), flood_pair.hip (frame-pair kernel), flood_stream.hip (streaming decoders),
+// (compile-time schedules), flood_stream.hip (streaming decoders),
 // and this file (table-driven kernel, early-stop passes, host dispatch, the C ABI).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "flood_host.hpp"
 
@@ -212,30 +214,6 @@ int launch_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter,
     return LDPC_OK;
 }
 
-// frame-pair kernel (flood_pair.inc): the reference's codes without early stopping, opt-in with
-// LDPC_FLOOD_PAIR=1 (measured slower than flood_fixed_kernel on cfg3: DESIGN.md section 3.1)
-bool use_pair(const ldpc_graph *g) {
-    if (g->fixed_id == 0) return false;
-    const char *e = std::getenv("LDPC_FLOOD_PAIR");
-    return e && std::atoi(e) != 0;
-}
-int pair_frames(const ldpc_graph *g) { return 2 * g->FG; }
-
-template <int ALGO>
-int launch_pair(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha, int out_dtype,
-                void *bits, const Outs &O, hipStream_t s) {
-    const int64_t nwg = (B + pair_frames(g) - 1) / pair_frames(g);
-    return launch_pair_kernel(ALGO, g->fixed_id, nwg, s, llr, B, max_iter, alpha, out_dtype, bits, O);
-}
-
-// 6-wave kernel (flood_w6.inc): the reference's codes without early stopping, opt-in with
-// LDPC_FLOOD_W6=1 (A/B)
-bool use_w6(const ldpc_graph *g) {
-    if (g->fixed_id == 0) return false;
-    const char *e = std::getenv("LDPC_FLOOD_W6");
-    return e && std::atoi(e) != 0;
-}
-
 int reduce_rows(const ldpc_graph *g, int64_t B, const uint32_t *partials, uint64_t *counters, int32_t *batch_iters,
                 const int32_t *gate, hipStream_t s, int frames_per_wg = 0) {
     if (!counters && !batch_iters) return LDPC_OK;
@@ -250,18 +228,31 @@ int run_flood(const ldpc_graph *g, const float *llr, int64_t B, int max_iter, fl
     const FloodWs ws = flood_ws(g, B, max_iter, es, work);
     const bool want = counters || batch_iters;
     const Outs O{iters_out, want ? ws.partials : nullptr};
-    if (es == LDPC_ES_OFF && use_pair(g)) {
-        int rc = launch_pair<ALGO>(g, llr, B, max_iter, alpha, out_dtype, bits, O, s);
-        return rc != LDPC_OK ? rc : reduce_rows(g, B, ws.partials, counters, nullptr, nullptr, s, pair_frames(g));
-    }
-    if (es == LDPC_ES_OFF && use_w6(g)) {
-        const int64_t nwg = (B + g->FG - 1) / g->FG;
-        int rc = launch_w6_kernel(ALGO, g->fixed_id, nwg, flood_lds_bytes(g, LDPC_ES_OFF), s, g->ft, llr, B, max_iter,
-                                  alpha, out_dtype, bits, O);
-        return rc != LDPC_OK ? rc : reduce_rows(g, B, ws.partials, counters, nullptr, nullptr, s);
-    }
     if (es == LDPC_ES_OFF) {
+#ifdef LDPC_TIMELINE
+        // timeline build: stamps of the first kTlWgs workgroups, dumped after the decode to
+        // $LDPC_TIMELINE_OUT (header: kTlWgs, waves, stamps per wave, max_iter, then uint64 stamps)
+        static uint64_t *tl = nullptr;
+        const size_t tl_n = (size_t)kTlWgs * 4 * kTlPer;
+        if (!tl) LDPC_HIP(hipMalloc(&tl, tl_n * 8));
+        LDPC_HIP(hipMemsetAsync(tl, 0, tl_n * 8, s));
+        Outs Ot = O;
+        Ot.timeline = tl;
+        int rc = launch_flood<ALGO, LDPC_ES_OFF>(g, llr, B, max_iter, alpha, out_dtype, bits, Ot, EsWs{}, s);
+        if (const char *path = std::getenv("LDPC_TIMELINE_OUT")) {
+            std::vector<uint64_t> h(tl_n);
+            LDPC_HIP(hipStreamSynchronize(s));
+            LDPC_HIP(hipMemcpy(h.data(), tl, tl_n * 8, hipMemcpyDeviceToHost));
+            if (FILE *f = std::fopen(path, "wb")) {
+                const int32_t hdr[4] = {kTlWgs, 4, kTlPer, max_iter};
+                std::fwrite(hdr, 4, 4, f);
+                std::fwrite(h.data(), 8, h.size(), f);
+                std::fclose(f);
+            }
+        }
+#else
         int rc = launch_flood<ALGO, LDPC_ES_OFF>(g, llr, B, max_iter, alpha, out_dtype, bits, O, EsWs{}, s);
+#endif
         // ES off: every frame ran max_iter (batch_iters was set before the launch)
         return rc != LDPC_OK ? rc : reduce_rows(g, B, ws.partials, counters, nullptr, nullptr, s);
     }

@@ -57,7 +57,14 @@ struct EsWs {
 struct Outs {
     int32_t *iters_out;
     uint32_t *partials;  // [nwg][kPartRow] counter rows (NULL: no counters wanted)
+    uint64_t *timeline;  // LDPC_TIMELINE builds only (tools/flood_timeline.py): NULL otherwise
 };
+
+// Timeline build (-DLDPC_TIMELINE, tools/build_timeline.sh): lane 0 of every wave of the first
+// kTlWgs workgroups stores s_memtime at each phase boundary of the iteration loop -- after the
+// init barrier, then per iteration: check phase done, barrier 1 passed, variable phase done,
+// barrier 2 passed -- so the waves each barrier waits on can be read off.
+constexpr int kTlWgs = 2048, kTlMaxIter = 16, kTlPer = 2 + 4 * kTlMaxIter;
 
 namespace {
 
@@ -176,9 +183,6 @@ __device__ __forceinline__ uint32_t sign_parity_n(const float (&v)[CAP]) {
 
 // m2 = median(m1, |x|, m2) then m1 = min(m1, |x|): the two smallest magnitudes of a row with no
 // NaN (v_min / v_med3 with |x| as a source modifier; fminf would add a NaN-quieting v_max)
-#ifndef LDPC_MIN_ASM
-#define LDPC_MIN_ASM 0
-#endif
 // -inf in a VGPR the compiler cannot see through: med3(m, |x|, -inf) = min(m, |x|) for non-NaN
 // operands, and an opaque third operand keeps the compiler from turning it back into a
 // canonicalising fminf
@@ -197,16 +201,10 @@ __device__ __forceinline__ float opaque_vf(float v) {
     return v;
 }
 __device__ __forceinline__ void two_min_step(float &m1, float &m2, float x, float ninf) {
-#if LDPC_MIN_ASM
-    (void)ninf;
-    asm("v_med3_f32 %0, %1, |%2|, %3" : "=v"(m2) : "v"(m1), "v"(x), "v"(m2));
-    asm("v_min_f32 %0, %1, |%2|" : "=v"(m1) : "v"(m1), "v"(x));
-#else
     // builtins, not inline asm: a VALU reading a VGPR written by inline asm gets a conservative
     // s_nop from the hazard recognizer (one per edge in the check phase)
     m2 = __builtin_amdgcn_fmed3f(m1, fabsf(x), m2);
     m1 = __builtin_amdgcn_fmed3f(m1, fabsf(x), ninf);
-#endif
 }
 
 // The two smallest magnitudes of a row with no NaN, three messages per step: the smallest and the
@@ -216,9 +214,6 @@ __device__ __forceinline__ void two_min_step(float &m1, float &m2, float x, floa
 // message for the running med3 / min chain (BG2: 217 instead of 310 of these half-rate ops per
 // base-graph iteration).  Every op returns one of its inputs: the pair (m1, m2) is bit-identical.
 // minimum / maximum (IEEE, NaN-propagating) need no canonicalising v_max, unlike fminf.
-#ifndef LDPC_MIN3
-#define LDPC_MIN3 1
-#endif
 __device__ __forceinline__ float vmin(float a, float b) { return __builtin_elementwise_minimum(a, b); }
 __device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 template <int DC, int CAP>
@@ -723,6 +718,22 @@ __device__ __forceinline__ void flood_drive(Body &body, Ctx &C, const Lane &L, i
     __syncthreads();
     body.init(C, L);
     __syncthreads();
+#ifdef LDPC_TIMELINE
+    uint64_t *tl = (O.timeline && blockIdx.x < (unsigned)kTlWgs && L.lane == 0)
+                       ? O.timeline + ((int64_t)blockIdx.x * 4 + wave) * kTlPer : nullptr;
+    // one asm statement with its own lgkmcnt(0) and scheduling fences around it: the builtin form
+    // leaves the wait's place to the compiler, which then drains LDS reads all over the loop
+    auto mark = [&](int k) {
+        uint64_t t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (tl && k < kTlPer) tl[k] = t;
+    };
+#else
+    auto mark = [](int) {};
+#endif
+    mark(0);
 
     int my_iters = max_iter;
     uint64_t done = 0;
@@ -737,7 +748,9 @@ __device__ __forceinline__ void flood_drive(Body &body, Ctx &C, const Lane &L, i
             body.template check<true>(C, L, errs);
         else
             body.template check<false>(C, L, errs);
+        mark(1 + 4 * it);
         LDPC_ITER_SYNC();
+        mark(2 + 4 * it);
         if (C.ballots && tid == 0) C.words[Nb] = 0;
         if (last)
             body.template var<true, false>(C, L, errs);
@@ -745,7 +758,9 @@ __device__ __forceinline__ void flood_drive(Body &body, Ctx &C, const Lane &L, i
             body.template var<true, true>(C, L, errs);
         else
             body.template var<false, true>(C, L, errs);
+        mark(3 + 4 * it);
         LDPC_ITER_SYNC();
+        mark(4 + 4 * it);
         if (C.ballots) {
             // syndrome H x = 0 per frame (traditional_decoders.py:111-134), from the ballots
             const uint64_t m = __ballot(body.parity(C, L));
@@ -856,11 +871,29 @@ __global__ __launch_bounds__(512) void flood_kernel(FloodTables T, const float *
 namespace {
 
 
+// Variable-phase schedule (gen/fixed_codes.hpp): VT pairs two columns per task on v_pk_add_f32
+// (default), VS runs every column alone (LDPC_VAR_PAIRS=0, A/B builds)
+#ifndef LDPC_VAR_PAIRS
+#define LDPC_VAR_PAIRS 1
+#endif
+#if LDPC_VAR_PAIRS
+#define LDPC_VT(x) G::VT_##x
+#else
+#define LDPC_VT(x) G::VS_##x
+#endif
+
 // per-wave compile-time plan
 template <class G, int WV>
 struct FxPlan {
     static constexpr int R0 = G::CHK_PTR[WV], NR = G::CHK_PTR[WV + 1] - R0;
-    static constexpr int C0 = G::VAR_PTR[WV], NC = G::VAR_PTR[WV + 1] - C0;
+    // the wave's columns (LLRs in registers, init, shifts) and its variable tasks
+    static constexpr int C0 = LDPC_VT(COL_PTR)[WV], NC = LDPC_VT(COL_PTR)[WV + 1] - C0;
+    static constexpr int T0 = LDPC_VT(PTR)[WV], NT = LDPC_VT(PTR)[WV + 1] - T0;
+    static constexpr int col_index(int col) {
+        for (int i = 0; i < NC; ++i)
+            if (LDPC_VT(COLS)[C0 + i] == col) return i;
+        return -1;
+    }
     struct Tab {
         int nsh = 0, next = 0, maxdc = 1, maxdv = 1;
         int shv[64] = {};        // distinct shifts of the wave's columns
@@ -879,7 +912,7 @@ struct FxPlan {
                 if (G::ROW_SLOT[e] < 0) ++t.next;
         }
         for (int i = 0; i < NC; ++i) {
-            const int c = G::VAR_COLS[C0 + i];
+            const int c = LDPC_VT(COLS)[C0 + i];
             const int dv = G::COL_PTR[c + 1] - G::COL_PTR[c];
             if (dv > t.maxdv) t.maxdv = dv;
             for (int j = G::COL_PTR[c]; j < G::COL_PTR[c + 1]; ++j) {
@@ -905,24 +938,6 @@ struct FxPlan {
 
 #ifndef LDPC_VAR_PIPE
 #define LDPC_VAR_PIPE 24
-#endif
-#ifndef LDPC_SEL_ASM
-// 1: the select by v_cmp / v_cndmask in asm (measured fastest); 0: the compare-free select (fewer
-// VALU pipe cycles but one more instruction per edge: 3.7 % slower, the kernel is bound by the
-// per-wave issue and dependency latency rather than by the VALU pipe)
-#define LDPC_SEL_ASM 1
-#endif
-#ifndef LDPC_ZFLAG
-#define LDPC_ZFLAG 1  // zero inputs join the sticky NaN flag: one slow/fast branch per check phase (+5%)
-#endif
-#ifndef LDPC_VAR_PK
-#define LDPC_VAR_PK 0  // 1: variable update on v_pk_add_f32 pairs (6 % slower than scalar adds)
-#endif
-#ifndef LDPC_MIN_SPLIT
-#define LDPC_MIN_SPLIT 0  // 1: the row's two minima as two half-row chains + a merge (shorter chain)
-#endif
-#ifndef LDPC_ADDTID
-#define LDPC_ADDTID 1  // check-phase stores as ds_write_addtid_b32 (the slot entry of a row is slot[lane])
 #endif
 // the next column's reads are issued before the current column's adds when the two columns hold
 // at most this many messages together (register budget: 4 workgroups per CU = 128 VGPRs)
@@ -950,11 +965,7 @@ struct FixedBody {
                 if constexpr (G::ROW_SLOT[P0 + E] < 0) {
                     constexpr int X = P::ext_index(I, E), COL = G::ROW_COL[P0 + E], S4 = 4 * G::ROW_SHIFT[P0 + E];
                     ext[X] = L.llr_at(COL * 4 * G::Z + ((L.k4 + S4) & ZM4));
-#if LDPC_ZFLAG
-                    nan |= is_zero_sign(ext[X]);  // zero or NaN
-#else
-                    nan |= ext[X] != ext[X];
-#endif
+                    nan |= is_zero_sign(ext[X]);  // zero or NaN: the sticky flag (see check())
                 }
             });
         });
@@ -963,14 +974,10 @@ struct FixedBody {
             rot[J] = L.fz4 + ((L.k4 + (4 * G::Z - 4 * P::T.shv[J])) & ZM4);
         });
         sfor<P::NC>([&](auto i) {
-            constexpr int I = decltype(i)::value, COL = G::VAR_COLS[P::C0 + I];
+            constexpr int I = decltype(i)::value, COL = LDPC_VT(COLS)[P::C0 + I];
             constexpr int P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
             cllr[I] = L.llr_at(COL * 4 * G::Z + L.k4);
-#if LDPC_ZFLAG
             nan |= is_zero_sign(cllr[I]);
-#else
-            nan |= cllr[I] != cllr[I];
-#endif
             sfor<DV>([&](auto jj) {
                 constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
                 constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
@@ -994,19 +1001,14 @@ struct FixedBody {
     }
 
     template <int I, bool DEC, bool SLOW = false>
-    __device__ __forceinline__ void row(const Ctx &C, const Lane &L, const float (&v)[MAXDC], bool nanflag,
-                                        int &errs, float ninf, float pinf, uint32_t sgn, float alv) const {
+    __device__ __forceinline__ void row(const Ctx &C, const Lane &L, const float (&v)[MAXDC], int &errs, float ninf, float pinf, uint32_t sgn, float alv) const {
         constexpr int R = G::CHK_ROWS[P::R0 + I], P0 = G::ROW_PTR[R], DC = G::ROW_PTR[R + 1] - P0;
         // an output is needed for a slot edge always, for a degree-1 edge only to take its decision
         auto needed = [](int e) constexpr { return DEC || G::ROW_SLOT[P0 + e] >= 0; };
         auto emit = [&](auto e, float o) {
             constexpr int E = decltype(e)::value, SL = G::ROW_SLOT[P0 + E];
             if constexpr (SL >= 0) {
-#if LDPC_ADDTID
-                lds_wr_tid<SL * 256>(o);
-#else
-                lds_wr(C.lds + SL * 256, L.lane4, o);
-#endif
+                lds_wr_tid<SL * 256>(o);  // ds_write_addtid_b32: the slot entry of a row is slot[lane]
             } else if constexpr (DEC) {
                 if (C.direct_bits || C.ballots)  // degree-1 variable: APP = llr + c2v
                     ext_decision(C, L, G::ROW_COL[P0 + E], 4 * G::ROW_SHIFT[P0 + E], v[E] + o, errs);
@@ -1017,43 +1019,15 @@ struct FixedBody {
             // m2 starts as an opaque +inf: a constant one lets the compiler rewrite the first
             // v_med3 as a canonicalising fmaxf
             float m1 = fabsf(v[0]), m2 = pinf;
-#if LDPC_MIN3
             two_smallest<DC>(v, m1, m2, ninf);
-#elif LDPC_MIN_SPLIT
-            if constexpr (DC >= 6) {
-                // two independent chains over the halves, then the second smallest of the union =
-                // med3(m1a, m1b, min(m2a, m2b)) (both minima are <= their chains' second minima)
-                constexpr int H1 = DC / 2;
-                float m1b = fabsf(v[H1]), m2b = pinf;
-                sfor<H1 - 1>([&](auto e) {
-                    two_min_step(m1, m2, v[decltype(e)::value + 1], ninf);
-                    two_min_step(m1b, m2b, v[H1 + decltype(e)::value + 1], ninf);
-                });
-                if constexpr (DC - H1 > H1) two_min_step(m1b, m2b, v[DC - 1], ninf);
-                const float t = __builtin_amdgcn_fmed3f(m2, m2b, ninf);  // min(m2, m2b)
-                m2 = __builtin_amdgcn_fmed3f(m1, m1b, t);
-                m1 = __builtin_amdgcn_fmed3f(m1, m1b, ninf);
-            } else {
-                sfor<DC - 1>([&](auto e) { two_min_step(m1, m2, v[decltype(e)::value + 1], ninf); });
-            }
-#else
-            sfor<DC - 1>([&](auto e) { two_min_step(m1, m2, v[decltype(e)::value + 1], ninf); });
-#endif
             // Fast path: no zero message in the row (then m1 > 0) and no possible NaN in the
             // workgroup (the sticky flag, see var()): torch.sign is +-1 on every message, so
             //   c2v_e = (par ^ sign(x_e)) * (alpha * (|x_e| == m1 ? m2 : m1))
             // bit for bit (a tie at m1 puts m1 in m2 too).  Otherwise MinSumStats (exact
             // torch.sign(0) = 0 and NaN semantics).
-#if LDPC_ZFLAG
             // the workgroup's sticky flag (init / var) covers zero and NaN inputs: one branch per
             // phase (check) instead of one per row, and the hot loop holds the fast code only
             if (!SLOW) {
-#elif LDPC_EXP_NOSLOW  // timing experiment only: the fast path unconditionally (inexact for zeros / NaN)
-            if (true) {
-#else
-            if (!nanflag && !__any(m1 == 0.0f)) {
-#endif
-#if LDPC_SEL_ASM
                 // the sign mask and alpha as VGPR operands: an SGPR (or SGPR-held constant) source
                 // halves a VALU op's issue rate (tools/ubench), so the per-edge v_bitop3 below and
                 // the per-row products run at the full rate
@@ -1074,26 +1048,6 @@ struct FixedBody {
                     if constexpr (needed(E))
                         emit(e, __uint_as_float(__builtin_amdgcn_bitop3_b32(sel[E], __float_as_uint(v[E]), sgn, 0x78)));
                 });
-#else
-                // The select without compares: t = m1 - |x_e| is +0 exactly when |x_e| == m1 and
-                // negative otherwise (x - y == 0 only for x == y; a flushed tiny difference is -0),
-                // so its arithmetic shift by 31 is the "use s1" mask.  v_sub / v_ashr / v_bitop3
-                // with VGPR operands issue at the full VALU rate, where v_cmp, v_cndmask and any
-                // op with an SGPR operand take two passes (measured: tools/ubench).  The sign
-                // mask and alpha are opaque VGPRs for the same reason.
-                const uint32_t par = sign_parity_n<DC>(v) & sgn;
-                const uint32_t s1 = __float_as_uint(alv * m1) ^ par, s2 = __float_as_uint(alv * m2) ^ par;
-                sfor<DC>([&](auto e) {
-                    constexpr int E = decltype(e)::value;
-                    if constexpr (needed(E)) {
-                        // (opaque: the compiler would turn the mask back into v_cmp + v_cndmask)
-                        const uint32_t mk = opaque_vu((uint32_t)((int32_t)__float_as_uint(m1 - fabsf(v[E])) >> 31));
-                        const uint32_t sel = (s1 & mk) | (s2 & ~mk);
-                        // sel ^ (x & SIGN) as one v_bitop3 (the compiler splits it into and + xor)
-                        emit(e, __uint_as_float(__builtin_amdgcn_bitop3_b32(sel, __float_as_uint(v[E]), sgn, 0x78)));
-                    }
-                });
-#endif
             } else {
                 MinSumStats st;
                 sfor<DC>([&](auto e) { st.add(decltype(e)::value, v[decltype(e)::value]); });
@@ -1116,26 +1070,20 @@ struct FixedBody {
 
     template <bool DEC>
     __device__ __forceinline__ void check(const Ctx &C, const Lane &L, int &errs) const {
-        bool nanflag = false;
-        if constexpr (ALGO == LDPC_ALGO_MINSUM) nanflag = __builtin_amdgcn_readfirstlane(*C.flag) != 0;
-#if LDPC_ZFLAG
         if constexpr (ALGO == LDPC_ALGO_MINSUM) {
-            if (nanflag)
+            if (__builtin_amdgcn_readfirstlane(*C.flag) != 0)
                 rows<DEC, true>(C, L, errs);
             else
                 rows<DEC, false>(C, L, errs);
             return;
         }
-#endif
-        rows<DEC, false>(C, L, errs, nanflag);
+        rows<DEC, false>(C, L, errs);
     }
 
     template <bool DEC, bool SLOW>
-    __device__ __forceinline__ void rows(const Ctx &C, const Lane &L, int &errs, bool nanflag = false) const {
+    __device__ __forceinline__ void rows(const Ctx &C, const Lane &L, int &errs) const {
         float va[MAXDC], vb[MAXDC];
-#if LDPC_ADDTID
         addtid_begin(C.lds);
-#endif
         const float ninf = opaque_sf(-INFINITY), pinf = opaque_sf(INFINITY);
         const uint32_t sgn = opaque_vu(0x80000000u);
         const float alv = opaque_vf(C.alpha);
@@ -1144,97 +1092,130 @@ struct FixedBody {
             constexpr int I = decltype(i)::value;
             if constexpr (I % 2 == 0) {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, vb);
-                row<I, DEC, SLOW>(C, L, va, nanflag, errs, ninf, pinf, sgn, alv);
+                row<I, DEC, SLOW>(C, L, va, errs, ninf, pinf, sgn, alv);
             } else {
                 if constexpr (I + 1 < P::NR) load_row<I + 1>(C, L, va);
-                row<I, DEC, SLOW>(C, L, vb, nanflag, errs, ninf, pinf, sgn, alv);
+                row<I, DEC, SLOW>(C, L, vb, errs, ninf, pinf, sgn, alv);
             }
         });
-#if LDPC_ADDTID
         addtid_end();
-#endif
     }
 
-    // ---- variable phase
-    static constexpr int dv_of(int i) { return G::COL_PTR[G::VAR_COLS[P::C0 + i] + 1] - G::COL_PTR[G::VAR_COLS[P::C0 + i]]; }
+    // ---- variable phase: tasks (column A, column B or none, outputs [LO, HI) of both), see
+    // tools/gen_fixed_codes.py var_schedule.  Per output e of a column of degree D:
+    //   v2c_e = P_e + c_{e+1} + ... + c_{D-1},  P_0 = llr, P_{J+1} = P_J + c_J
+    // in this order (traditional_decoders.py:235-250: the sum over i' != i from llr in ascending
+    // check order); the APP is P_D.  A pair runs both columns' chains in the two halves of
+    // v_pk_add_f32 (two independent IEEE fp32 adds: each half is the scalar sequence, bit for bit)
+    // while both have messages (J < DB); column A's remaining steps are scalar v_add_f32.
+    template <int TK>
+    struct Task {
+        static constexpr int X = P::T0 + TK;
+        static constexpr int CA = LDPC_VT(A)[X], CB = LDPC_VT(B)[X], LO = LDPC_VT(LO)[X], HI = LDPC_VT(HI)[X];
+        static constexpr int PA = G::COL_PTR[CA], DA = G::COL_PTR[CA + 1] - PA;
+        static constexpr int PB = CB >= 0 ? G::COL_PTR[CB] : 0, DB = CB >= 0 ? G::COL_PTR[CB + 1] - PB : 0;
+        static_assert(DB <= DA && (DB == 0 || LO < DB), "pair tasks: A is the longer column, B has outputs");
+        static constexpr int IA = P::col_index(CA), IB = CB >= 0 ? P::col_index(CB) : 0;
+        static constexpr int NPREFA = HI == DA ? DA : (HI > 0 ? HI - 1 : 0);
+        static constexpr bool BLAST = DB > 0 && LO <= DB - 1 && DB - 1 < HI;  // B's APP here
+        static constexpr int NPREF = NPREFA > (BLAST ? DB : 0) ? NPREFA : (BLAST ? DB : 0);
+        static constexpr int NMSG = DA + DB;
+    };
+    struct TaskIn {
+        f32x2 cp[MAXDV];  // J < DB: {c_A[J], c_B[J]}
+        float cs[MAXDV];  // DB <= J < DA: c_A[J]
+    };
 
-    template <int I>
-    __device__ __forceinline__ void load_col(const Ctx &C, float (&c)[MAXDV]) const {
-        constexpr int COL = G::VAR_COLS[P::C0 + I], P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
-        sfor<DV>([&](auto jj) {
-            constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
-            constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
-            c[J] = lds_rd(C.lds + SL * 256, rot[SI]);
-        });
-    }
-
-    // v2c_e = llr + sum_{e' != e} c_e' in ascending check order (traditional_decoders.py:235-250):
-    // acc[e] = P_e (prefix) then + c_{e+1} + ... ; in pairs, one v_pk_add_f32 adds c to two
-    // running sums (two independent IEEE fp32 adds, the same sequence per element)
-    template <int I, bool DEC, bool WRITE>
-    __device__ __forceinline__ void col(const Ctx &C, const Lane &L, const float (&c)[MAXDV], int &errs,
-                                        bool &bad, float &mz) const {
-        constexpr int COL = G::VAR_COLS[P::C0 + I], P0 = G::COL_PTR[COL], DV = G::COL_PTR[COL + 1] - P0;
-        float Pp = cllr[I];
-        f32x2 acc[(DV + 1) / 2];
-#if LDPC_VAR_PK
-        sfor<DV>([&](auto jj) {
+    template <int TK>
+    __device__ __forceinline__ void load_task(const Ctx &C, TaskIn &in) const {
+        using K = Task<TK>;
+        sfor<K::DA>([&](auto jj) {
             constexpr int J = decltype(jj)::value;
-            const f32x2 cc = {c[J], c[J]};
-            sfor<J / 2>([&](auto p) { acc[decltype(p)::value] = acc[decltype(p)::value] + cc; });
-            if constexpr (J % 2 == 1) {
-                acc[J / 2].x = acc[J / 2].x + c[J];
-                acc[J / 2].y = Pp;
+            constexpr int SA = G::COL_SLOT[K::PA + J], RA = P::T.shidx[G::COL_SHIFT[K::PA + J]];
+            if constexpr (J < K::DB) {
+                constexpr int SB = G::COL_SLOT[K::PB + J], RB = P::T.shidx[G::COL_SHIFT[K::PB + J]];
+                in.cp[J].x = lds_rd(C.lds + SA * 256, rot[RA]);
+                in.cp[J].y = lds_rd(C.lds + SB * 256, rot[RB]);
             } else {
-                acc[J / 2].x = Pp;
+                in.cs[J] = lds_rd(C.lds + SA * 256, rot[RA]);
             }
-            Pp = Pp + c[J];
         });
-#else
-        // scalar v_add_f32 (measured 6 % faster for the whole kernel than v_pk_add_f32 pairs: the
-        // running sums are dependency chains, and a packed add's chain latency is longer)
-        float a[DV];
-        sfor<DV>([&](auto jj) {
+    }
+
+    template <int TK, bool DEC, bool WRITE>
+    __device__ __forceinline__ void task(const Ctx &C, const Lane &L, const TaskIn &in, int &errs, bool &bad,
+                                         float &mz) const {
+        using K = Task<TK>;
+        constexpr int DA = K::DA, DB = K::DB, LO = K::LO, HI = K::HI;
+        f32x2 P2;
+        float PA = cllr[K::IA];
+        if constexpr (DB > 0) {
+            P2.x = cllr[K::IA];
+            P2.y = cllr[K::IB];
+        }
+        f32x2 acc2[DB > 0 ? DB : 1];
+        float accA[DA];
+        sfor<DA>([&](auto jj) {
             constexpr int J = decltype(jj)::value;
-            sfor<J>([&](auto p) { a[decltype(p)::value] = a[decltype(p)::value] + c[J]; });
-            a[J] = Pp;
-            Pp = Pp + c[J];
+            constexpr int EN = (J < HI ? J : HI) - LO;  // outputs [LO, min(J, HI)) take c_J
+            if constexpr (J < DB) {
+                if constexpr (EN > 0)
+                    sfor<EN>([&](auto q) {
+                        constexpr int E = LO + decltype(q)::value;
+                        acc2[E] = acc2[E] + in.cp[J];
+                    });
+                if constexpr (LO <= J && J < HI) acc2[J] = P2;
+                if constexpr (J < K::NPREF) P2 = P2 + in.cp[J];
+                if constexpr (J == DB - 1) PA = P2.x;
+            } else {
+                if constexpr (EN > 0)
+                    sfor<EN>([&](auto q) {
+                        constexpr int E = LO + decltype(q)::value;
+                        if constexpr (E < DB)
+                            acc2[E].x = acc2[E].x + in.cs[J];
+                        else
+                            accA[E] = accA[E] + in.cs[J];
+                    });
+                if constexpr (LO <= J && J < HI) accA[J] = PA;
+                if constexpr (J < K::NPREF) PA = PA + in.cs[J];
+            }
         });
-        sfor<DV>([&](auto jj) {
-            constexpr int J = decltype(jj)::value;
-            if constexpr (J % 2 == 0) acc[J / 2].x = a[J]; else acc[J / 2].y = a[J];
-        });
-#endif
         if constexpr (WRITE) {
-            sfor<DV>([&](auto jj) {
-                constexpr int J = decltype(jj)::value, SL = G::COL_SLOT[P0 + J];
-                constexpr int SI = P::T.shidx[G::COL_SHIFT[P0 + J]];
-                lds_wr(C.lds + SL * 256, rot[SI], J % 2 == 0 ? acc[J / 2].x : acc[J / 2].y);
+            sfor<HI - LO>([&](auto q) {
+                constexpr int E = LO + decltype(q)::value;
+                constexpr int SA = G::COL_SLOT[K::PA + E], RA = P::T.shidx[G::COL_SHIFT[K::PA + E]];
+                if constexpr (E < DB) {
+                    constexpr int SB = G::COL_SLOT[K::PB + E], RB = P::T.shidx[G::COL_SHIFT[K::PB + E]];
+                    lds_wr(C.lds + SA * 256, rot[RA], acc2[E].x);
+                    lds_wr(C.lds + SB * 256, rot[RB], acc2[E].y);
+                    // smallest |v2c| written: a zero sets the flag (v_minimum3: no canonicalising
+                    // v_max; a NaN here implies a non-finite APP, caught by `bad`)
+                    if constexpr (ALGO == LDPC_ALGO_MINSUM) mz = vmin(vmin(mz, fabsf(acc2[E].x)), fabsf(acc2[E].y));
+                } else {
+                    lds_wr(C.lds + SA * 256, rot[RA], accA[E]);
+                    if constexpr (ALGO == LDPC_ALGO_MINSUM) {
+                        // two A-only outputs per v_minimum3
+                        if constexpr ((E - (DB > LO ? DB : LO)) % 2 == 1)
+                            mz = vmin(vmin(mz, fabsf(accA[E - 1])), fabsf(accA[E]));
+                        else if constexpr (E == HI - 1)
+                            mz = vmin(mz, fabsf(accA[E]));
+                    }
+                }
             });
-#if LDPC_ZFLAG
-            if constexpr (ALGO == LDPC_ALGO_MINSUM) {  // smallest |v2c| written: a zero sets the flag
-                sfor<(DV + 1) / 2>([&](auto pp) {
-                    constexpr int Q = decltype(pp)::value;
-#if LDPC_MIN3  // v_minimum3: no canonicalising v_max (a NaN here implies a non-finite APP: `bad`)
-                    if constexpr (2 * Q + 1 < DV)
-                        mz = vmin(vmin(mz, fabsf(acc[Q].x)), fabsf(acc[Q].y));
-                    else
-                        mz = vmin(mz, fabsf(acc[Q].x));
-#else
-                    if constexpr (2 * Q + 1 < DV)
-                        mz = fminf(mz, fminf(fabsf(acc[Q].x), fabsf(acc[Q].y)));
-                    else
-                        mz = fminf(mz, fabsf(acc[Q].x));
-#endif
-                });
-            }
-#endif
         }
         // a NaN v2c implies a NaN or infinite APP of its column (every summand of a v2c is a
         // summand of the APP; +-inf is absorbing), so this flag bounds the fast check path
-        if constexpr (ALGO == LDPC_ALGO_MINSUM) bad |= !(fabsf(Pp) < INFINITY);
-        if constexpr (DEC) {
-            if (C.direct_bits || C.ballots) var_decision(C, L, COL, Pp, errs);
+        if constexpr (HI == DA) {
+            if constexpr (ALGO == LDPC_ALGO_MINSUM) bad |= !(fabsf(PA) < INFINITY);
+            if constexpr (DEC) {
+                if (C.direct_bits || C.ballots) var_decision(C, L, K::CA, PA, errs);
+            }
+        }
+        if constexpr (K::BLAST) {
+            if constexpr (ALGO == LDPC_ALGO_MINSUM) bad |= !(fabsf(P2.y) < INFINITY);
+            if constexpr (DEC) {
+                if (C.direct_bits || C.ballots) var_decision(C, L, K::CB, P2.y, errs);
+            }
         }
     }
 
@@ -1242,27 +1223,29 @@ struct FixedBody {
     __device__ __forceinline__ void var(const Ctx &C, const Lane &L, int &errs) const {
         bool bad = false;
         float mz = INFINITY;
-        if constexpr (P::NC > 0) {
-            float ca[MAXDV], cb[MAXDV];
-            load_col<0>(C, ca);
-            sfor<P::NC>([&](auto i) {
+        if constexpr (P::NT > 0) {
+            // software pipelining: the next task's reads are issued before the current task's adds
+            // when the two hold at most kVarPipe messages together (slots are disjoint between
+            // tasks, so the reads never depend on the writes in flight)
+            TaskIn ta, tb;
+            load_task<0>(C, ta);
+            sfor<P::NT>([&](auto i) {
                 constexpr int I = decltype(i)::value;
-                constexpr bool ahead = I + 1 < P::NC && dv_of(I) + dv_of(I + 1) <= kVarPipe;
+                constexpr bool more = I + 1 < P::NT;
+                constexpr bool ahead = more && Task<I>::NMSG + Task<(more ? I + 1 : I)>::NMSG <= kVarPipe;
                 if constexpr (I % 2 == 0) {
-                    if constexpr (ahead) load_col<I + 1>(C, cb);
-                    col<I, DEC, WRITE>(C, L, ca, errs, bad, mz);
-                    if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, cb);
+                    if constexpr (ahead) load_task<I + 1>(C, tb);
+                    task<I, DEC, WRITE>(C, L, ta, errs, bad, mz);
+                    if constexpr (more && !ahead) load_task<(more ? I + 1 : I)>(C, tb);
                 } else {
-                    if constexpr (ahead) load_col<I + 1>(C, ca);
-                    col<I, DEC, WRITE>(C, L, cb, errs, bad, mz);
-                    if constexpr (I + 1 < P::NC && !ahead) load_col<I + 1>(C, ca);
+                    if constexpr (ahead) load_task<I + 1>(C, ta);
+                    task<I, DEC, WRITE>(C, L, tb, errs, bad, mz);
+                    if constexpr (more && !ahead) load_task<(more ? I + 1 : I)>(C, ta);
                 }
             });
         }
         if constexpr (ALGO == LDPC_ALGO_MINSUM) {
-#if LDPC_ZFLAG
             bad |= mz == 0.0f;
-#endif
             if (__any(bad) && L.lane == 0) *C.flag = 1;
         }
         (void)mz;

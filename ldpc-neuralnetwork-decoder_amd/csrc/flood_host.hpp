@@ -23,15 +23,6 @@ int launch_fixed_bp(int fixed_id, int es, dim3 grid, dim3 block, size_t lds, hip
                     const float *llr, int64_t B, int max_iter, float alpha, int out_dtype, void *bits, const Outs &O,
                     const EsWs &W);
 
-// flood_pair.hip: the frame-pair kernel (no early stop) for fixed_id 1 / 2, nwg workgroups
-int launch_pair_kernel(int algo, int fixed_id, int64_t nwg, hipStream_t s, const float *llr, int64_t B,
-                       int max_iter, float alpha, int out_dtype, void *bits, const Outs &O);
-
-// flood_w6.hip: the 6-wave kernel (no early stop) for fixed_id 1 / 2, one-frame LDS image (lds bytes)
-int launch_w6_kernel(int algo, int fixed_id, int64_t nwg, size_t lds, hipStream_t s, const FloodTables &T,
-                     const float *llr, int64_t B, int max_iter, float alpha, int out_dtype, void *bits,
-                     const Outs &O);
-
 // flood_stream.hip: the streaming decoders (messages in HBM, any graph)
 int64_t stream_ws_bytes(const ldpc_graph *g, int64_t B, int max_iter);
 int run_stream_decode(int algo, const ldpc_graph *g, const float *llr, int64_t B, int max_iter, float alpha, int es,

@@ -1032,7 +1032,7 @@ __global__ void csr_sort_kernel(const int32_t *__restrict__ ptr, int N, int32_t 
 }
 __global__ void gnn_output_csr_kernel(const float *__restrict__ msg_out, const int32_t *__restrict__ ints,
                                       const float *__restrict__ llr, int64_t E, int N, int64_t n,
-                                      const uint8_t *__restrict__ active, float *__restrict__ probs, int var_major) {
+                                      const uint8_t *__restrict__ active, float *__restrict__ probs) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t b = i / N;
@@ -1041,7 +1041,7 @@ __global__ void gnn_output_csr_kernel(const float *__restrict__ msg_out, const i
     const int32_t *ptr = ints, *mem = ints + 2 * N + 2;
     const float *mo = msg_out + b * E;
     float s = 0.0f;  // var_llrs[var] += decoded_llrs[b, msg] in ascending msg (:277-296)
-    for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[var_major ? q : mem[q]];
+    for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[mem[q]];
     probs[i] = 1.0f / (1.0f + expf(-(s + llr[i])));  // sigmoid(var_llrs + input_llr) (:298-307)
 }
 
@@ -1250,10 +1250,10 @@ int ldpc::gnn_build_var_csr(const int32_t *d_msg_var, int64_t E, int N, int32_t 
 }
 
 int ldpc::gnn_output(const float *d_msg_out, const int32_t *d_ints, const float *d_llr, int64_t E, int N, int64_t B,
-                     const uint8_t *d_active, float *d_probs, hipStream_t s, bool var_major) {
+                     const uint8_t *d_active, float *d_probs, hipStream_t s) {
     const int64_t n = B * N;
     hipLaunchKernelGGL(gnn_output_csr_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_msg_out, d_ints,
-                       d_llr, E, N, n, d_active, d_probs, var_major ? 1 : 0);
+                       d_llr, E, N, n, d_active, d_probs);
     LDPC_CHECK_LAUNCH("gnn_output_csr_kernel");
     return LDPC_OK;
 }

@@ -52,11 +52,9 @@ namespace ldpc {
 // Workspace: gnn_csr_ints(E, N) int32 words.
 inline int64_t gnn_csr_ints(int64_t E, int N) { return 2LL * N + 2 + E; }
 int gnn_build_var_csr(const int32_t *d_msg_var, int64_t E, int N, int32_t *d_ints, hipStream_t s);
-// probs[b][v] = sigmoid(sum_{m -> v} msg_out[b][m] + llr[b][v]) for frames with active[b] (null = all);
-// var_major: msg_out rows are stored in the CSR's variable-major order (bf16 path), so v's messages
-// are the contiguous slots ptr[v] .. ptr[v + 1] (the same ascending order, the same sums)
+// probs[b][v] = sigmoid(sum_{m -> v} msg_out[b][m] + llr[b][v]) for frames with active[b] (null = all)
 int gnn_output(const float *d_msg_out, const int32_t *d_ints, const float *d_llr, int64_t E, int N, int64_t B,
-               const uint8_t *d_active, float *d_probs, hipStream_t s, bool var_major = false);
+               const uint8_t *d_active, float *d_probs, hipStream_t s);
 __device__ __forceinline__ const int32_t *csr_ptr(const int32_t *ints) { return ints; }
 __device__ __forceinline__ const int32_t *csr_mem(const int32_t *ints, int N) { return ints + 2 * N + 2; }
 

@@ -47,9 +47,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int H = 64;
-#ifndef LDPC_BF16_RELU_I16
-#define LDPC_BF16_RELU_I16 1
-#endif
+constexpr int kMlpThreads = 256;  // the MLP kernel's workgroup (4 waves), 2 waves per SIMD
 
 __host__ __device__ constexpr int pi_unit(int p) {
     return 32 * (p >> 5) + 16 * ((p >> 4) & 1) + 8 * ((p >> 2) & 1) + 4 * ((p >> 3) & 1) + (p & 3);
@@ -115,20 +113,6 @@ __global__ void gnn_bf16_info_kernel(int E, const int32_t *vgroup, const int32_t
     const int g = vgroup[m];
     const bool one = d1 && vg_ptr[g + 1] - vg_ptr[g] == 1;
     info[m] = make_int4(one ? ~g : g, cgroup[m], msg_type[m], msg_var[m]);
-}
-
-// Projected MLP: per tile slot i of the plan's message order (gnn.hpp mt_perm),
-// {var group (~ when degree 1 and d1), check group, type | variable << 8, message (-1 = padding)};
-// padding slots carry message 0's groups (valid addresses, nothing written).
-__global__ void gnn_bf16_info_perm_kernel(int n, const int32_t *perm, const int32_t *vgroup, const int32_t *vg_ptr,
-                                          int d1, const int32_t *cgroup, const int32_t *msg_type,
-                                          const int32_t *msg_var, int4 *info) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int mp = perm[i], m = mp < 0 ? 0 : mp;
-    const int g = vgroup[m];
-    const bool one = d1 && vg_ptr[g + 1] - vg_ptr[g] == 1;
-    info[i] = make_int4(one ? ~g : g, cgroup[m], msg_type[m] | (msg_var[m] << 8), mp);
 }
 
 struct GtArgs {
@@ -252,156 +236,15 @@ __device__ __forceinline__ bf16x8 relu8(const f32x16 &a, int half) {
     bf16x8 o;
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (__bf16)a[8 * half + i];
-#if LDPC_BF16_RELU_I16
     s16x8 b = __builtin_bit_cast(s16x8, o);
     b = __builtin_elementwise_max(b, (s16x8)0);
     return __builtin_bit_cast(bf16x8, b);
-#else
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (__bf16)fmaxf(a[8 * half + i], 0.0f);
-    return o;
-#endif
 }
 __device__ __forceinline__ bf16x8 pack8(const f32x16 &a, int half) {
     bf16x8 o;
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (__bf16)a[8 * half + i];
     return o;
-}
-
-// ------------------------------------------------------------------------ projected group rows
-// (opt-in, LDPC_GNN_BF16_PROJ=1; measured slower than the group-mean rows above).  As the fp32 path (gnn.hip):
-// W1_s,right g is one row per GROUP, so it is computed here once per group and the MLP starts
-// GEMM1 from it: the MLP's GEMM1 runs over x alone, 32 instead of 48 MFMAs per 32-message tile.
-// One wave per (frame, projection tile of 32 groups of one side): lane (q, c) sums stored
-// positions 8c .. 8c+7 of the tile's groups 8p + q (p < 4, ascending members, two members of all
-// four in flight), x 1/|group| + the group's mean type embedding, rounded to bf16 -- the same row
-// the group-mean kernel writes -- into the wave's LDS tile; lane (j, h) then reads group j's row
-// as the B operand of 2 x 4 v_mfma_f32_32x32x16_bf16 against W1_right (bf16, LDS) and writes the
-// product in bf16, in the features' stored order, to Pv / Pc (the Mv / Mc buffers).  No bias:
-// b1 is in the type constants.
-constexpr int kPjRow = 144;  // bytes per LDS row: 64 bf16 + 8 pad
-inline size_t proj_lds_bytes_bf16(int waves) { return (size_t)(2 + waves / 2) * 64 * kPjRow; }
-
-struct PjArgs {
-    const __bf16 *x_in;  // null at layer 0
-    const float *llr;
-    const int32_t *msg_var;
-    const float *w_in, *b_in;
-    const float *memb;  // this layer, (Gv + Gc, 64) fp32 stored order
-    const float *w1v, *w1c;
-    const int4 *meta;
-    const int32_t *grp, *deg, *mem;
-    int n_tiles, first;
-    __bf16 *Pv, *Pc;
-    const uint8_t *active;
-    const int32_t *list, *count;
-    int Gv, Gc, E, N;
-    int64_t B;
-};
-
-template <int NT>
-__global__ __launch_bounds__(NT) void gnn_bf16_proj_kernel(PjArgs A) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < 64 * 64; i += NT) {
-        const int u = i >> 6, p = i & 63, k = 64 + pi_unit(p);
-        reinterpret_cast<__bf16 *>(smem)[u * (kPjRow / 2) + p] = (__bf16)A.w1v[u * 128 + k];
-        reinterpret_cast<__bf16 *>(smem + 64 * kPjRow)[u * (kPjRow / 2) + p] = (__bf16)A.w1c[u * 128 + k];
-    }
-    __syncthreads();
-    const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
-    const int q = lane >> 3, c8 = 8 * (lane & 7);
-    char *tile = smem + 2 * 64 * kPjRow + wave * 32 * kPjRow;
-    const int nt = A.n_tiles - A.first;
-    const int64_t nact = A.count ? (int64_t)__builtin_amdgcn_readfirstlane(*A.count) : A.B;
-    const TileWalk tw = xcd_tiles(nact * nt, NT / 64, wave);
-    for (int64_t tt = tw.first; tt < tw.end; tt += tw.stride) {
-        const int64_t slot = tt / nt;
-        const int t = A.first + (int)(tt - slot * nt);
-        const int64_t b = A.list ? (int64_t)A.list[slot] : slot;
-        if (A.active && !A.active[b]) continue;
-        const int4 md = A.meta[t];  // {side, max degree, member offset, 0}
-        int dg[4];
-        float acc[4][8];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            dg[p] = A.deg[32 * t + 8 * p + q];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc[p][k] = 0.0f;
-        }
-        const int32_t *mem = A.mem + md.z + q;
-        if (A.x_in) {
-            const __bf16 *xb = A.x_in + b * A.E * H + c8;
-            for (int i = 0; i < md.y; i += 2) {  // the table holds max degree + 1 rows
-                bf16x8 v[4], w[4];
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    v[p] = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)mem[32 * i + 8 * p] * H);
-                    w[p] = *reinterpret_cast<const bf16x8 *>(xb + (int64_t)mem[32 * (i + 1) + 8 * p] * H);
-                }
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    if (i < dg[p]) {
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) acc[p][k] += (float)v[p][k];
-                    }
-                    if (i + 1 < dg[p]) {
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) acc[p][k] += (float)w[p][k];
-                    }
-                }
-            }
-        } else {
-            float ls[4] = {};
-            for (int i = 0; i < md.y; ++i) {
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    if (i < dg[p]) ls[p] += A.llr[b * A.N + A.msg_var[mem[32 * i + 8 * p]]];
-            }
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int u = pi_unit(c8 + k);
-                    acc[p][k] = fmaf(A.w_in[u], ls[p], (float)dg[p] * A.b_in[u]);
-                }
-        }
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int s = 8 * p + q, g = A.grp[32 * t + s];
-            bf16x8 o;
-            if (g >= 0) {
-                const float *e = A.memb + (int64_t)(md.x ? A.Gv + g : g) * H + c8;
-                const float inv = 1.0f / (float)dg[p];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) o[k] = (__bf16)fmaf(acc[p][k], inv, e[k]);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) o[k] = (__bf16)0.0f;
-            }
-            *reinterpret_cast<bf16x8 *>(tile + s * kPjRow + 2 * c8) = o;
-        }
-        __builtin_amdgcn_wave_barrier();
-        bf16x8 gb[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) gb[s] = ld8(tile + j * kPjRow + 16 * h + 32 * s);
-        __builtin_amdgcn_wave_barrier();
-        const char *W = smem + (md.x ? 64 * kPjRow : 0);
-        f32x16 h0 = {}, h1 = {};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W + j * kPjRow + 16 * h + 32 * s), gb[s], h0, 0, 0, 0);
-            h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W + (32 + j) * kPjRow + 16 * h + 32 * s), gb[s], h1, 0, 0, 0);
-        }
-        const int g = A.grp[32 * t + j];
-        if (g < 0) continue;
-        char *dst = reinterpret_cast<char *>(md.x ? A.Pc + (b * A.Gc + g) * H : A.Pv + (b * A.Gv + g) * H) + 16 * h;
-        *reinterpret_cast<bf16x8 *>(dst) = pack8(h0, 0);
-        *reinterpret_cast<bf16x8 *>(dst + 32) = pack8(h0, 1);
-        *reinterpret_cast<bf16x8 *>(dst + 64) = pack8(h1, 0);
-        *reinterpret_cast<bf16x8 *>(dst + 96) = pack8(h1, 1);
-    }
 }
 
 // ------------------------------------------------------------------------ fused MLP
@@ -412,10 +255,6 @@ __global__ __launch_bounds__(NT) void gnn_bf16_proj_kernel(PjArgs A) {
 constexpr int kW1B = 64 * 136 * 2, kW2B = 64 * 72 * 2;
 constexpr int kOffW1v = 0, kOffW1c = kW1B, kOffW2v = 2 * kW1B, kOffW2c = 2 * kW1B + kW2B;
 constexpr int kOffK = 2 * kW1B + 2 * kW2B;
-// projected MLP (MODE bit 2): W1v,left, W1c,left, W1v,left + W1v,right (degree-1 tiles) bf16
-// [64 u][72], W2v, W2c [64 o][72], then the fp32 part as above
-constexpr int kPOffW1v = 0, kPOffW1c = kW2B, kPOffW1s = 2 * kW2B, kPOffW2v = 3 * kW2B, kPOffW2c = 4 * kW2B;
-constexpr int kPOffK = 5 * kW2B;
 constexpr int kKStride = 132;
 // D1 rows: 68 floats apart (a row stride of 64 put every type's row on the same LDS banks: the
 // 16-lane groups of a ds_read_b128 with lanes of different types serialised up to 16-way)
@@ -423,27 +262,23 @@ constexpr int kKStride = 132;
 #define LDPC_BF16_D1_STRIDE 68
 #endif
 constexpr int kD1Stride = LDPC_BF16_D1_STRIDE;
-inline size_t mlp_lds_bytes(int T, bool d1, bool proj) {
-    return (size_t)(proj ? kPOffK : kOffK) + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * kD1Stride : 0)) * 4;
+inline size_t mlp_lds_bytes(int T, bool d1) {
+    return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * kD1Stride : 0)) * 4;
 }
 
 struct MlpArgs {
     const __bf16 *x_in;  // null at layer 0
     __bf16 *x_out;       // null at the last layer
-    const __bf16 *Mv, *Mc;               // group-mean rows, or (projected) W1_right g rows
-    const int4 *info;                    // per message {var group, check group, type, variable};
-                                         // projected: per tile slot (gnn_bf16_info_perm_kernel)
+    const __bf16 *Mv, *Mc;               // group-mean rows
+    const int4 *info;                    // per message {var group, check group, type, variable}
     const float *llr;
     const float *w1v, *w1c, *w2v, *w2c;  // this layer, nn.Linear layout, fp32
     const float *kd;                     // this layer's derived constants
     const float *bo;                     // output_projection bias (device)
     int T, Gv, Gc, E, N, tpf;            // tpf = 32-message tiles per frame
-    int tpf1;                            // projected: the leading tiles of degree-1 messages
     int d1;                              // degree-1 var groups use D1 (info.x < 0), layers >= 1
     int64_t B;
-    float *msg_out;                      // last layer / early termination: (B, E) projected LLRs,
-    const int32_t *vpos;                 // ... stored variable-major: message m at vpos[m] (the
-                                         // position of m in the per-call CSR of msg_var)
+    float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
     const uint8_t *active;               // early termination: frames still decoding (null = all)
     const int32_t *list, *count;         // early termination: the frames still decoding (see GmArgs)
     const float *kd_last, *bo_last;      // early termination: the last layer's output projection
@@ -455,41 +290,25 @@ struct TileIn {
     float l;
     int ty, var;
     bool one;  // degree-1 var group (D1 constant instead of K[ty][var side])
-    bool t1;   // projected: a tile of degree-1 messages (uniform over the wave)
     int64_t row, b;
-    int mpos;     // the message's slot in the variable-major msg_out row
     bool ok, on;  // on: the frame is still decoding (early termination)
 };
 
 // MODE bit 0: layer 0 (x from the LLRs, no GEMM1 over x, no residual); bit 1: last layer
-// (output projection + per-variable sum instead of writing x); bit 2: projected group rows
-// (GEMM1 over x only, started from K + the group's W1_right g row; tiles in the plan's message
-// order, whose degree-1 tiles run GEMM1 over x with W1v,left + W1v,right and D1)
-// PF: 0 no register prefetch; 1 the next tile's rows one tile ahead; 2 (non-projected, layers >= 1)
-// as 1, and the feature rows -- the HBM part of a tile -- two tiles ahead; 3 as 1, the group rows
-// two tiles ahead; 4 as 1, both sides' GEMM1 before either GEMM2
-template <int NT, int WPS, int PF, int MODE>
-__global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
+// (output projection + per-variable sum instead of writing x).  The next tile's rows are
+// prefetched into registers one tile ahead, the small per-tile items two tiles ahead.
+template <int MODE>
+__global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
-    constexpr bool proj = (MODE & 4) != 0;
-    constexpr int oW1v = proj ? kPOffW1v : kOffW1v, oW1c = proj ? kPOffW1c : kOffW1c;
-    constexpr int oW2v = proj ? kPOffW2v : kOffW2v, oW2c = proj ? kPOffW2c : kOffW2c;
-    constexpr int w1row = proj ? 144 : 272;  // bytes per W1 image row
-    if constexpr (proj) {
-        for (int i = tid; i < 64 * 64; i += NT) {
-            const int u = i >> 6, p = i & 63, k = pi_unit(p);
-            reinterpret_cast<__bf16 *>(smem + kPOffW1v)[u * 72 + p] = (__bf16)A.w1v[u * 128 + k];
-            reinterpret_cast<__bf16 *>(smem + kPOffW1c)[u * 72 + p] = (__bf16)A.w1c[u * 128 + k];
-            reinterpret_cast<__bf16 *>(smem + kPOffW1s)[u * 72 + p] = (__bf16)(A.w1v[u * 128 + k] + A.w1v[u * 128 + 64 + k]);
-        }
-    } else {
-        for (int i = tid; i < 64 * 128; i += NT) {
-            const int u = i >> 7, p = i & 127;
-            const int k = p < 64 ? pi_unit(p) : 64 + pi_unit(p - 64);
-            reinterpret_cast<__bf16 *>(smem + kOffW1v)[u * 136 + p] = (__bf16)A.w1v[u * 128 + k];
-            reinterpret_cast<__bf16 *>(smem + kOffW1c)[u * 136 + p] = (__bf16)A.w1c[u * 128 + k];
-        }
+    constexpr int NT = kMlpThreads;
+    constexpr int oW1v = kOffW1v, oW1c = kOffW1c, oW2v = kOffW2v, oW2c = kOffW2c;
+    constexpr int w1row = 272;  // bytes per W1 image row
+    for (int i = tid; i < 64 * 128; i += NT) {
+        const int u = i >> 7, p = i & 127;
+        const int k = p < 64 ? pi_unit(p) : 64 + pi_unit(p - 64);
+        reinterpret_cast<__bf16 *>(smem + kOffW1v)[u * 136 + p] = (__bf16)A.w1v[u * 128 + k];
+        reinterpret_cast<__bf16 *>(smem + kOffW1c)[u * 136 + p] = (__bf16)A.w1c[u * 128 + k];
     }
     for (int i = tid; i < 64 * 64; i += NT) {
         const int o = i >> 6, q = i & 63;
@@ -497,7 +316,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         reinterpret_cast<__bf16 *>(smem + oW2v)[o * 72 + q] = (__bf16)A.w2v[o * 64 + u];
         reinterpret_cast<__bf16 *>(smem + oW2c)[o * 72 + q] = (__bf16)A.w2c[o * 64 + u];
     }
-    float *Ks = reinterpret_cast<float *>(smem + (proj ? kPOffK : kOffK));
+    float *Ks = reinterpret_cast<float *>(smem + kOffK);
     const int nk = (A.T + 2) * 128;
     for (int i = tid; i < nk; i += NT) Ks[(i >> 7) * kKStride + (i & 127)] = A.kd[i];
     float *tail = Ks + (A.T + 2) * kKStride;  // b2 [64], wo [64]
@@ -522,55 +341,23 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     // per-message static info {var group, check group, type, variable} of this lane's message
     auto load_info = [&](int64_t k) {
         const int m0 = (int)k * 32 + j;
-        if constexpr (proj) return A.info[m0];  // one entry per tile slot
         return A.info[m0 < A.E ? m0 : A.E - 1];
     };
     // the frame's "still decoding" flag of tile t (frame b), read ahead of the tile's row loads
     auto load_on = [&](int64_t t, int64_t b) -> bool {
         return A.list || !A.active || A.active[t < tw.end ? b : fb];  // listed frames are active
     };
-    // the feature rows of tile t (frame slot b, in-frame tile k) alone: PF 2 issues them a tile
-    // before the rest of the tile's loads (a terminated frame's rows are loaded too: harmless)
-    struct XRows { bf16x8 v[4]; };
-    auto load_x = [&](int64_t t, int64_t b, int64_t k) {
-        XRows X;
-        const int m0 = (int)k * 32 + j;
-        const int64_t bb = frame_of(t < tw.end ? b : fb);
-        const char *xr = reinterpret_cast<const char *>(A.x_in + (bb * A.E + (m0 < A.E ? m0 : A.E - 1)) * H) + 16 * h;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) X.v[s] = ld8(xr + 32 * s);
-        return X;
-    };
-    // the group rows of tile t alone (PF 3 issues them a tile before the rest of the tile's loads)
-    struct GRows { bf16x8 a[4], c[4]; };
-    auto load_g = [&](const int4 &inf, bool on, int64_t t, int64_t b) {
-        GRows G;
-        const int64_t lb = on ? frame_of(t < tw.end ? b : fb) : 0;
-        const int vg = inf.x < 0 ? ~inf.x : inf.x;
-        const char *ma = reinterpret_cast<const char *>(A.Mv + (lb * A.Gv + vg) * H) + 16 * h;
-        const char *mc = reinterpret_cast<const char *>(A.Mc + (lb * A.Gc + inf.y) * H) + 16 * h;
-        if (layer0 || !A.d1 || inf.x >= 0) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) G.a[s] = ld8(ma + 32 * s);
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) G.c[s] = ld8(mc + 32 * s);
-        return G;
-    };
-    auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k, const XRows *xpre = nullptr,
-                    const GRows *gpre = nullptr) {
+    auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k) {
         TileIn I;
         const int m0 = (int)k * 32 + j;
-        I.ok = (proj ? inf.w >= 0 : m0 < A.E) && t < tw.end;
-        const int m = proj ? (inf.w < 0 ? 0 : inf.w) : m0 < A.E ? m0 : A.E - 1;
+        I.ok = m0 < A.E && t < tw.end;
+        const int m = m0 < A.E ? m0 : A.E - 1;
         const int64_t bb = frame_of(t < tw.end ? b : fb);
-        I.ty = proj ? (inf.z & 255) : inf.z;
-        I.var = proj ? (inf.z >> 8) : inf.w;
+        I.ty = inf.z;
+        I.var = inf.w;
         I.one = !layer0 && A.d1 && inf.x < 0;
-        I.t1 = proj && !layer0 && A.d1 && k < A.tpf1;
         I.row = bb * A.E + m;
         I.b = bb;
-        I.mpos = (!last && !A.kd_last) ? 0 : A.vpos[m];
         I.on = on;
         // A terminated frame (uniform over the tile) loads frame 0's rows instead of its own:
         // L2 hits, and no branch around the loads -- a branch here makes the compiler wait for
@@ -580,33 +367,14 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         const char *ma = reinterpret_cast<const char *>(A.Mv + (lb * A.Gv + vg) * H) + 16 * h;
         const char *mc = reinterpret_cast<const char *>(A.Mc + (lb * A.Gc + inf.y) * H) + 16 * h;
         if constexpr (!layer0) {
-            if (xpre) {
+            const char *xr = reinterpret_cast<const char *>(A.x_in + (lb * A.E + m) * H) + 16 * h;
 #pragma unroll
-                for (int s = 0; s < 4; ++s) I.xf[s] = xpre->v[s];
-            } else {
-                const char *xr = reinterpret_cast<const char *>(A.x_in + (lb * A.E + m) * H) + 16 * h;
-#pragma unroll
-                for (int s = 0; s < 4; ++s) I.xf[s] = ld8(xr + 32 * s);
-            }
+            for (int s = 0; s < 4; ++s) I.xf[s] = ld8(xr + 32 * s);
             I.l = 0.0f;
         } else {
             I.l = A.llr[lb * A.N + I.var];
         }
-        if (gpre) {  // PF 3: the group rows came two tiles ahead
-            const bool own = layer0 || !A.d1 || inf.x >= 0;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                I.af[s] = own ? gpre->a[s] : I.xf[s];
-                I.cf[s] = gpre->c[s];
-            }
-            return I;
-        }
-        if constexpr (proj) {
-            if (!I.t1) {  // degree-1 tiles need no W1_right g row (D1 + W1v,left+right x)
-#pragma unroll
-                for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
-            }
-        } else if (layer0 || !A.d1 || inf.x >= 0) {
+        if (layer0 || !A.d1 || inf.x >= 0) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
         } else {  // degree-1 var group: g = x, its emb part is in D1
@@ -624,25 +392,12 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
         f32x16 y0 = ld16(tail + 16 * h), y1 = ld16(tail + 32 + 16 * h);  // b2v + b2c
         int wbase = j * w1row + 16 * h, w2base = j * 144 + 16 * h;
         asm volatile("" : "+v"(wbase), "+v"(w2base));
-        // GEMM1 of one side into (h0, h1), then ReLU + GEMM2 into y.  PF 4 runs both sides' GEMM1
-        // before either GEMM2, so one side's ReLU can issue beside the other side's MFMAs (the
-        // same operations in the same order per accumulator: bitwise the same result)
+        // GEMM1 of one side into (h0, h1), then ReLU + GEMM2 into y
         auto gemm1 = [&](int side, f32x16 &h0, f32x16 &h1) {
-            const char *W1 = smem + (side == 0 ? (proj && I.t1 ? kPOffW1s : oW1v) : oW1c);
-            const bool d1k = proj ? I.t1 : I.one;
-            const float *K0 = side == 0 && d1k ? D1s + I.ty * kD1Stride : Kt + side * 64;
+            const char *W1 = smem + (side == 0 ? oW1v : oW1c);
+            const float *K0 = side == 0 && I.one ? D1s + I.ty * kD1Stride : Kt + side * 64;
             h0 = ld16(K0 + 16 * h);
             h1 = ld16(K0 + 32 + 16 * h);
-            if (proj && !(side == 0 && I.t1)) {  // + the group's W1_right g row (bf16)
-                const bf16x8 *P = side == 0 ? I.af : I.cf;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    h0[i] += (float)P[0][i];
-                    h0[8 + i] += (float)P[1][i];
-                    h1[i] += (float)P[2][i];
-                    h1[8 + i] += (float)P[3][i];
-                }
-            }
             if constexpr (layer0) {  // + llr * (W1 w_in) + W1 b_in
                 const float *U = Ks + A.T * kKStride + side * 64 + 16 * h, *V = U + kKStride;
 #pragma unroll
@@ -657,13 +412,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                     h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * w1row + wbase + 32 * s), I.xf[s], h1, 0, 0, 0);
                 }
             }
-            if constexpr (!proj) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const bf16x8 g = side == 0 ? I.af[s] : I.cf[s];
-                    h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + wbase + 32 * (4 + s)), g, h0, 0, 0, 0);
-                    h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * (4 + s)), g, h1, 0, 0, 0);
-                }
+            for (int s = 0; s < 4; ++s) {
+                const bf16x8 g = side == 0 ? I.af[s] : I.cf[s];
+                h0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + wbase + 32 * (4 + s)), g, h0, 0, 0, 0);
+                h1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W1 + 32 * 272 + wbase + 32 * (4 + s)), g, h1, 0, 0, 0);
             }
         };
         auto gemm2 = [&](int side, const f32x16 &h0, const f32x16 &h1) {
@@ -677,19 +430,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                 y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ld8(W2 + 32 * 144 + qb), bop, y1, 0, 0, 0);
             }
         };
-        if constexpr (PF == 4) {
-            f32x16 hv0, hv1, hc0, hc1;
-            gemm1(0, hv0, hv1);
-            gemm1(1, hc0, hc1);
-            gemm2(0, hv0, hv1);
-            gemm2(1, hc0, hc1);
-        } else {
 #pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                f32x16 h0, h1;
-                gemm1(side, h0, h1);
-                gemm2(side, h0, h1);
-            }
+        for (int side = 0; side < 2; ++side) {
+            f32x16 h0, h1;
+            gemm1(side, h0, h1);
+            gemm2(side, h0, h1);
         }
         if constexpr (!layer0) {  // residual (message_gnn_decoder.py:261): chunk s <-> y_{s>>1}[8 (s&1) ..]
 #pragma unroll
@@ -709,7 +454,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                 part = fmaf(y1[r], wo[32 + 16 * h + r], part);
             }
             part += __shfl_xor(part, 32, 64);
-            if (I.ok && h == 0) A.msg_out[I.b * A.E + I.mpos] = part + A.bo[0];
+            if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo[0];
         } else {
             if (A.kd_last) {  // early termination: project with the last layer's output head
                 const float *wo = tail + 128;
@@ -720,7 +465,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
                     part = fmaf(y1[r], wo[32 + 16 * h + r], part);
                 }
                 part += __shfl_xor(part, 32, 64);
-                if (I.ok && h == 0) A.msg_out[I.b * A.E + I.mpos] = part + A.bo_last[0];
+                if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo_last[0];
             }
             if (!I.ok) return;
             char *xo = reinterpret_cast<char *>(A.x_out + I.row * H) + 16 * h;
@@ -732,54 +477,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
     };
 
     if (tw.first >= tw.end) return;
-    if constexpr (PF == 2 && !proj && !layer0) {
-        // feature rows two tiles ahead, everything else one tile ahead, message info and frame
-        // flags as in PF 1
-        TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
-        int64_t nb = fb + sb, nk = fk + sk;
-        if (nk >= A.tpf) { nk -= A.tpf; ++nb; }
-        int4 inf_n = load_info(nk);
-        bool on_n = load_on(tw.first + tw.stride, nb);
-        XRows x_n = load_x(tw.first + tw.stride, nb, nk);
-        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-            int64_t nb2 = nb + sb, nk2 = nk + sk;
-            if (nk2 >= A.tpf) { nk2 -= A.tpf; ++nb2; }
-            const int4 inf_nn = load_info(nk2);
-            const bool on_nn = load_on(t + 2 * tw.stride, nb2);
-            const XRows x_nn = load_x(t + 2 * tw.stride, nb2, nk2);
-            const TileIn nxt = load(inf_n, on_n, t + tw.stride, nb, nk, &x_n);
-            compute(cur);
-            cur = nxt;
-            x_n = x_nn;
-            inf_n = inf_nn;
-            on_n = on_nn;
-            nb = nb2;
-            nk = nk2;
-        }
-    } else if constexpr (PF == 3 && !proj) {
-        // group rows (L2 gathers) two tiles ahead, message info three, feature rows one
-        TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
-        int64_t b1 = fb + sb, k1 = fk + sk;
-        if (k1 >= A.tpf) { k1 -= A.tpf; ++b1; }
-        int64_t b2 = b1 + sb, k2 = k1 + sk;
-        if (k2 >= A.tpf) { k2 -= A.tpf; ++b2; }
-        int4 inf1 = load_info(k1), inf2 = load_info(k2);
-        bool on1 = load_on(tw.first + tw.stride, b1), on2 = load_on(tw.first + 2 * tw.stride, b2);
-        GRows g1 = load_g(inf1, on1, tw.first + tw.stride, b1);
-        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-            int64_t b3 = b2 + sb, k3 = k2 + sk;
-            if (k3 >= A.tpf) { k3 -= A.tpf; ++b3; }
-            const int4 inf3 = load_info(k3);
-            const bool on3 = load_on(t + 3 * tw.stride, b3);
-            const GRows g2 = load_g(inf2, on2, t + 2 * tw.stride, b2);
-            const TileIn nxt = load(inf1, on1, t + tw.stride, b1, k1, nullptr, &g1);
-            compute(cur);
-            cur = nxt;
-            g1 = g2;
-            inf1 = inf2; on1 = on2; b1 = b2; k1 = k2;
-            inf2 = inf3; on2 = on3; b2 = b3; k2 = k3;
-        }
-    } else if constexpr (PF != 0) {
+    {
         // rows are prefetched one tile ahead; the small per-tile items (message info, frame
         // flag) two tiles ahead, so the row loads never wait behind an index load
         TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
@@ -800,19 +498,6 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
             nb = nb2;
             nk = nk2;
         }
-    } else {
-        // the next tile's message info is fetched one tile ahead, so each tile's row loads
-        // start at once instead of behind a dependent index load
-        int64_t b = fb, k = fk;
-        int4 inf = load_info(k);
-        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-            const TileIn cur = load(inf, load_on(t, b), t, b, k);
-            b += sb;
-            k += sk;
-            if (k >= A.tpf) { k -= A.tpf; ++b; }
-            inf = load_info(k < A.tpf ? k : 0);
-            compute(cur);
-        }
     }
 }
 
@@ -823,6 +508,10 @@ __global__ __launch_bounds__(NT, WPS) void gnn_bf16_mlp_kernel(MlpArgs A) {
 // written now, its layer count recorded, and every later kernel skips it.  A frame that goes on is
 // appended to out_list (one atomic per frame): the next layer's kernels walk that list, so no
 // separate compaction pass is needed (the list order varies run to run; no result depends on it).
+// ZS: the variable sums are kept in LDS for the probs of a finished frame ((N + 31) / 32 + N words;
+// syndrome_lds_bytes); without ZS (codes whose N does not fit) they are summed again, in the same
+// order, only for a finished frame.
+template <bool ZS>
 __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__restrict__ msg_out,
                                                                 const int32_t *__restrict__ csr, int64_t E,
                                                                 const float *__restrict__ llr, int N,
@@ -833,23 +522,26 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
                                                                 const int32_t *__restrict__ count,
                                                                 int32_t *__restrict__ iters, float *__restrict__ probs,
                                                                 int32_t *__restrict__ out_list,
-                                                                int32_t *__restrict__ out_count, int vm) {
-    extern __shared__ uint32_t bits[];  // [(N + 31) / 32] decision bits, then zs [N]
+                                                                int32_t *__restrict__ out_count) {
+    extern __shared__ uint32_t bits[];  // [(N + 31) / 32] decision bits, then (ZS) zs [N]
     float *zs = reinterpret_cast<float *>(bits + (N + 31) / 32);
+    const int32_t *vptr = csr_ptr(csr), *vmem = csr_mem(csr, N);
+    auto zsum = [&](const float *mo, const float *lr, int v) {
+        float sum = 0.0f;  // the output stage's own sum order (gnn_output)
+        for (int q = vptr[v]; q < vptr[v + 1]; ++q) sum += mo[vmem[q]];
+        return sum + lr[v];
+    };
     __shared__ int odd;
     if (count && (int)blockIdx.x >= *count) return;
     const int64_t b = list ? list[blockIdx.x] : blockIdx.x;
     if (!active[b]) return;
     const float *mo = msg_out + b * E, *lr = llr + b * N;
-    const int32_t *vptr = csr_ptr(csr), *vmem = csr_mem(csr, N);
     for (int i = threadIdx.x; i < (N + 31) / 32; i += blockDim.x) bits[i] = 0u;
     if (threadIdx.x == 0) odd = 0;
     __syncthreads();
     for (int v = threadIdx.x; v < N; v += blockDim.x) {
-        float sum = 0.0f;  // the output stage's own sum order (gnn_output): msg_out is variable-major
-        for (int q = vptr[v]; q < vptr[v + 1]; ++q) sum += mo[vm ? q : vmem[q]];
-        const float zv = sum + lr[v];
-        zs[v] = zv;
+        const float zv = zsum(mo, lr, v);
+        if constexpr (ZS) zs[v] = zv;
         if (zv > 0.0f) atomicOr(&bits[v >> 5], 1u << (v & 31));
     }
     __syncthreads();
@@ -870,26 +562,13 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
         active[b] = 0;
         if (iters) iters[b] = layer + 1;
     }
-    for (int v = threadIdx.x; v < N; v += blockDim.x) probs[b * N + v] = 1.0f / (1.0f + expf(-zs[v]));
+    for (int v = threadIdx.x; v < N; v += blockDim.x)
+        probs[b * N + v] = 1.0f / (1.0f + expf(-(ZS ? zs[v] : zsum(mo, lr, v))));
 }
 
-// vpos[mem[q]] = q: each message's slot in the variable-major msg_out rows (mem = the CSR of msg_var)
-__global__ void gnn_bf16_vpos_kernel(const int32_t *__restrict__ csr, int N, int64_t E, int32_t *__restrict__ vpos,
-                                     int vm) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < E) {
-        if (vm) vpos[csr_mem(csr, N)[q]] = (int32_t)q;
-        else vpos[q] = (int32_t)q;  // message order
-    }
-}
-
-// LDPC_GNN_MSGOUT_VM=1: msg_out rows variable-major (contiguous sums in the syndrome and output
-// passes, but a scattered 4-byte store per message in the MLP); default message order, measured
-// 2.3 % faster on cfg5 (profiles/r03ac).  Read per call.
-int msgout_vm() {
-    const char *e = std::getenv("LDPC_GNN_MSGOUT_VM");
-    return e && std::atoi(e) == 1;
-}
+// dynamic LDS of gnn_bf16_syndrome_kernel<ZS>
+inline size_t syndrome_lds_bytes(int N, bool zs) { return (size_t)((N + 31) / 32 + (zs ? N : 0)) * 4; }
+constexpr size_t kSyndromeLdsMax = 64 * 1024;  // the z cache only while several workgroups fit a CU
 
 // cg_var[q] = msg_var[cg_mem[q]]: the variable of every check-group member (syndrome tables)
 __global__ void gnn_bf16_cgvar_kernel(const int32_t *__restrict__ cg_mem, const int32_t *__restrict__ msg_var,
@@ -905,7 +584,7 @@ __global__ void fill_i32_kernel(int32_t *p, int64_t n, int32_t v) {
 
 struct Bf16Ws {
     float *kd, *memb, *msg_out;
-    int32_t *csr, *alist, *acount, *cg_var, *vpos;
+    int32_t *csr, *alist, *acount, *cg_var;
     int4 *info;
     uint8_t *active;
     __bf16 *xa, *xb, *Mv, *Mc;
@@ -917,7 +596,7 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4);
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
     const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * p->E * 4);
-    const int64_t inf = al(std::max<int64_t>(p->E, (int64_t)p->n_mtiles * 32) * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
+    const int64_t inf = al(p->E * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
     const int64_t alb = al(2 * B * 4) + 256;  // two active lists [B] + the two ranges' two counts
     char *c = static_cast<char *>(base);
     Bf16Ws w;
@@ -934,56 +613,32 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     w.alist = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs);
     w.acount = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + al(2 * B * 4));
     w.cg_var = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb);
-    w.vpos = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb + al(p->E * 4));
-    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb + 2 * al(p->E * 4);
+    w.bytes = kd + memb + xa + xb + mv + mc + vs + inf + act + cs + alb + al(p->E * 4);
     return w;
 }
 
 int g_cus = 0;
 
-template <int NT, int WPS, int PF, int MODE>
+template <int MODE>
 int launch_mlp_t(int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
-    const void *fn = reinterpret_cast<const void *>(gnn_bf16_mlp_kernel<NT, WPS, PF, MODE>);
+    const void *fn = reinterpret_cast<const void *>(gnn_bf16_mlp_kernel<MODE>);
     LDPC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const int per_cu = 4 * WPS / (NT / 64);  // workgroups per CU at WPS waves per SIMD
-    const unsigned grid = (unsigned)std::min<int64_t>((tiles + NT / 64 - 1) / (NT / 64), (int64_t)g_cus * per_cu);
-    hipLaunchKernelGGL((gnn_bf16_mlp_kernel<NT, WPS, PF, MODE>), dim3(grid), dim3(NT), lds, s, m);
+    const int per_cu = 4 * 2 / (kMlpThreads / 64);  // workgroups per CU at 2 waves per SIMD
+    const unsigned grid = (unsigned)std::min<int64_t>((tiles + kMlpThreads / 64 - 1) / (kMlpThreads / 64),
+                                                      (int64_t)g_cus * per_cu);
+    hipLaunchKernelGGL((gnn_bf16_mlp_kernel<MODE>), dim3(grid), dim3(kMlpThreads), lds, s, m);
     return LDPC_OK;
 }
 
-template <int NT, int WPS, int PF>
-int launch_mlp_v(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
+// the MLP kernel per layer mode (bit 0 layer 0, bit 1 last layer): 256 threads, 2 waves per SIMD,
+// next tile prefetched into registers (measured against 3-4 waves per SIMD, one 512-thread
+// workgroup per CU and deeper prefetch: all within 2 % or slower)
+int launch_mlp(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (mode) {
-        case 0: return launch_mlp_t<NT, WPS, PF, 0>(tiles, lds, s, m);
-        case 1: return launch_mlp_t<NT, WPS, PF, 1>(tiles, lds, s, m);
-        case 2: return launch_mlp_t<NT, WPS, PF, 2>(tiles, lds, s, m);
-        case 3: return launch_mlp_t<NT, WPS, PF, 3>(tiles, lds, s, m);
-        case 4: return launch_mlp_t<NT, WPS, PF, 4>(tiles, lds, s, m);
-        case 5: return launch_mlp_t<NT, WPS, PF, 5>(tiles, lds, s, m);
-        case 6: return launch_mlp_t<NT, WPS, PF, 6>(tiles, lds, s, m);
-        default: return launch_mlp_t<NT, WPS, PF, 7>(tiles, lds, s, m);
-    }
-}
-
-// LDPC_GNN_BF16_MLP selects the MLP kernel's occupancy / pipelining (speed only):
-//   1 = 256 threads, 2 waves/SIMD, next tile prefetched into registers (default)
-//   0 = 768 threads, 3 waves/SIMD, no register prefetch
-//   2 = 512 threads, 4 waves/SIMD, no prefetch (spills at 128 VGPRs)
-//   3 = 512 threads, 2 waves/SIMD, prefetch: one workgroup (one LDS weight copy) per CU
-//   4 = 768 threads, 3 waves/SIMD, prefetch; 5 = 1024 threads, 4 waves/SIMD, no prefetch
-//   6 = as 1, feature rows two tiles ahead (PF 2); 7 = as 1, group rows two tiles ahead (PF 3)
-//   8 = as 1, both sides' GEMM1 before either GEMM2 (PF 4)
-int launch_mlp(int variant, int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
-    switch (variant) {
-        case 0: return launch_mlp_v<768, 3, 0>(mode, tiles, lds, s, m);
-        case 2: return launch_mlp_v<512, 4, 0>(mode, tiles, lds, s, m);
-        case 3: return launch_mlp_v<512, 2, 1>(mode, tiles, lds, s, m);
-        case 4: return launch_mlp_v<768, 3, 1>(mode, tiles, lds, s, m);
-        case 5: return launch_mlp_v<1024, 4, 0>(mode, tiles, lds, s, m);
-        case 6: return launch_mlp_v<256, 2, 2>(mode, tiles, lds, s, m);
-        case 7: return launch_mlp_v<256, 2, 3>(mode, tiles, lds, s, m);
-        case 8: return launch_mlp_v<256, 2, 4>(mode, tiles, lds, s, m);
-        default: return launch_mlp_v<256, 2, 1>(mode, tiles, lds, s, m);
+        case 0: return launch_mlp_t<0>(tiles, lds, s, m);
+        case 1: return launch_mlp_t<1>(tiles, lds, s, m);
+        case 2: return launch_mlp_t<2>(tiles, lds, s, m);
+        default: return launch_mlp_t<3>(tiles, lds, s, m);
     }
 }
 
@@ -1004,13 +659,6 @@ int compact_env() {
     return e ? std::atoi(e) : 1;
 }
 
-// LDPC_GNN_BF16_PROJ=1: projected group rows (one third fewer MFMAs, measured 16 % slower: this
-// path is bound by memory, not MFMA); default: group-mean rows, GEMM1 over [x; g]
-int proj_env() {
-    const char *e = std::getenv("LDPC_GNN_BF16_PROJ");  // read per call (tests toggle it)
-    return e ? std::atoi(e) : 0;
-}
-
 // LDPC_GNN_GM_CAP=n: after the first syndrome pass the group-mean kernel runs at most n workgroups
 // per CU, striding over the frames still decoding, instead of one wave per (frame, tile) of the
 // whole range (whose early-exiting waves cost ~0.1 ms per layer once few frames are left).  Default
@@ -1018,11 +666,6 @@ int proj_env() {
 int gm_cap() {
     const char *e = std::getenv("LDPC_GNN_GM_CAP");
     return e ? std::atoi(e) : 256;
-}
-
-int mlp_variant() {
-    const char *e = std::getenv("LDPC_GNN_BF16_MLP");  // read per call (tests compare variants)
-    return e ? std::atoi(e) : 1;
 }
 
 }  // namespace
@@ -1039,21 +682,12 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     Bf16Ws w = carve_bf16(p, N, B, T, L, d_work);
     if (!d_work || work_bytes < w.bytes)
         return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
-    // projected group rows (see gnn_bf16_proj_kernel): needs the plan's projection tiles and a
-    // variable index that fits the packed per-slot info (type | variable << 8)
-    const bool proj = proj_env() && p->n_ptiles > 0 && p->n_mtiles > 0 && N < (1 << 23);
-    const int64_t tpf = proj ? p->n_mtiles : (p->E + 31) / 32;
-    if (B * tpf >= (1LL << 31) || B * p->n_gtiles >= (1LL << 31) || B * p->n_ptiles >= (1LL << 31) ||
-        p->E >= (1LL << 31))
+    const int64_t tpf = (p->E + 31) / 32;
+    if (B * tpf >= (1LL << 31) || B * p->n_gtiles >= (1LL << 31) || p->E >= (1LL << 31))
         return fail(LDPC_EUNSUPPORTED, "batch too large for one launch (chunk it)");
     // degree-1 skip when its D1 table still lets two 256-thread workgroups share a CU's LDS
-    // (LDPC_GNN_BF16_D1=0 disables it, for A/B runs)
-    static const int d1_env = [] {
-        const char *e = std::getenv("LDPC_GNN_BF16_D1");
-        return e ? std::atoi(e) : 1;
-    }();
-    const bool d1 = d1_env && p->n_gtiles_v1 > 0 && 2 * mlp_lds_bytes(T, true, proj) <= 160 * 1024;
-    const size_t lds = mlp_lds_bytes(T, d1, proj);
+    const bool d1 = p->n_gtiles_v1 > 0 && 2 * mlp_lds_bytes(T, true) <= 160 * 1024;
+    const size_t lds = mlp_lds_bytes(T, d1);
     if (T > kBf16MaxTypes || lds > 160 * 1024)
         return fail(LDPC_EUNSUPPORTED, "too many message types for the bf16 LDS image");
     if (!g_cus) {
@@ -1063,12 +697,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     }
     const GtArgs G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles, 0};
     const int Gtot = p->Gv + p->Gc;
-    if (proj) {
-        const int n = p->n_mtiles * 32;
-        hipLaunchKernelGGL(gnn_bf16_info_perm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, p->mt_perm,
-                           p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, d_msg_type, d_msg_var, w.info);
-        LDPC_CHECK_LAUNCH("gnn_bf16_info_perm_kernel");
-    } else {
+    {
         hipLaunchKernelGGL(gnn_bf16_info_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, (int)p->E,
                            p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, d_msg_type, d_msg_var, w.info);
         LDPC_CHECK_LAUNCH("gnn_bf16_info_kernel");
@@ -1079,10 +708,6 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
                        d_weights, T, L, d_msg_type, G, Gtot, w.memb);
     LDPC_CHECK_LAUNCH("gnn_bf16_memb_kernel");
     if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
-    const int vm = msgout_vm();
-    hipLaunchKernelGGL(gnn_bf16_vpos_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, w.csr, N, p->E,
-                       w.vpos, vm);
-    LDPC_CHECK_LAUNCH("gnn_bf16_vpos_kernel");
     if (d_iters) {
         hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, d_iters, B, L);
         LDPC_CHECK_LAUNCH("fill_i32_kernel");
@@ -1129,37 +754,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.active = act;
         gm.list = listed ? alist : nullptr;
         gm.count = listed ? acount : nullptr;
-        if (proj) {
-            PjArgs pj{};
-            pj.x_in = x_in;
-            pj.llr = gm.llr;
-            pj.msg_var = d_msg_var;
-            pj.w_in = gm.w_in;
-            pj.b_in = gm.b_in;
-            pj.memb = gm.memb;
-            pj.w1v = lw.w1v;
-            pj.w1c = lw.w1c;
-            pj.meta = p->pt_meta;
-            pj.grp = p->pt_grp;
-            pj.deg = p->pt_deg;
-            pj.mem = p->pt_mem;
-            pj.n_tiles = p->n_ptiles;
-            pj.first = d1 && l > 0 ? p->n_ptiles_v1 : 0;
-            pj.Pv = gm.Mv;
-            pj.Pc = gm.Mc;
-            pj.active = gm.active;
-            pj.list = gm.list;
-            pj.count = gm.count;
-            pj.Gv = p->Gv;
-            pj.Gc = p->Gc;
-            pj.E = (int)p->E;
-            pj.N = N;
-            pj.B = nb;
-            const int64_t pw = nb * (pj.n_tiles - pj.first);  // waves of work
-            const unsigned pgrid = (unsigned)std::min<int64_t>((pw + 3) / 4, (int64_t)g_cus * 8);
-            hipLaunchKernelGGL(gnn_bf16_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds_bytes_bf16(4), st, pj);
-            LDPC_CHECK_LAUNCH("gnn_bf16_proj_kernel");
-        } else {
+        {
             const int64_t gwaves = nb * (gm.G.n_tiles - gm.G.first);
             int64_t gblocks = (gwaves + 3) / 4;
             if (gm.count && gm_cap() > 0) gblocks = std::min<int64_t>(gblocks, (int64_t)g_cus * gm_cap());
@@ -1186,28 +781,32 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.E = (int)p->E;
         m.N = N;
         m.tpf = (int)tpf;
-        m.tpf1 = p->n_mtiles_v1;
         m.d1 = d1 ? 1 : 0;
         m.B = nb;
         m.msg_out = w.msg_out + b0 * p->E;
-        m.vpos = w.vpos;
         m.active = act;
         m.list = listed ? alist : nullptr;
         m.count = listed ? acount : nullptr;
         m.kd_last = et && l < L - 1 ? kd_last : nullptr;
         m.bo_last = bo_last;
-        const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0) | (proj ? 4 : 0);
-        const int rc = launch_mlp(mlp_variant(), mode, nb * tpf, lds, st, m);
+        const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0);
+        const int rc = launch_mlp(mode, nb * tpf, lds, st, m);
         if (rc != LDPC_OK) return rc;
         LDPC_CHECK_LAUNCH("gnn_bf16_mlp_kernel");
         if (m.kd_last) {
             const bool cmp = compact_env();
             int32_t *olist = lists[cur ^ 1], *ocount = counts[cur ^ 1];
             if (cmp) LDPC_HIP(hipMemsetAsync(ocount, 0, 4, st));
-            hipLaunchKernelGGL(gnn_bf16_syndrome_kernel, dim3((unsigned)nb), dim3(256),
-                               (size_t)((N + 31) / 32 + N) * 4, st, w.msg_out + b0 * p->E, w.csr, p->E,
+            const bool zs = syndrome_lds_bytes(N, true) <= kSyndromeLdsMax;
+            const size_t slds = syndrome_lds_bytes(N, zs);
+            if (slds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "early termination: N too large for the syndrome pass");
+            auto synd = zs ? gnn_bf16_syndrome_kernel<true> : gnn_bf16_syndrome_kernel<false>;
+            if (slds > kSyndromeLdsMax)
+                LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(synd),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)slds));
+            hipLaunchKernelGGL(synd, dim3((unsigned)nb), dim3(256), slds, st, w.msg_out + b0 * p->E, w.csr, p->E,
                                d_llr + b0 * N, N, p->cg_ptr, w.cg_var, p->Gc, l, act, listed ? alist : nullptr, listed ? acount : nullptr,
-                               d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N, cmp ? olist : nullptr, ocount, vm);
+                               d_iters ? d_iters + b0 : nullptr, d_probs + b0 * N, cmp ? olist : nullptr, ocount);
             LDPC_CHECK_LAUNCH("gnn_bf16_syndrome_kernel");
             if (cmp) {
                 cur ^= 1;
@@ -1234,7 +833,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     } else if (int rc = run_range(0, B, s, 0)) {
         return rc;
     }
-    return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s, vm != 0);
+    return gnn_output(w.msg_out, w.csr, d_llr, p->E, N, B, active, d_probs, s);
 }
 
 }  // namespace ldpc

@@ -576,161 +576,6 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
     }
 }
 
-// ---- the PJ kernel above with GEMM1 and GEMM3' as bf16x6 splits on v_mfma_f32_32x32x16_bf16 (fp32
-// products up to summation order; gnn.hpp split3 / mfma6, gnn.hip gnn_mlp2s_kernel); GEMM2' stays
-// on the fp32 MFMA (three more split images would not fit the LDS).  K orders: GEMM1's k-step s,
-// lane half h, element i is c unit pi16(16 s + 8 h + i), so the lane's c values are the units it
-// owns in the accumulator layout; GEMM3' runs over the hidden units in the same order, so its B
-// operand is the masked GEMM2' accumulator as it stands.  LDS: W1_left in two orientations (rows
-// u for GEMM1, rows k for GEMM3'), three split images each per side, then W2v, W2c fp32 [64][65].
-constexpr int kB6Row = 72, kB6Img = 64 * kB6Row;
-inline size_t bwd_split_lds() { return (size_t)12 * kB6Img * 2 + (size_t)2 * 64 * kS2 * 4; }
-
-template <int NT>
-__global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd_split_kernel(MlpT A) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    constexpr int H = 64;
-    __bf16 *img = reinterpret_cast<__bf16 *>(sm);  // [W1vL, W1cL, W1vL^T, W1cL^T] x 3 splits
-    float *W2v = sm + 6 * kB6Img, *W2c = W2v + H * kS2;
-    for (int i = threadIdx.x; i < H * H; i += NT) {
-        const int o = i >> 6, p = i & 63, u = pi16(p);
-        split_store(A.w1v[o * 128 + u], img + 0 * kB6Img + o * kB6Row + p, 4 * kB6Img);
-        split_store(A.w1c[o * 128 + u], img + 1 * kB6Img + o * kB6Row + p, 4 * kB6Img);
-        split_store(A.w1v[u * 128 + o], img + 2 * kB6Img + o * kB6Row + p, 4 * kB6Img);
-        split_store(A.w1c[u * 128 + o], img + 3 * kB6Img + o * kB6Row + p, 4 * kB6Img);
-        W2v[o * kS2 + p] = A.w2v[i];
-        W2c[o * kS2 + p] = A.w2c[i];
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, j = lane & 31, half = lane >> 5, wave = threadIdx.x >> 6;
-    const int abase = j * kB6Row + 8 * half;
-    const int64_t ntiles = (A.R + 31) / 32;
-    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
-    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-        const int64_t row = t * 32 + j;
-        const bool ok = row < A.R;
-        const int64_t rr = ok ? row : A.R - 1;
-        const int64_t b = rr / A.E, m = rr - b * A.E;
-        // c = x (or w_in llr + b_in) + emb[type] at units pi16(16 s + 8 h + i): float4 pairs
-        float c[4][8];
-        {
-            const float *e = A.emb + A.msg_type[m] * H + 4 * half;
-            const float l = A.x ? 0.0f : A.llr[b * A.N + A.msg_var[m]];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int u0 = 32 * (s >> 1) + 16 * (s & 1) + 8 * q;  // + 4 half
-                    float4 v;
-                    if (A.x) {
-                        v = *reinterpret_cast<const float4 *>(A.x + rr * H + u0 + 4 * half);
-                    } else {
-                        const float4 w = *reinterpret_cast<const float4 *>(A.w_in + u0 + 4 * half);
-                        const float4 bi = *reinterpret_cast<const float4 *>(A.b_in + u0 + 4 * half);
-                        v = make_float4(w.x * l + bi.x, w.y * l + bi.y, w.z * l + bi.z, w.w * l + bi.w);
-                    }
-                    const float4 ev = *reinterpret_cast<const float4 *>(e + u0);
-                    c[s][4 * q] = v.x + ev.x; c[s][4 * q + 1] = v.y + ev.y;
-                    c[s][4 * q + 2] = v.z + ev.z; c[s][4 * q + 3] = v.w + ev.w;
-                    if (ok)
-                        *reinterpret_cast<float4 *>(A.cbuf + row * H + u0 + 4 * half) =
-                            make_float4(c[s][4 * q], c[s][4 * q + 1], c[s][4 * q + 2], c[s][4 * q + 3]);
-                }
-        }
-        f32x16 dco0 = {}, dco1 = {};
-        const int l2 = (32 * half) * kS2 + j;
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            const float *W2 = side == 0 ? W2v : W2c;
-            // GEMM2' (fp32 MFMA): d[u][msg] = sum_o W2[o][u] dX[o]
-            f32x16 d0 = {}, d1 = {};
-            {
-                float dx[32];
-                const float4 *dp = reinterpret_cast<const float4 *>(A.dX + rr * H + 32 * half);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const float4 v = dp[q];
-                    dx[4 * q] = v.x; dx[4 * q + 1] = v.y; dx[4 * q + 2] = v.z; dx[4 * q + 3] = v.w;
-                }
-#pragma unroll
-                for (int kk = 0; kk < 32; ++kk) {
-                    const float *wr = W2 + l2 + kk * kS2;
-                    d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[0], dx[kk], d0, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[32], dx[kk], d1, 0, 0, 0);
-                }
-            }
-            // GEMM1 from the projected row (b1 included): u = W1_left c + (W1_right g + b1)
-            f32x16 u0, u1;
-            {
-                const float *pr = side == 0 ? A.Mv + (b * A.Gv + A.vgroup[m]) * H : A.Mc + (b * A.Gc + A.cgroup[m]) * H;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 p0 = *reinterpret_cast<const float4 *>(pr + 8 * q + 4 * half);
-                    const float4 p1 = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q + 4 * half);
-                    u0[4 * q] = p0.x; u0[4 * q + 1] = p0.y; u0[4 * q + 2] = p0.z; u0[4 * q + 3] = p0.w;
-                    u1[4 * q] = p1.x; u1[4 * q + 1] = p1.y; u1[4 * q + 2] = p1.z; u1[4 * q + 3] = p1.w;
-                }
-                const __bf16 *W1 = img + side * kB6Img + abase;
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    bf16x8_t c0, c1, c2;
-                    split3(c[s], c0, c1, c2);
-                    u0 = mfma6(W1 + 16 * s, c0, c1, c2, u0, 4 * kB6Img);
-                    u1 = mfma6(W1 + 32 * kB6Row + 16 * s, c0, c1, c2, u1, 4 * kB6Img);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            // relu, mask: lane holds units 32 rt + crow(r, half)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float a0 = u0[r], a1 = u1[r];
-                u0[r] = fmaxf(a0, 0.0f);
-                u1[r] = fmaxf(a1, 0.0f);
-                d0[r] = a0 > 0.0f ? d0[r] : 0.0f;
-                d1[r] = a1 > 0.0f ? d1[r] : 0.0f;
-            }
-            if (ok) {
-                float *ho = (side == 0 ? A.hv : A.hc) + row * H, *dho = (side == 0 ? A.dhv : A.dhc) + row * H;
-#pragma unroll
-                for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const f32x16 &uu = rt ? u1 : u0, &dd = rt ? d1 : d0;
-                        const int o0 = 32 * rt + 8 * q + 4 * half;
-                        *reinterpret_cast<float4 *>(ho + o0) =
-                            make_float4(uu[4 * q], uu[4 * q + 1], uu[4 * q + 2], uu[4 * q + 3]);
-                        *reinterpret_cast<float4 *>(dho + o0) =
-                            make_float4(dd[4 * q], dd[4 * q + 1], dd[4 * q + 2], dd[4 * q + 3]);
-                    }
-            }
-            // GEMM3' (c part): dz[k][msg] = sum_u W1[u][k] dh[u]; k-step s = registers 8 (s&1) .. of d_{s>>1}
-            const __bf16 *W1T = img + (2 + side) * kB6Img + abase;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                float hr[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) hr[i] = s < 2 ? d0[8 * (s & 1) + i] : d1[8 * (s & 1) + i];
-                bf16x8_t h0, h1, h2;
-                split3(hr, h0, h1, h2);
-                dco0 = mfma6(W1T + 16 * s, h0, h1, h2, dco0, 4 * kB6Img);
-                dco1 = mfma6(W1T + 32 * kB6Row + 16 * s, h0, h1, h2, dco1, 4 * kB6Img);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if (ok) {
-            float *co = A.dco + row * H;
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const f32x16 &cc = rt ? dco1 : dco0;
-                    *reinterpret_cast<float4 *>(co + 32 * rt + 8 * q + 4 * half) =
-                        make_float4(cc[4 * q], cc[4 * q + 1], cc[4 * q + 2], cc[4 * q + 3]);
-                }
-        }
-    }
-}
-
 // PJ backward: the group part of dz averaged over a group, formed per group --
 // Mda[b][g][k] = inv[g] sum_u W1v[u][64 + k] S_v[b][g][u] with S the group sums of dh (Mdb: the
 // check side with W1c).  One wave per 4 rows of a side, lanes = k, W1_right in LDS.
@@ -1252,15 +1097,6 @@ int bwd_proj() {
     return e ? std::atoi(e) : 1;
 }
 
-// LDPC_GNN_TRAIN_SPLIT=1: GEMM1 and GEMM3' of the backward MLP as bf16x6 splits
-// (train_mlp_bwd_split_kernel), like the forward's MLP (gnn.hip); default 0: the fp32-MFMA kernel.
-// Measured 1.27 vs 1.24 ms per layer at B = 256 (profiles/r03n): the kernel is bound by its six
-// (B, E, H) outputs, not by the matrix pipe.  Read per call.
-int bwd_split() {
-    const char *e = std::getenv("LDPC_GNN_TRAIN_SPLIT");
-    return e && std::atoi(e) == 1;
-}
-
 // LDPC_GNN_TRAIN_OVERLAP=1: the backward's forward recompute (group projections of layer l - 1)
 // runs on a side stream into a second buffer set while layer l's gradients run on the caller's
 // stream; 0: one set, in line.  42.3-42.5 vs 42.7-43.0 ms per B = 256 step (profiles/r03aj, three
@@ -1345,9 +1181,6 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     // projected groups (see train_mlp_bwd_mfma_kernel): H = 64 on MFMA with the plan's projection tiles
     const bool pj = H == 64 && bwd_mfma() && bwd_proj() && p->n_ptiles > 0;
-    if (pj && bwd_split())
-        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_split_kernel<512>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_split_lds()));
     if (pj) {
         LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<512, true>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
@@ -1391,13 +1224,16 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         LDPC_HIP(hipEventRecord(ev_ready[j & 1], s2));
         return LDPC_OK;
     };
+    hipEvent_t fork = nullptr, join = nullptr;
     if (ovl) {
-        hipEvent_t fork, join;
         if (int rc = gnn_side_stream(&s2, &fork, &join)) return rc;
         if (int rc = train_events(ev_ready, ev_free)) return rc;
         LDPC_HIP(hipEventRecord(fork, s));  // the workspace and inputs are the caller stream's
         LDPC_HIP(hipStreamWaitEvent(s2, fork, 0));
     }
+    // the layers, then (side stream) a join on every exit, error returns included: nothing queued
+    // on s2 may still write the caller's workspace once the caller's stream moves on
+    auto layers_back = [&]() -> int {
     for (int l = L - 1; l >= 0; --l) {
         const float *W[11];
         t_layer(d_weights, H, T, l, W);
@@ -1457,9 +1293,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         if (H == 64 && bwd_mfma()) {  // LDPC_GNN_TRAIN_MFMA=0 selects the VALU kernel (A/B runs)
             const int nt = bwd_mfma() == 2 ? 256 : 512;  // =2: 256 threads, 1 wave per SIMD
             const unsigned grid = (unsigned)std::min<int64_t>((R + 32 * (nt / 64) - 1) / (32 * (nt / 64)), (int64_t)g_cus_t);
-            if (pj && bwd_split() && nt == 512)
-                hipLaunchKernelGGL(train_mlp_bwd_split_kernel<512>, dim3(grid), dim3(512), bwd_split_lds(), s, m);
-            else if (pj && nt == 256)
+            if (pj && nt == 256)
                 hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<256, true>), dim3(grid), dim3(256), mlp_bwd_mfma_lds(), s, m);
             else if (pj)
                 hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<512, true>), dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);
@@ -1558,6 +1392,13 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         std::swap(w.dX, w.dXp);
     }
     return LDPC_OK;
+    };
+    const int rc = layers_back();
+    if (ovl) {
+        LDPC_HIP(hipEventRecord(join, s2));
+        LDPC_HIP(hipStreamWaitEvent(s, join, 0));
+    }
+    return rc;
 }
 
 extern "C" int ldpc_gnn_backward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,

@@ -102,13 +102,14 @@ class CustomCheckMessageGNNLayer(MessageGNNLayer):
 
 def _index_rows(index_tensor, n_nodes, n_msgs, device):
     """An index tensor (R, W) as int64 on `device`, validated as the reference's indexing would
-    be: ids in [-1, n_msgs) (-1 = padding), the node column in [0, n_nodes) when it is used."""
+    be: ids below n_msgs, every negative id is padding (the reference filters with ids >= 0,
+    MGD:644, :1004), the node column in [0, n_nodes) when it is used."""
     t = torch.as_tensor(index_tensor)
     if t.dim() != 2 or t.shape[1] < 1:
         raise ValueError(f"index tensor must be (rows, 1 + max degree), got {tuple(t.shape)}")
     t = t.long()
     ids = t[:, 1:]
-    if ids.numel() and (int(ids.max()) >= n_msgs or int(ids.min()) < -1):
+    if ids.numel() and int(ids.max()) >= n_msgs:
         raise IndexError(f"message id out of range for {n_msgs} messages")
     if n_nodes is not None and t.shape[0] and (int(t[:, 0].max()) >= n_nodes or int(t[:, 0].min()) < 0):
         raise IndexError(f"node index out of range for {n_nodes} nodes")
@@ -140,6 +141,8 @@ def _graph_from_index_tensors(check_index_tensor, variable_index_tensor, num_che
 class CustomMinSumMessageGNNDecoder(MessageGNNDecoder):
     """MGD:1137-1251.  forward(input_llrs, variable_adjacency, check_adjacency, message_types,
     variable_to_message_mapping, ground_truth=None) -> probs, or (probs, loss) with ground truth.
+    The decode reads none of the module's parameters (the learnable alpha of MGD:974 included), so
+    probs never require grad -- exactly the reference's autograd graph for these updates.
     The adjacency / type / mapping arguments are accepted for signature compatibility; the graph
     comes from the index tensors (set_variable_index_tensor / set_check_index_tensor), as in the
     reference's update loops."""
@@ -280,9 +283,15 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
 
     and the output (:855-877): out_m = output_projection_L(x_m), probs_v = sigmoid(mean over v's
     messages of out_m + llr_v).  forward(...) returns (probs, None), or (probs, max over bits of
-    the per-bit BCE) with ground truth, as the reference does.  Inference only (no backward);
-    hidden_dim 64; clique / identity check adjacencies.  Kernels: ldpc_gnn_custom_var_forward
-    (csrc/gnn.hip).  Oracle: oracle/oracle.py custom_variable_forward."""
+    the per-bit BCE) with ground truth, as the reference does.  hidden_dim 64; clique / identity
+    check adjacencies.  Kernels: ldpc_gnn_custom_var_forward (csrc/gnn.hip).  Oracle:
+    oracle/oracle.py custom_variable_forward.
+
+    Training: this build has no backward for the hybrid GNN.  With grad enabled and trainable
+    parameters the probs carry a grad_fn whose backward raises NotImplementedError (naming this
+    decoder), instead of torch's generic "does not require grad".  The layers' w_ch / w_res
+    (MGD:605-606) are never read by any forward in the reference (nor here): their gradient is None
+    by construction, whatever the backward."""
 
     def __init__(self, num_messages, num_iterations=5, hidden_dim=64, num_message_types=1, depth_L=3):
         if hidden_dim != 64:  # refused up front rather than at the first forward
@@ -341,6 +350,8 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
                     N.check(lib.ldpc_gnn_custom_var_forward(
                         plan.handle, 64, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr[s:s + n]), Nv, n,
                         N.ptr(probs[s:s + n]), N.ptr(ws), wsb, N.stream_ptr(dev)))
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            probs = _NoHybridBackward.apply(probs, *[p for p in self.parameters() if p.requires_grad])
         if home != dev:
             probs = probs.to(home)
         if ground_truth is not None:
@@ -354,6 +365,21 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
             probs, _ = self.forward(input_llr, message_to_var_mapping, message_types, var_to_check_adjacency,
                                     check_to_var_adjacency)
         return (probs > 0.5).float()
+
+
+class _NoHybridBackward(torch.autograd.Function):
+    """Identity on probs that refuses the backward with a clear error (see the decoder's docstring)."""
+
+    @staticmethod
+    def forward(ctx, probs, *params):
+        return probs.view_as(probs)
+
+    @staticmethod
+    def backward(ctx, grad):
+        raise NotImplementedError(
+            "CustomVariableMessageGNNDecoder is inference-only in this build: there is no HIP backward for "
+            "the hybrid GNN (its w_ch / w_res are never read by the forward, MGD:605-606, so they would get "
+            "no gradient in any case); decode() / torch.no_grad() for inference")
 
 
 def create_custom_variable_message_gnn_decoder(H, num_iterations=5, hidden_dim=64, depth_L=3, base_graph=None, Z=None):

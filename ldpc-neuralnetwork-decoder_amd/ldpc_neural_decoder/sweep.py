@@ -58,9 +58,10 @@ def rates(counts, n):
 def _dist_all_reduce():
     """(all_reduce fn, rank, world) of the initialised process group.  RCCL ("nccl") reduces the
     device tensor in place over xGMI; gloo (CPU tests, multi-rank rehearsals sharing one card)
-    reduces a host copy."""
+    reduces a host copy.  Any initialised group reduces, a world of one included (BENCH_DIST=1 runs
+    the RCCL branch on one GPU)."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         if dist.get_backend() == "gloo":
             def ar(t):
                 h = t.cpu()

@@ -109,9 +109,9 @@ def gen(name, base, z):
     # reads / writes issued
     rcost = [4.1 * n_min_ops(dc[r]) + 2.2 * (dc[r] // 2) + 10.4 * nslot[r] + 12 + 2.0 * dc[r] for r in rows]
     vcols = [c for c in range(nb) if dv[c] != 1]
-    vcost = [1.94 * (dv[c] * (dv[c] - 1) // 2 + dv[c]) + 2.0 * dv[c] + 6 for c in vcols]
     chk = balance(rows, rcost, W)
-    var = balance(vcols, vcost, W)
+    vt_pair = var_schedule(vcols, dv, W, pairs=True)
+    vt_single = var_schedule(vcols, dv, W, pairs=False)
     bw = lpt(list(range(nb)), [1.0] * nb, W)
     col_blocks = [[i for i, b in enumerate(blocks) if b[1] == c] for c in range(nb)]
     col_ptr = [0]
@@ -131,7 +131,6 @@ def gen(name, base, z):
         return ptr, out
 
     cp, cl = flat(chk)
-    vp, vl = flat(var)
     bp, bl = flat(bw)
     s = f"struct {name} {{\n"
     s += f"    static constexpr int Z = {z}, Mb = {mb}, Nb = {nb}, N = {nb * z}, NSLOTS = {n}, W = {W};\n"
@@ -148,20 +147,22 @@ def gen(name, base, z):
     s += arr("COL_SHIFT", col_shift)
     s += arr("CHK_PTR", cp)
     s += arr("CHK_ROWS", cl)
-    s += arr("VAR_PTR", vp)
-    s += arr("VAR_COLS", vl)
+    for pre, sched in (("VT", vt_pair), ("VS", vt_single)):
+        # per wave: the distinct columns of its tasks (LLRs, init, shifts), then the tasks
+        # (column A, column B or -1, outputs [lo, hi)); VT pairs columns on v_pk_add_f32, VS does not
+        vp, vl = flat([sorted({t[0] for t in p} | {t[1] for t in p if t[1] >= 0}) for p in sched])
+        tp, tl = flat(sched)
+        s += arr(f"{pre}_COL_PTR", vp)
+        s += arr(f"{pre}_COLS", vl)
+        s += arr(f"{pre}_PTR", tp)
+        s += arr(f"{pre}_A", [t[0] for t in tl])
+        s += arr(f"{pre}_B", [t[1] for t in tl])
+        s += arr(f"{pre}_LO", [t[2] for t in tl])
+        s += arr(f"{pre}_HI", [t[3] for t in tl])
     s += arr("BW_PTR", bp)
     s += arr("BW_COLS", bl)
-    s += task_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z)
-    # one frame per lane, 6 waves (flood_w6.inc): the fixed kernel's slot numbering
-    s += task_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z, W=6, prefix="S", frames=1, add=1.94,
-                       remap=False)
     s += "};\n\n"
     return s
-
-
-# ---- frame-pair kernel (flood.hip flood_pair_kernel): 8 waves, each lane carries two frames
-PW = 8
 
 
 def n_min_ops(d):
@@ -173,121 +174,77 @@ def n_min_ops(d):
     return 2 + 5 * ((d - 3) // 3) + 2 * ((d - 3) % 3)
 
 
-def var_task_adds(d, lo, hi):
-    """v_pk_add_f32 of a column task writing outputs [lo, hi): the prefix P_1..P_{hi-1} (P_d, the
-    APP, when hi == d) and the tails sum_{e in [lo, hi)} (d - 1 - e)"""
-    pre = d if hi == d else hi - 1
-    return pre + sum(d - 1 - e for e in range(lo, hi))
+def var_task_ops(DA, DB, lo, hi):
+    """Instruction counts of a variable task (flood_dev.hpp FixedBody::task): outputs [lo, hi) of
+    column A (degree DA) and, when DB > 0, of column B (degree DB <= DA) on v_pk_add_f32 pairs.
+    Per output e: acc[e] = P_e, then + c_J for J = e + 1 .. D - 1 (the reference's ascending
+    exclusive sum, traditional_decoders.py:235-250); prefix adds P_J -> P_{J+1} as far as an output
+    or an APP (the column's last prefix) needs them.  Returns (pk adds, scalar adds, LDS reads,
+    LDS writes, APPs)."""
+    hasB = DB > 0 and lo < DB
+    if not hasB:
+        DB = 0
+    nprefA = DA if hi == DA else max(hi - 1, 0)
+    blast = hasB and lo <= DB - 1 < hi  # the task holding B's last output also takes B's APP
+    npref = max(nprefA, DB if blast else 0)
+    pk = sc = 0
+    for J in range(DA):
+        for e in range(lo, min(J, hi)):
+            if J < DB:
+                pk += 1
+            else:
+                sc += 1
+        if J < npref:
+            if J < DB:
+                pk += 1
+            else:
+                sc += 1
+    writes = (hi - lo) + (max(0, min(hi, DB) - lo) if hasB else 0)
+    return pk, sc, DA + DB, writes, int(hi == DA) + int(blast)
 
 
-def var_task_cost(d, lo, hi, add=2.6):
-    # pipe cycles at 4 waves / SIMD (tools/ubench): v_pk_add_f32 2.6 (the pair kernel), v_add_f32
-    # 1.94 (one frame per lane); + LDS reads / writes issued
-    return add * var_task_adds(d, lo, hi) + 1.0 * d + 1.5 * (hi - lo) + 6.0
+def var_task_cost(DA, DB, lo, hi):
+    """Cycles of a variable task inside the running kernel: least squares over the measured phase
+    times of both schedules (tools/flood_timeline.py on the timeline builds, profiles/r04_flood_timeline_*):
+    8.2 per v_pk_add_f32 (its dependent chains issue slower than the 2.6-cycle ubench rate), 4.85
+    per v_add_f32, 18.1 per LDS read or write, 33.6 per task."""
+    pk, sc, rd, wr, apps = var_task_ops(DA, DB, lo, hi)
+    return 8.21 * pk + 4.85 * sc + 18.12 * (rd + wr) + 33.6
 
 
-def split_column(d, parts, add=2.6):
-    """output ranges [lo, hi) of a degree-d column cut into `parts` tasks of about equal cost"""
-    bounds = [0]
-    for q in range(1, parts):
-        # the cut after which the first q parts hold q/parts of the cost (greedy on prefix cost)
-        total = var_task_cost(d, 0, d, add)
-        best = min(range(bounds[-1] + 1, d), key=lambda h: abs(
-            sum(var_task_cost(d, bounds[i], bounds[i + 1], add) for i in range(len(bounds) - 1))
-            + var_task_cost(d, bounds[-1], h, add) - q * total / parts))
-        bounds.append(best)
-    bounds.append(d)
-    return [(bounds[i], bounds[i + 1]) for i in range(parts)]
-
-
-def row_cost(dcr, nslot, frames=2):
-    # per frame: the two minima (half rate, 4.1), sign parity (bitop3 per two messages), per slot
-    # edge compare + select + sign (4.1 + 4.1 + 2.2), row constants; x frames per lane
-    return frames * (4.1 * n_min_ops(dcr) + 2.2 * (dcr // 2) + 10.4 * nslot + 12.0) + 2.0 * dcr
-
-
-def makespan(tasks, cost, w):
-    per = lpt(tasks, cost, w)
-    loads = [sum(cost[tasks.index(t)] for t in p) for p in per]
-    return max(loads), per
-
-
-def task_schedule(blocks, slot, dc, dv, row_ptr, col_blocks, z, W=PW, prefix="P", frames=2, add=2.6,
-                  remap=True):
-    """Rows (LPT + refinement) and variable tasks (columns split by output range while that lowers
-    the LPT makespan) for W waves.  frames / add: lanes' frames and the pipe cost of one ordered
-    add (2 frames on v_pk_add_f32, or 1 on v_add_f32)."""
-    mb = len(dc)
-    nb = len(dv)
-    # rows
-    rows = list(range(mb))
-    rc = [row_cost(dc[r], sum(1 for i in range(row_ptr[r], row_ptr[r + 1]) if slot[i] >= 0), frames) for r in rows]
-    chk = balance(rows, rc, W)
-    # variable tasks: split the heaviest columns while the LPT makespan improves
-    vcols = [c for c in range(nb) if dv[c] >= 2]
-    parts = {c: 1 for c in vcols}
-
-    def tasks_of(parts):
-        t = []
-        for c in vcols:
-            for lo, hi in split_column(dv[c], parts[c], add):
-                t.append((c, lo, hi))
-        return t
-
-    def span(parts):
-        t = tasks_of(parts)
-        cost = [var_task_cost(dv[c], lo, hi, add) for c, lo, hi in t]
-        per = balance(t, cost, W)
+def var_schedule(vcols, dv, w, pairs=True):
+    """Variable tasks per wave.  Columns sorted by degree; every pattern of pairing neighbours in
+    that order (pairs=True; a pair's exclusive sums share v_pk_add_f32 instructions, the smaller
+    column's adds riding along for free), each balanced over the waves (LPT + move / swap
+    refinement); the smallest makespan wins (ties: least total cost).  A column is never split by
+    output range over two waves: every output reads all of the column's messages and is written in
+    place, so a split column's writes would race the other wave's reads within the phase.
+    Returns [[(A, B or -1, 0, degree of A)]] per wave."""
+    cols = sorted(vcols, key=lambda c: (-dv[c], c))
+    n = len(cols)
+    patterns = [[]]
+    if pairs:
+        def pats(i):
+            if i >= n:
+                return [[]]
+            out = [[(cols[i],)] + p for p in pats(i + 1)]
+            if i + 1 < n:
+                out += [[(cols[i], cols[i + 1])] + p for p in pats(i + 2)]
+            return out
+        patterns = pats(0)
+    else:
+        patterns = [[(c,) for c in cols]]
+    best = None
+    for pat in patterns:
+        t = [(u[0], u[1] if len(u) > 1 else -1, 0, dv[u[0]]) for u in pat]
+        cost = [var_task_cost(dv[a], dv[b] if b >= 0 else 0, lo, hi) for a, b, lo, hi in t]
+        per = balance(t, cost, w)
         c = dict(zip(t, cost))
-        return max(sum(c[x] for x in p) for p in per), per
-
-    best, per = span(parts)
-    while True:
-        t = tasks_of(parts)
-        cost = [var_task_cost(dv[c], lo, hi, add) for c, lo, hi in t]
-        heavy = t[max(range(len(t)), key=lambda i: cost[i])][0]
-        trial = dict(parts)
-        trial[heavy] += 1
-        if trial[heavy] > dv[heavy]:
-            break
-        m, p2 = span(trial)
-        if m >= best - 1e-9:
-            break
-        best, per, parts = m, p2, trial
-    # slot numbering of the pair image: column-major, heaviest columns first, so the slots of the
-    # waves with the most messages sit below the 64 KB reach of a ds_read's 16-bit offset
-    order = sorted(vcols, key=lambda c: -dv[c])
-    nslots = sum(1 for x in slot if x >= 0)
-    pslot = [-1] * nslots
-    n = 0
-    for c in order:
-        for i in col_blocks[c]:
-            pslot[slot[i]] = n
-            n += 1
-    if not remap:
-        pslot = list(range(nslots))
-    vt_ptr, vt_col, vt_lo, vt_hi = [0], [], [], []
-    for p in per:
-        for c, lo, hi in sorted(p):
-            vt_col.append(c)
-            vt_lo.append(lo)
-            vt_hi.append(hi)
-        vt_ptr.append(len(vt_col))
-    cp = [0]
-    cl = []
-    for p in chk:
-        cl += p
-        cp.append(len(cl))
-    s = f"    // {prefix}: {W} waves, {frames} frame(s) per lane; variable tasks (column, outputs [lo, hi)); slot map\n"
-    s += f"    static constexpr int {prefix}W = {W};\n"
-    s += arr(f"{prefix}_CHK_PTR", cp)
-    s += arr(f"{prefix}_CHK_ROWS", cl)
-    s += arr(f"{prefix}_VT_PTR", vt_ptr)
-    s += arr(f"{prefix}_VT_COL", vt_col)
-    s += arr(f"{prefix}_VT_LO", vt_lo)
-    s += arr(f"{prefix}_VT_HI", vt_hi)
-    s += arr(f"{prefix}_SLOT", pslot)
-    return s
+        cur = (max(sum(c[x] for x in p) for p in per), sum(cost), per)
+        key = (round(cur[0], 6), cur[1])
+        if best is None or key < best[0]:
+            best = (key, cur[2])
+    return [sorted(p) for p in best[1]]
 
 
 def main(out):

@@ -39,7 +39,7 @@ def test_hybrid_gnn_vs_oracle(cuda, oracle_mod, z, layers, B, identity):
     sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
     ref = oracle_mod.custom_variable_forward(sd, llr, conv.edge_var, conv.edge_chk, H.shape[1], H.shape[0],
                                              types=types, check_identity=identity)
-    np.testing.assert_allclose(probs.cpu().numpy(), ref.numpy(), atol=TOL, rtol=0)
+    np.testing.assert_allclose(probs.detach().cpu().numpy(), ref.numpy(), atol=TOL, rtol=0)
 
 
 def test_hybrid_gnn_loss_decode_and_one_hot_mapping(cuda, oracle_mod):
@@ -81,3 +81,20 @@ def test_hybrid_gnn_bench_size_chunks(cuda, oracle_mod):
     ref = oracle_mod.custom_variable_forward(sd, llr[spots].cpu(), conv.edge_var, conv.edge_chk, H.shape[1],
                                              H.shape[0], types=types)
     np.testing.assert_allclose(full[spots].cpu().numpy(), ref.numpy(), atol=TOL, rtol=0)
+
+
+def test_hybrid_training_is_refused_clearly(cuda):
+    """No HIP backward for the hybrid decoders: the hybrid GNN's probs carry a grad_fn whose
+    backward names the decoder (not torch's generic "does not require grad"); the hybrid min-sum
+    reads no parameter (its alpha, MGD:974, is never used), so its probs need no grad at all."""
+    H, dec, conv, types = setup(4, 2, 3)
+    llr = (torch.randn(4, H.shape[1]) + 1.5).to(cuda)
+    Av, Ac = conv.var_to_check_adjacency, conv.check_to_var_adjacency
+    p, loss = dec(llr, conv.message_to_var_index().to(cuda), types.to(cuda), Av, Ac, ground_truth=torch.zeros_like(llr))
+    assert p.requires_grad
+    with pytest.raises(NotImplementedError, match="CustomVariableMessageGNNDecoder"):
+        loss.mean().backward()
+    from ldpc_neural_decoder.models import create_custom_minsum_message_gnn_decoder
+    hdec, _ = create_custom_minsum_message_gnn_decoder(H, num_iterations=3)
+    q = hdec(llr)
+    assert not q.requires_grad

@@ -160,7 +160,8 @@ def test_check_layer_update_general_rows(cuda):
         rows[m, 0] = rng.integers(0, 10)
         rows[m, pos] = ids
     rows[0, 1:] = [3, 7, 11, -1, 5, -1]
-    got = CustomCheckMessageGNNLayer(1, 8).check_layer_update(torch.from_numpy(x).to(cuda), None,
+    rows[1, 1:] = [4, -2, 9, -7, 13, -2]  # any negative id is padding (the reference keeps ids >= 0, MGD:1004)
+    got =CustomCheckMessageGNNLayer(1, 8).check_layer_update(torch.from_numpy(x).to(cuda), None,
                                                               torch.from_numpy(rows)).cpu().numpy()
     ref = _literal_check_rows(x, rows)
     assert np.array_equal(np.isnan(got), np.isnan(ref))

@@ -360,43 +360,6 @@ def test_streaming_large_sparse_code_chunked_grid(cuda, oracle_mod):
     assert np.array_equal(bits.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("variant", ["LDPC_FLOOD_PAIR", "LDPC_FLOOD_W6"])
-@pytest.mark.parametrize("z", [4, 32])
-@pytest.mark.parametrize("algo", ["minsum", "bp"])
-def test_pair_kernel_matches_fixed_kernel(cuda, monkeypatch, z, algo, variant):
-    """The opt-in kernels without early stopping on the reference's codes -- the frame-pair kernel
-    (two frames per lane, LDPC_FLOOD_PAIR=1) and the 6-wave kernel (LDPC_FLOOD_W6=1) -- against the
-    default 4-wave fixed kernel: identical decisions, counters and iteration outputs, for odd batch
-    sizes (a workgroup's last frame(s) missing), both output dtypes, and zeros / infinities / NaN in
-    some frames (the exact path)."""
-    H = H_of(z)
-    n = H.shape[1]
-    rng = np.random.default_rng(100 + z)
-    mk = (lambda: MinSumScaledDecoder(H, 6, 0.75, early_stopping=False)) if algo == "minsum" \
-        else (lambda: BeliefPropagationDecoder(H, 6, early_stopping=False))
-    for B, snr, special in ((1, 0.0, False), (3, -2.0, False), (37, 1.0, True), (1001, 2.0, True)):
-        llr = (2 * 10 ** (snr / 10) * (1 / np.sqrt(2) + rng.normal(0, np.sqrt(10 ** (-snr / 10) / 2), size=(B, n))))
-        llr = llr.astype(np.float32)
-        if special:
-            llr[0, :23] = 0.0
-            llr[min(2, B - 1), 5] = np.inf
-            llr[min(4, B - 1), 9] = -np.inf
-            llr[B - 1, 11] = np.nan
-        x = torch.from_numpy(llr).to(cuda)
-        outs = []
-        for pair in ("1", "0"):
-            monkeypatch.setenv(variant, pair)
-            cnt = torch.zeros(4, dtype=torch.int64, device=cuda)
-            b8, it, fi = mk().decode(x, out_dtype=torch.uint8, counters=cnt, return_frame_iters=True)
-            bf, _ = mk().decode(x)
-            outs.append((b8, it, fi, cnt, bf))
-        (b8p, itp, fip, cp, bfp), (b8f, itf, fif, cf, bff) = outs
-        assert torch.equal(b8p, b8f), (B, snr)
-        assert torch.equal(bfp, bff) and torch.equal(bfp, b8p.float())
-        assert itp == itf == 6 and torch.equal(fip, fif)
-        assert torch.equal(cp, cf)
-
-
 def test_cfg3_full_batch_spot_frames_vs_oracle(cuda, oracle_mod, H32):
     """cfg3 exactly as benched (BG2 Z=32, min-sum alpha 0.75, 10 iterations, B = 65 536 frames of
     the on-device channel at 2 dB, bench.py's seed): four spot frames spread over the batch (first,

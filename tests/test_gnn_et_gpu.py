@@ -21,7 +21,9 @@ pytestmark = pytest.mark.gpu
 
 def _decoder(z, layers, cuda, seed=0):
     torch.manual_seed(seed)
-    base = load_base_matrix(code_path(z))
+    # Z = 384 (5G's largest lifting): the BG2 shifts of the Z = 32 file lifted at 384, N = 19 968 --
+    # the syndrome pass's variable sums no longer fit its LDS cache and are summed again instead
+    base = load_base_matrix(code_path(32 if z == 384 else z))
     H = expand_base_matrix(base, z)
     dec, conv = create_message_gnn_decoder(H, num_iterations=layers, hidden_dim=64, base_graph=base, Z=z)
     with torch.no_grad():
@@ -52,7 +54,7 @@ def test_no_stop_is_the_full_run(cuda):
 
 
 @pytest.mark.parametrize("compact", ["1", "0"])
-@pytest.mark.parametrize("z,layers,B", [(4, 5, 512), (32, 4, 64), (32, 15, 64), (32, 3, 300)])
+@pytest.mark.parametrize("z,layers,B", [(4, 5, 512), (32, 4, 64), (32, 15, 64), (32, 3, 300), (384, 3, 8)])
 def test_stops_exactly_on_codeword_decisions(cuda, oracle_mod, monkeypatch, z, layers, B, compact):
     """(compact: after a syndrome pass the layers walk the list of frames still decoding, or --
     LDPC_GNN_ET_COMPACT=0 -- every frame, skipping the finished ones; same results either way)"""
@@ -83,34 +85,6 @@ def test_fp32_early_termination_is_refused(cuda):
     llr = awgn_llr(4, H.shape[1], 3.0, device=cuda)
     with pytest.raises(NotImplementedError):
         _run(dec, conv, base, 4, llr, True)
-
-
-@pytest.mark.parametrize("variant", ["0", "6", "7", "8"])
-@pytest.mark.parametrize("et", [False, True])
-def test_mlp_variants_are_bitwise_equal(cuda, monkeypatch, variant, et):
-    """The bf16 MLP kernel's occupancy / prefetch variants (LDPC_GNN_BF16_MLP: 1 default, 0 = 3
-    waves without register prefetch, 6 = feature rows two tiles ahead) run the same arithmetic in
-    the same order: bitwise equal probs and layer counts, with and without early termination."""
-    base, H, dec, conv = _decoder(32, 6, cuda, seed=2)
-    llr = awgn_llr(300, H.shape[1], 4.0, seed=21, device=cuda)
-    monkeypatch.setenv("LDPC_GNN_BF16_MLP", "1")
-    p1, it1 = _run(dec, conv, base, 32, llr, et)
-    monkeypatch.setenv("LDPC_GNN_BF16_MLP", variant)
-    p2, it2 = _run(dec, conv, base, 32, llr, et)
-    assert torch.equal(p1, p2) and torch.equal(it1, it2)
-
-
-def test_msg_out_order_is_bitwise_neutral(cuda, monkeypatch):
-    """msg_out rows variable-major (default) or in message order (LDPC_GNN_MSGOUT_VM=0): the output
-    stage and the syndrome pass sum each variable's messages in the same ascending order either
-    way, so probs and layer counts are bitwise equal."""
-    base, H, dec, conv = _decoder(32, 6, cuda, seed=4)
-    llr = awgn_llr(200, H.shape[1], 4.0, seed=23, device=cuda)
-    monkeypatch.setenv("LDPC_GNN_MSGOUT_VM", "1")
-    p1, it1 = _run(dec, conv, base, 32, llr, True)
-    monkeypatch.setenv("LDPC_GNN_MSGOUT_VM", "0")
-    p2, it2 = _run(dec, conv, base, 32, llr, True)
-    assert torch.equal(p1, p2) and torch.equal(it1, it2)
 
 
 def test_group_mean_grid_cap_is_bitwise_neutral(cuda, monkeypatch):

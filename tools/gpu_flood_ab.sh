@@ -1,0 +1,20 @@
+# Flood kernel A/B on one box: the default library against variant libraries (interleaved, two
+# rounds), plus the phase timelines of timeline builds.  Lines land in gpurun_out/flood_ab/.
+# usage: bash tools/gpu_flood_ab.sh "<variant names>" "<timeline names>" [bench args]
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/flood_ab; mkdir -p $O
+V=$R/ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib/variants
+VARS=$1; TLS=$2; shift 2
+run() {  # tag lib args...
+  local tag=$1 lib=$2; shift 2
+  LDPC_AMD_LIB=$lib timeout -k 10 120 python3 bench.py --cpu-baseline-seconds 0 "$@" > $O/$tag.json 2> $O/$tag.err || { echo "$tag rc=$?"; tail -5 $O/$tag.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/$tag.json')); print('$tag', round(d['value']/1e6,3), 'M', round(d['roofline']['kernel_ms'],4), 'ms')"
+}
+for r in 1 2; do
+  run base_$r $R/ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib/libldpc_amd.so "$@"
+  for v in $VARS; do run ${v}_$r $V/$v.so "$@"; done
+done
+for t in $TLS; do
+  LDPC_TIMELINE_OUT=$O/$t.bin run $t $V/$t.so --steps 1 --warmup 1 "$@"
+  python3 tools/flood_timeline.py $O/$t.bin $O/$t.json > /dev/null && echo "timeline $t ok"
+done

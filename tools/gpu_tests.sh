@@ -6,6 +6,6 @@ timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_ou
 echo smoke ok
 K=()
 [ -n "$1" ] && K=(-k "$1")
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider "${K[@]}" > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rP --timeout 240 --timeout-method thread -p no:cacheprovider "${K[@]}" > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -5 gpurun_out/pytest_gpu.log
 exit $rc
