@@ -1313,7 +1313,28 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     add_tiles(vptr, vmem, n_vgroups, 0);
     int n_v1 = 0;  // var tiles come first, sorted by degree: the degree-1 ones lead
     while (2 * n_v1 < (int)gt_meta.size() && gt_meta[2 * n_v1] == 1) ++n_v1;
+    const int n_gt_v = (int)(gt_meta.size() / 2);
     add_tiles(cptr, cmem, n_cgroups, n_vgroups);
+    // bf16 MLP tiles (gnn.hpp ct_m0): whole check groups when each is a contiguous message run of
+    // at most 32 (greedy, in message order), else plain 32-message tiles
+    bool aligned = true;
+    for (int g = 0; g < n_cgroups && aligned; ++g) {
+        const int d = cptr[g + 1] - cptr[g];
+        aligned = d <= 32 && (d == 0 || cmem[cptr[g + 1] - 1] - cmem[cptr[g]] == d - 1);
+    }
+    std::vector<int32_t> ct_m0{0};
+    if (aligned) {
+        int64_t m = 0;
+        while (m < E) {
+            const int g = h_cgroup[m];
+            const int d = cptr[g + 1] - cptr[g];  // the group's run starts at m (contiguous, ascending)
+            if (m + d - ct_m0.back() > 32) ct_m0.push_back((int32_t)m);
+            m += d;
+        }
+    } else {
+        for (int64_t m = 32; m < E; m += 32) ct_m0.push_back((int32_t)m);
+    }
+    ct_m0.push_back((int32_t)E);
     // fp32 path: projection tiles of 32 groups of one side (gnn.hpp), each side sorted by degree
     std::vector<int32_t> pt;  // meta [4 n] | grp [32 n] | deg [32 n] | mem
     std::vector<int32_t> pt_meta, pt_grp, pt_deg, pt_mem;
@@ -1381,7 +1402,9 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     hipError_t e3 = hipMalloc(&p->d_inv, inv.size() * 4);
     hipError_t e4 = hipMalloc(&p->d_gt, gt_words * 4);
     hipError_t e5 = hipMalloc(&p->d_pt, pt.size() * 4);
-    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
+    hipError_t e6 = hipMalloc(&p->d_ct, ct_m0.size() * 4);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess ||
+        e6 != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan allocation failed");
     }
@@ -1391,7 +1414,8 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         hipMemcpy(p->d_gt + gt_meta.size(), gt_grp.data(), gt_grp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_gt + gt_meta.size() + gt_grp.size(), gt_mem.data(), gt_mem.size() * 4,
                   hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->d_pt, pt.data(), pt.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(p->d_pt, pt.data(), pt.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_ct, ct_m0.data(), ct_m0.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan upload failed");
     }
@@ -1405,6 +1429,10 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     p->mt_perm = p->pt_mem + pt_mem.size();
     p->n_mtiles = (int)(mperm.size() / 32);
     p->n_mtiles_v1 = n_mtiles_v1;
+    p->n_gtiles_v = n_gt_v;
+    p->n_ctiles = (int)ct_m0.size() - 1;
+    p->ct_aligned = aligned;
+    p->ct_m0 = p->d_ct;
     p->vgroup = p->d_tab;
     p->cgroup = p->vgroup + E;
     p->vg_ptr = p->cgroup + E;
@@ -1489,6 +1517,7 @@ extern "C" int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p) {
     if (p->d_w) (void)hipFree(p->d_w);
     if (p->d_gt) (void)hipFree(p->d_gt);
     if (p->d_pt) (void)hipFree(p->d_pt);
+    if (p->d_ct) (void)hipFree(p->d_ct);
     delete p;
     return LDPC_OK;
 }

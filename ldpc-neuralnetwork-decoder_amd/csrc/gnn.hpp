@@ -23,6 +23,7 @@ struct ldpc_gnn_plan {
     //   offset by Gv; -1 = padding), gt_mem[off + 8 i + q] = i-th member message of group q.
     int n_gtiles = 0;
     int n_gtiles_v1 = 0;  // the leading tiles whose groups are var groups of degree 1
+    int n_gtiles_v = 0;   // the var side's tiles (the check side's follow)
     int32_t *d_gt = nullptr;
     const int2 *gt_meta = nullptr;
     const int32_t *gt_grp = nullptr, *gt_mem = nullptr;
@@ -42,6 +43,15 @@ struct ldpc_gnn_plan {
     // tiles with -1, so every tile is either all degree-1 or has none.  mt_perm[32 n_mtiles].
     int n_mtiles = 0, n_mtiles_v1 = 0;
     const int32_t *mt_perm = nullptr;
+    // bf16 MLP message tiles (gnn_bf16.hip): tile k of a frame holds messages ct_m0[k] .. ct_m0[k+1]
+    // - 1 (at most 32).  When every check group is a contiguous run of at most 32 messages (the
+    // reference's check-major edge order, message_gnn_decoder.py:397-406), the tiles hold whole
+    // check groups (ct_aligned) and the MLP forms the check means from its own tile; otherwise
+    // they are the plain 32-message tiles.
+    int n_ctiles = 0;
+    bool ct_aligned = false;
+    int32_t *d_ct = nullptr;
+    const int32_t *ct_m0 = nullptr;  // [n_ctiles + 1]
 };
 
 namespace ldpc {

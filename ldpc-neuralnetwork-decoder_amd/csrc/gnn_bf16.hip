@@ -47,7 +47,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int H = 64;
-constexpr int kMlpThreads = 256;  // the MLP kernel's workgroup (4 waves), 2 waves per SIMD
+constexpr int kMlpThreads = 512;  // the MLP kernel's workgroup (8 waves): one per CU, 2 waves per SIMD
 
 __host__ __device__ constexpr int pi_unit(int p) {
     return 32 * (p >> 5) + 16 * ((p >> 4) & 1) + 8 * ((p >> 2) & 1) + 4 * ((p >> 3) & 1) + (p & 3);
@@ -104,15 +104,29 @@ __global__ __launch_bounds__(128) void gnn_bf16_kconst_kernel(const float *blob,
     }
 }
 
-// info.x = var group, or ~var group (< 0) for a degree-1 var group when `d1` (see header)
-__global__ void gnn_bf16_info_kernel(int E, const int32_t *vgroup, const int32_t *vg_ptr, int d1,
-                                     const int32_t *cgroup, const int32_t *msg_type, const int32_t *msg_var,
-                                     int4 *info) {
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= E) return;
-    const int g = vgroup[m];
+// Per tile slot i = 32 k + j (lane j of a frame's tile k, gnn.hpp ct_m0):
+//   info[i] = {var group, or ~var group (< 0) for a degree-1 var group when `d1` (see header),
+//              check group, type, variable} of the slot's message
+//   slot[i] = {message, or ~message of the tile's last one for a padding slot; mask of the tile
+//              slots holding the message's check group (aligned tiles), 0 for padding}
+__global__ void gnn_bf16_info_kernel(int nslots, const int32_t *ct_m0, int aligned, const int32_t *vgroup,
+                                     const int32_t *vg_ptr, int d1, const int32_t *cgroup, const int32_t *cg_ptr,
+                                     const int32_t *cg_mem, const int32_t *msg_type, const int32_t *msg_var,
+                                     int4 *info, int2 *slot) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nslots) return;
+    const int k = i >> 5, j = i & 31;
+    const int m0 = ct_m0[k], n = ct_m0[k + 1] - m0;
+    const int m = m0 + (j < n ? j : n - 1);
+    const int g = vgroup[m], cg = cgroup[m];
     const bool one = d1 && vg_ptr[g + 1] - vg_ptr[g] == 1;
-    info[m] = make_int4(one ? ~g : g, cgroup[m], msg_type[m], msg_var[m]);
+    info[i] = make_int4(one ? ~g : g, cg, msg_type[m], msg_var[m]);
+    uint32_t mask = 0;
+    if (aligned && j < n) {
+        const int d = cg_ptr[cg + 1] - cg_ptr[cg], s = cg_mem[cg_ptr[cg]] - m0;
+        mask = (d >= 32 ? 0xFFFFFFFFu : ((1u << d) - 1u)) << s;
+    }
+    slot[i] = make_int2(j < n ? m : ~m, (int)mask);
 }
 
 struct GtArgs {
@@ -262,20 +276,37 @@ constexpr int kKStride = 132;
 #define LDPC_BF16_D1_STRIDE 68
 #endif
 constexpr int kD1Stride = LDPC_BF16_D1_STRIDE;
-inline size_t mlp_lds_bytes(int T, bool d1) {
+// then (MODE bit 2) one 4 KB staging tile per wave for the in-tile check sums
+constexpr int kCTileB = 32 * 128;
+__host__ __device__ inline size_t mlp_tables_bytes(int T, bool d1) {
     return (size_t)kOffK + ((size_t)(T + 2) * kKStride + 192 + (d1 ? (size_t)T * kD1Stride : 0)) * 4;
 }
+inline size_t mlp_lds_bytes(int T, bool d1) {
+    return (mlp_tables_bytes(T, d1) + 15) / 16 * 16 + (size_t)(kMlpThreads / 64) * kCTileB;
+}
+// byte offset of (message row, byte b of its 128-B feature row) in a staging tile: 16-B chunks
+// XOR-swizzled by the row so that the four ds_write_b128 of a tile and the eight
+// ds_read_b64_tr_b16 that transpose it are all conflict-free (64-bank model of the LDS table in
+// MI355X_MICROARCH.md)
+__device__ __forceinline__ int ctile_off(int row, int b) {
+    return row * 128 + 16 * ((b >> 4) ^ (((row & 3) << 1) | ((row >> 2) & 1))) + (b & 15);
+}
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 struct MlpArgs {
     const __bf16 *x_in;  // null at layer 0
     __bf16 *x_out;       // null at the last layer
-    const __bf16 *Mv, *Mc;               // group-mean rows
-    const int4 *info;                    // per message {var group, check group, type, variable}
+    const __bf16 *Mv, *Mc;               // group-mean rows (Mc: layer 0, or tiles not check-aligned)
+    const int4 *info;                    // per tile slot (gnn_bf16_info_kernel)
+    const int2 *slot;                    // per tile slot {message, check member mask}
+    const float *inv_c;                  // 1 / |check group|
+    const float *memb_c;                 // this layer's mean type embedding per check group (Gc, 64)
     const float *llr;
     const float *w1v, *w1c, *w2v, *w2c;  // this layer, nn.Linear layout, fp32
     const float *kd;                     // this layer's derived constants
     const float *bo;                     // output_projection bias (device)
-    int T, Gv, Gc, E, N, tpf;            // tpf = 32-message tiles per frame
+    int T, Gv, Gc, E, N, tpf;            // tpf = message tiles per frame (gnn.hpp ct_m0)
     int d1;                              // degree-1 var groups use D1 (info.x < 0), layers >= 1
     int64_t B;
     float *msg_out;                      // last layer / early termination: (B, E) projected LLRs
@@ -287,16 +318,32 @@ struct MlpArgs {
 // Per-tile inputs of one lane (message j of the tile, lane half h).
 struct TileIn {
     bf16x8 xf[4], af[4], cf[4];
+    float mb[32];     // in-tile check means: the check group's mean type embedding, stored positions 16 s + 8 h + i
+    float cinv;       // ... 1 / |check group|
+    uint32_t cmask;   // ... the tile slots of the check group
     float l;
     int ty, var;
     bool one;  // degree-1 var group (D1 constant instead of K[ty][var side])
     int64_t row, b;
     bool ok, on;  // on: the frame is still decoding (early termination)
 };
+struct SlotIn {
+    int4 inf;
+    int2 sl;
+};
 
 // MODE bit 0: layer 0 (x from the LLRs, no GEMM1 over x, no residual); bit 1: last layer
-// (output projection + per-variable sum instead of writing x).  The next tile's rows are
-// prefetched into registers one tile ahead, the small per-tile items two tiles ahead.
+// (output projection + per-variable sum instead of writing x); bit 2: check means in-tile (the
+// tiles hold whole check groups: the check side's group mean is formed here from the tile's own
+// feature rows, message_gnn_decoder.py:116-118, instead of read from a group-mean pass):
+//   sum_c(m) = X S   as v_mfma_f32_32x32x16_bf16: A = the tile's feature rows transposed through
+//                    a swizzled LDS tile by ds_read_b64_tr_b16 (rows permuted so that the
+//                    accumulator holds exactly the stored positions GEMM1's B operand takes), B =
+//                    S[k][j] = 1 when slots k and j share a check (bf16 1.0 / 0, exact)
+//   g_c(m) = bf16(sum_c(m) / |group| + mean of the group's type embeddings)  (fp32 math, as the
+//                    group-mean kernel: the same value up to the summation order of the sum)
+// The next tile's rows are prefetched into registers one tile ahead, the small per-tile items two
+// tiles ahead.
 template <int MODE>
 __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -328,7 +375,8 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
-    constexpr bool layer0 = (MODE & 1) != 0, last = (MODE & 2) != 0;
+    constexpr bool layer0 = (MODE & 1) != 0, last = (MODE & 2) != 0, itc = (MODE & 4) != 0;
+    char *ctile = smem + (mlp_tables_bytes(A.T, A.d1 != 0) + 15) / 16 * 16 + wave * kCTileB;
     // tiles of the frames still decoding: slot-major (slot s = the s-th listed frame)
     const int64_t nact = A.count ? (int64_t)__builtin_amdgcn_readfirstlane(*A.count) : A.B;
     const int64_t ntiles = nact * A.tpf;
@@ -338,20 +386,22 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
     const int64_t sb = tw.stride / A.tpf, sk = tw.stride - sb * A.tpf;
     int64_t fb = tw.first / A.tpf, fk = tw.first - fb * A.tpf;
 
-    // per-message static info {var group, check group, type, variable} of this lane's message
+    // this lane's tile slot: {var group, check group, type, variable}, {message, check mask}
     auto load_info = [&](int64_t k) {
-        const int m0 = (int)k * 32 + j;
-        return A.info[m0 < A.E ? m0 : A.E - 1];
+        SlotIn s;
+        s.inf = A.info[k * 32 + j];
+        s.sl = A.slot[k * 32 + j];
+        return s;
     };
     // the frame's "still decoding" flag of tile t (frame b), read ahead of the tile's row loads
     auto load_on = [&](int64_t t, int64_t b) -> bool {
         return A.list || !A.active || A.active[t < tw.end ? b : fb];  // listed frames are active
     };
-    auto load = [&](const int4 &inf, bool on, int64_t t, int64_t b, int64_t k) {
+    auto load = [&](const SlotIn &si, bool on, int64_t t, int64_t b, int64_t k) {
         TileIn I;
-        const int m0 = (int)k * 32 + j;
-        I.ok = m0 < A.E && t < tw.end;
-        const int m = m0 < A.E ? m0 : A.E - 1;
+        const int4 inf = si.inf;
+        I.ok = si.sl.x >= 0 && t < tw.end;
+        const int m = si.sl.x >= 0 ? si.sl.x : ~si.sl.x;
         const int64_t bb = frame_of(t < tw.end ? b : fb);
         I.ty = inf.z;
         I.var = inf.w;
@@ -381,13 +431,75 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
 #pragma unroll
             for (int s = 0; s < 4; ++s) I.af[s] = I.xf[s];
         }
+        if constexpr (itc) {
+            I.cmask = (uint32_t)si.sl.y;
+            I.cinv = A.inv_c[inf.y];
+            const float *mbr = A.memb_c + (int64_t)inf.y * H + 8 * h;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) I.cf[s] = ld8(mc + 32 * s);
+            for (int s = 0; s < 4; ++s) {
+                const float4 u = *reinterpret_cast<const float4 *>(mbr + 16 * s);
+                const float4 v = *reinterpret_cast<const float4 *>(mbr + 16 * s + 4);
+                I.mb[8 * s] = u.x; I.mb[8 * s + 1] = u.y; I.mb[8 * s + 2] = u.z; I.mb[8 * s + 3] = u.w;
+                I.mb[8 * s + 4] = v.x; I.mb[8 * s + 5] = v.y; I.mb[8 * s + 6] = v.z; I.mb[8 * s + 7] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) I.cf[s] = ld8(mc + 32 * s);
+        }
         return I;
     };
 
-    auto compute = [&](const TileIn &I) {
+    // In-tile check means (MODE bit 2): g_c of this lane's message from the tile's feature rows
+    auto check_means = [&](TileIn &I) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8 *>(ctile + ctile_off(j, 32 * s + 16 * h)) = I.xf[s];
+        __builtin_amdgcn_wave_barrier();
+        // A fragment (row tile rt, k-step ks): lane (r, h) <- stored position sigma(32 rt + r) of
+        // slots 16 ks + 8 h + 0..7 (sigma swaps bits 2 and 3 of r: the accumulator's register
+        // 8 (s & 1) + i of tile s >> 1 then holds stored position 16 s + 8 h + i).  One
+        // ds_read_b64_tr_b16 per four slots: group lane 4q + p addresses slot row q, 4 stored
+        // positions; lane i of the 16-lane group receives column i (MI355X: T10).
+        const int g16 = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3, hh = g16 >> 1;
+        const int col0 = 16 * (g16 & 1) + 4 * (2 * (p & 1) + (p >> 1));
+        f32x16 sum[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) sum[rt] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            // B = S: element e of lane (j, h) is slot 16 ks + 8 h + e in j's check (bf16 1.0 / 0)
+            const uint32_t bits = (I.cmask >> (16 * ks + 8 * h)) & 0xFFu;
+            uint32_t sw[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+                const uint32_t t = (bits >> (2 * e2)) & 3u;
+                sw[e2] = ((t | (t << 15)) & 0x10001u) * 0x3F80u;
+            }
+            const bf16x8 sop = __builtin_bit_cast(bf16x8, (uint32_t __attribute__((ext_vector_type(4)))){sw[0], sw[1], sw[2], sw[3]});
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                const int col = 32 * rt + col0, row = 16 * ks + 8 * hh + q;
+                const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4 *)(ctile + ctile_off(row, 2 * col)));
+                const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4 *)(ctile + ctile_off(row + 4, 2 * col)));
+                const s16x4 a8[2] = {lo, hi};
+                const bf16x8 afr = __builtin_bit_cast(bf16x8, a8);
+                sum[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, sop, sum[rt], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the next tile's staging writes wait for these reads
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            bf16x8 o;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = (__bf16)fmaf(sum[s >> 1][8 * (s & 1) + i], I.cinv, I.mb[8 * s + i]);
+            I.cf[s] = o;
+        }
+    };
+
+    auto compute = [&](TileIn &I) {
         if (!I.on) return;
+        if constexpr (itc) check_means(I);
         const float *Kt = Ks + I.ty * kKStride;
         f32x16 y0 = ld16(tail + 16 * h), y1 = ld16(tail + 32 + 16 * h);  // b2v + b2c
         int wbase = j * w1row + 16 * h, w2base = j * 144 + 16 * h;
@@ -483,12 +595,12 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
         TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
         int64_t nb = fb + sb, nk = fk + sk;
         if (nk >= A.tpf) { nk -= A.tpf; ++nb; }
-        int4 inf_n = load_info(nk);
+        SlotIn inf_n = load_info(nk);
         bool on_n = load_on(tw.first + tw.stride, nb);
         for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
             int64_t nb2 = nb + sb, nk2 = nk + sk;
             if (nk2 >= A.tpf) { nk2 -= A.tpf; ++nb2; }
-            const int4 inf_nn = load_info(nk2);
+            const SlotIn inf_nn = load_info(nk2);
             const bool on_nn = load_on(t + 2 * tw.stride, nb2);
             const TileIn nxt = load(inf_n, on_n, t + tw.stride, nb, nk);
             compute(cur);
@@ -586,6 +698,7 @@ struct Bf16Ws {
     float *kd, *memb, *msg_out;
     int32_t *csr, *alist, *acount, *cg_var;
     int4 *info;
+    int2 *slot;
     uint8_t *active;
     __bf16 *xa, *xb, *Mv, *Mc;
     int64_t bytes;
@@ -596,11 +709,13 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4);
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
     const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * p->E * 4);
-    const int64_t inf = al(p->E * 16), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
+    const int64_t nslot = (int64_t)p->n_ctiles * 32;
+    const int64_t inf = al(nslot * 16) + al(nslot * 8), act = al(B), cs = al(gnn_csr_ints(p->E, N) * 4);
     const int64_t alb = al(2 * B * 4) + 256;  // two active lists [B] + the two ranges' two counts
     char *c = static_cast<char *>(base);
     Bf16Ws w;
     w.info = reinterpret_cast<int4 *>(c + kd + memb + xa + xb + mv + mc + vs);
+    w.slot = reinterpret_cast<int2 *>(c + kd + memb + xa + xb + mv + mc + vs + al(nslot * 16));
     w.active = reinterpret_cast<uint8_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf);
     w.csr = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act);
     w.kd = reinterpret_cast<float *>(c);
@@ -630,15 +745,18 @@ int launch_mlp_t(int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     return LDPC_OK;
 }
 
-// the MLP kernel per layer mode (bit 0 layer 0, bit 1 last layer): 256 threads, 2 waves per SIMD,
-// next tile prefetched into registers (measured against 3-4 waves per SIMD, one 512-thread
-// workgroup per CU and deeper prefetch: all within 2 % or slower)
+// the MLP kernel per layer mode (bit 0 layer 0, bit 1 last layer, bit 2 in-tile check means): one
+// 512-thread workgroup per CU, 2 waves per SIMD, next tile prefetched into registers (measured
+// against 3-4 waves per SIMD and deeper prefetch: all within 2 % or slower)
 int launch_mlp(int mode, int64_t tiles, size_t lds, hipStream_t s, const MlpArgs &m) {
     switch (mode) {
         case 0: return launch_mlp_t<0>(tiles, lds, s, m);
         case 1: return launch_mlp_t<1>(tiles, lds, s, m);
         case 2: return launch_mlp_t<2>(tiles, lds, s, m);
-        default: return launch_mlp_t<3>(tiles, lds, s, m);
+        case 3: return launch_mlp_t<3>(tiles, lds, s, m);
+        case 4: return launch_mlp_t<4>(tiles, lds, s, m);
+        case 6: return launch_mlp_t<6>(tiles, lds, s, m);
+        default: return fail(LDPC_EINVAL, "bad MLP mode");
     }
 }
 
@@ -682,11 +800,12 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     Bf16Ws w = carve_bf16(p, N, B, T, L, d_work);
     if (!d_work || work_bytes < w.bytes)
         return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
-    const int64_t tpf = (p->E + 31) / 32;
+    const int64_t tpf = p->n_ctiles;  // message tiles per frame (gnn.hpp ct_m0)
+    if (tpf <= 0) return fail(LDPC_EUNSUPPORTED, "plan has no message tiles");
     if (B * tpf >= (1LL << 31) || B * p->n_gtiles >= (1LL << 31) || p->E >= (1LL << 31))
         return fail(LDPC_EUNSUPPORTED, "batch too large for one launch (chunk it)");
-    // degree-1 skip when its D1 table still lets two 256-thread workgroups share a CU's LDS
-    const bool d1 = p->n_gtiles_v1 > 0 && 2 * mlp_lds_bytes(T, true) <= 160 * 1024;
+    // degree-1 skip when its D1 table still fits the LDS image
+    const bool d1 = p->n_gtiles_v1 > 0 && mlp_lds_bytes(T, true) <= 160 * 1024;
     const size_t lds = mlp_lds_bytes(T, d1);
     if (T > kBf16MaxTypes || lds > 160 * 1024)
         return fail(LDPC_EUNSUPPORTED, "too many message types for the bf16 LDS image");
@@ -698,8 +817,10 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     const GtArgs G{p->gt_meta, p->gt_grp, p->gt_mem, p->n_gtiles, 0};
     const int Gtot = p->Gv + p->Gc;
     {
-        hipLaunchKernelGGL(gnn_bf16_info_kernel, dim3((unsigned)((p->E + 255) / 256)), dim3(256), 0, s, (int)p->E,
-                           p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, d_msg_type, d_msg_var, w.info);
+        const int nslot = (int)(tpf * 32);
+        hipLaunchKernelGGL(gnn_bf16_info_kernel, dim3((unsigned)((nslot + 255) / 256)), dim3(256), 0, s, nslot,
+                           p->ct_m0, p->ct_aligned ? 1 : 0, p->vgroup, p->vg_ptr, d1 ? 1 : 0, p->cgroup, p->cg_ptr,
+                           p->cg_mem, d_msg_type, d_msg_var, w.info, w.slot);
         LDPC_CHECK_LAUNCH("gnn_bf16_info_kernel");
     }
     hipLaunchKernelGGL(gnn_bf16_kconst_kernel, dim3(L, T + 2), dim3(128), 0, s, d_weights, T, w.kd);
@@ -735,6 +856,9 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     const __bf16 *x_in = nullptr;
     for (int l = 0; l < L; ++l) {
         const LayerW lw = layer_w(d_weights, T, l);
+        // layers >= 1 on check-aligned tiles: the MLP forms the check means itself, the group-mean
+        // pass does the var groups alone (layer 0's means come from the LLRs: both sides here)
+        const bool itc = p->ct_aligned && l > 0;
         GmArgs gm{};
         gm.x_in = x_in;
         gm.llr = d_llr + b0 * N;
@@ -744,6 +868,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.memb = w.memb + (int64_t)l * Gtot * H;
         gm.G = G;
         if (d1 && l > 0) gm.G.first = p->n_gtiles_v1;
+        if (itc) gm.G.n_tiles = p->n_gtiles_v;
         gm.Mv = w.Mv + b0 * p->Gv * H;
         gm.Mc = w.Mc + b0 * p->Gc * H;
         gm.Gv = p->Gv;
@@ -754,7 +879,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         gm.active = act;
         gm.list = listed ? alist : nullptr;
         gm.count = listed ? acount : nullptr;
-        {
+        if (gm.G.n_tiles > gm.G.first) {
             const int64_t gwaves = nb * (gm.G.n_tiles - gm.G.first);
             int64_t gblocks = (gwaves + 3) / 4;
             if (gm.count && gm_cap() > 0) gblocks = std::min<int64_t>(gblocks, (int64_t)g_cus * gm_cap());
@@ -768,6 +893,9 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.Mv = w.Mv + b0 * p->Gv * H;
         m.Mc = w.Mc + b0 * p->Gc * H;
         m.info = w.info;
+        m.slot = w.slot;
+        m.inv_c = p->inv_c;
+        m.memb_c = w.memb + ((int64_t)l * Gtot + p->Gv) * H;
         m.llr = d_llr + b0 * N;
         m.w1v = lw.w1v;
         m.w1c = lw.w1c;
@@ -789,7 +917,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.count = listed ? acount : nullptr;
         m.kd_last = et && l < L - 1 ? kd_last : nullptr;
         m.bo_last = bo_last;
-        const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0);
+        const int mode = (l == 0 ? 1 : 0) | (l == L - 1 ? 2 : 0) | (itc ? 4 : 0);
         const int rc = launch_mlp(mode, nb * tpf, lds, st, m);
         if (rc != LDPC_OK) return rc;
         LDPC_CHECK_LAUNCH("gnn_bf16_mlp_kernel");

@@ -1,14 +1,15 @@
-# Flood kernel A/B on one box: the default library against variant libraries (interleaved, two
-# rounds), plus the phase timelines of timeline builds.  Lines land in gpurun_out/flood_ab/.
-# usage: bash tools/gpu_flood_ab.sh "<variant names>" "<timeline names>" [bench args]
+# A/B on one box: the default library against variant libraries (_lib/variants/<name>.so,
+# interleaved, two rounds) on one bench workload, plus the phase timelines of flood timeline builds.
+# Lines land in gpurun_out/ab_<TAG>/.
+# usage: TAG=x bash tools/gpu_ab.sh "<variant names>" "<timeline names>" [bench args]
 set -o pipefail
-R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/flood_ab; mkdir -p $O
+R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/ab_${TAG:-flood}; mkdir -p $O
 V=$R/ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib/variants
 VARS=$1; TLS=$2; shift 2
 run() {  # tag lib args...
   local tag=$1 lib=$2; shift 2
   LDPC_AMD_LIB=$lib timeout -k 10 120 python3 bench.py --cpu-baseline-seconds 0 "$@" > $O/$tag.json 2> $O/$tag.err || { echo "$tag rc=$?"; tail -5 $O/$tag.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/$tag.json')); print('$tag', round(d['value']/1e6,3), 'M', round(d['roofline']['kernel_ms'],4), 'ms')"
+  python3 -c "import json; d=json.load(open('$O/$tag.json')); print('$tag', round(d['value']), 'cw/s', round(d['roofline']['kernel_ms'],4), 'ms', 'layers', d.get('avg_layers'), 'ber', d.get('ber'))"
 }
 for r in 1 2; do
   run base_$r $R/ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib/libldpc_amd.so "$@"
