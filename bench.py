@@ -136,10 +136,12 @@ def parse():
                          "batch-global rule, traditional_decoders.py:104-107), frame (per-frame freeze)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
                     help="target CPU work for the oracle baseline sample (0 disables)")
-    ap.add_argument("--data", choices=("zero", "codewords"), default="zero",
+    ap.add_argument("--data", choices=("auto", "zero", "codewords"), default="auto",
                     help="transmitted frames: the all-zero codeword (every reference harness, e.g. "
                          "comparative_evaluation.py:133) or random codewords (utils/encoding.py), whose BER / "
-                         "FER show a neural decoder's decoding on typical frames")
+                         "FER show a neural decoder's decoding on typical frames.  auto: codewords when the "
+                         "bf16 GNN's early termination is on (the all-zero frame stops early by construction: "
+                         "the checkpoint saw it in every batch), the all-zero codeword otherwise")
     ap.add_argument("--checkpoint", default=None,
                     help="MessageGNN weights (a trainer checkpoint dict, loaded weights_only); default: "
                          "checkpoints/gnn_bg2_z<Z>_i<layers>_h64.pt when present, else random weights")
@@ -323,6 +325,10 @@ def main():
     snr = 0.0 if sweep else snr
     iters = a.iterations or iters
     B = a.batch or bdef
+    if a.data == "auto":
+        et_on = kind == "gnn-bf16" and (a.early_termination == "on" or
+                                        (a.early_termination == "auto" and a.workload == "gnn-z32-bf16"))
+        a.data = "codewords" if et_on else "zero"
 
     from ldpc_neural_decoder import _native as N
     from ldpc_neural_decoder.utils import awgn_llr, expand_base_matrix, load_base_matrix
@@ -506,10 +512,14 @@ def main():
             # check side only: 4 H^2 per message (W1 over c + W2) + 2 H^2 per check group (projection)
             per_launch_alg = (4 * 64 * 64 * E + 2 * 64 * 64 * g_m) * B * iters
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
-        elif kind == "gnn-sweep":
-            # the reference's useful FLOPs, 12 H^2 E per frame-layer
-            per_launch_alg = nominal_flops * B * iters * len(sweep_snrs)
-            bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
+        elif kind in ("gnn-sweep", "gnn") and z == 32:
+            # SURVEY 8(d) cfg4, HBM: per frame-layer 3 passes over the fp32 features (E x 64) + the
+            # group rows written and read ((N + M) x 64 fp32, twice).  The binding resource of this
+            # build's fp32 path: its kernels move their bytes at 4-5 TB/s while its MFMA pipe (fp32
+            # products as bf16x6 splits) is a quarter busy (roofline_notes)
+            fp32_layer_bytes = (3 * E * 64 * 4 + 2 * (g_n + g_m) * 64 * 4) * B
+            per_launch_alg = fp32_layer_bytes * iters * (len(sweep_snrs) if kind == "gnn-sweep" else 1)
+            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
         elif kind == "gnn-bf16":
             # HBM-bound; per frame-layer 3 passes over the bf16 features
             # (group-mean read, MLP read + write) + the fp32-sized group-mean rows written + read
@@ -604,12 +614,15 @@ def main():
         if kind in ("gnn", "gnn-sweep"):
             reps = len(sweep_snrs) if kind == "gnn-sweep" else 1
             split = os.environ.get("LDPC_GNN_SPLIT", "1") != "0"
-            notes = {"flop_model": "achieved = SURVEY 8(d)'s algorithmic FLOPs, the reference's per-message MLPs: "
-                                   "12 H^2 E per frame-layer, against the fp32 MFMA peak. This build executes "
-                                   "8 H^2 E + 2 H^2 (N + M) fp32-equivalent FLOPs (W1's group half applied once per "
-                                   "group): executed_frac is that rate",
-                     "executed_flops_per_launch": fwd_flops * B * iters * reps,
-                     "executed_frac": fwd_flops / nominal_flops * achieved / peak}
+            secs = kern_ms * 1e-3
+            notes = {"flop_model": "the reference's per-message MLPs cost 12 H^2 E FLOP per frame-layer (SURVEY 8(d)); "
+                                   "this build executes 8 H^2 E + 2 H^2 (N + M) fp32-equivalent FLOPs (W1's group half "
+                                   "once per group). Reported for reference only: the bound is HBM (roofline.bound)",
+                     "nominal_fp32_tflops": nominal_flops * B * iters * reps / secs / 1e12,
+                     "nominal_frac_of_fp32_mfma": nominal_flops * B * iters * reps / secs / 1e12 / FP32_MFMA_PEAK_TFS,
+                     "executed_flops_per_launch": fwd_flops * B * iters * reps}
+            if bound != "hbm":  # Z = 4 (cfg2 shape): FLOPs against the fp32 MFMA peak, as SURVEY 8(d) cfg2
+                notes["executed_frac"] = fwd_flops / nominal_flops * achieved / peak
             if split:
                 # gnn_mlp2s_kernel: the per-message products (8 H^2 E) as six bf16 products each on the
                 # bf16 MFMA; the group projection (2 H^2 (N + M)) stays on the fp32 MFMA

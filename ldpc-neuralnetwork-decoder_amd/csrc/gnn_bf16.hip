@@ -136,9 +136,11 @@ struct GtArgs {
     int first;  // group-mean launches start at this tile (skipping degree-1 var tiles)
 };
 
-// memb[l][g][p] = mean over group g's messages of emb_l[type][pi(p)]  (one wave per (l, tile))
+// memb[l][g][p] = mean over group g's messages of emb_l[type][pi(p)]  (one wave per (l, tile));
+// memb16: the same rows in bf16 (the MLP's in-tile check means: 16 instead of 32 registers per
+// prefetched tile)
 __global__ __launch_bounds__(256) void gnn_bf16_memb_kernel(const float *blob, int T, int L, const int32_t *msg_type,
-                                                            GtArgs G, int Gtot, float *memb) {
+                                                            GtArgs G, int Gtot, float *memb, __bf16 *memb16) {
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= (int64_t)L * G.n_tiles) return;
     const int l = (int)(w / G.n_tiles), t = (int)(w - (int64_t)l * G.n_tiles);
@@ -154,8 +156,13 @@ __global__ __launch_bounds__(256) void gnn_bf16_memb_kernel(const float *blob, i
         for (int k = 0; k < 8; ++k) acc[k] += e[pi_unit(p0 + k)];
     }
     float *o = memb + ((int64_t)l * Gtot + g) * H + p0;
+    bf16x8 o16;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = acc[k] / (float)md.x;
+    for (int k = 0; k < 8; ++k) {
+        o[k] = acc[k] / (float)md.x;
+        o16[k] = (__bf16)o[k];
+    }
+    *reinterpret_cast<bf16x8 *>(memb16 + ((int64_t)l * Gtot + g) * H + p0) = o16;
 }
 
 // ------------------------------------------------------------------------ group means
@@ -301,7 +308,7 @@ struct MlpArgs {
     const int4 *info;                    // per tile slot (gnn_bf16_info_kernel)
     const int2 *slot;                    // per tile slot {message, check member mask}
     const float *inv_c;                  // 1 / |check group|
-    const float *memb_c;                 // this layer's mean type embedding per check group (Gc, 64)
+    const __bf16 *memb_c;                // this layer's mean type embedding per check group (Gc, 64), bf16
     const float *llr;
     const float *w1v, *w1c, *w2v, *w2c;  // this layer, nn.Linear layout, fp32
     const float *kd;                     // this layer's derived constants
@@ -318,7 +325,7 @@ struct MlpArgs {
 // Per-tile inputs of one lane (message j of the tile, lane half h).
 struct TileIn {
     bf16x8 xf[4], af[4], cf[4];
-    float mb[32];     // in-tile check means: the check group's mean type embedding, stored positions 16 s + 8 h + i
+    bf16x8 mb[4];     // in-tile check means: the check group's mean type embedding, stored positions 16 s + 8 h + i
     float cinv;       // ... 1 / |check group|
     uint32_t cmask;   // ... the tile slots of the check group
     float l;
@@ -327,10 +334,14 @@ struct TileIn {
     int64_t row, b;
     bool ok, on;  // on: the frame is still decoding (early termination)
 };
-struct SlotIn {
+// Per-tile items fetched two tiles ahead: the slot's static info and the frame's id and flag
+struct TileCtl {
     int4 inf;
     int2 sl;
+    int64_t frame;
+    bool on;
 };
+struct TilePos { int64_t t, b, k; };
 
 // MODE bit 0: layer 0 (x from the LLRs, no GEMM1 over x, no residual); bit 1: last layer
 // (output projection + per-variable sum instead of writing x); bit 2: check means in-tile (the
@@ -376,73 +387,82 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
 
     const int lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
     constexpr bool layer0 = (MODE & 1) != 0, last = (MODE & 2) != 0, itc = (MODE & 4) != 0;
+    // the output head's bias, read once (a load inside the tile loop would wait for the
+    // prefetched rows before its store)
+    const float bo_out = last ? A.bo[0] : A.kd_last ? A.bo_last[0] : 0.0f;
     char *ctile = smem + (mlp_tables_bytes(A.T, A.d1 != 0) + 15) / 16 * 16 + wave * kCTileB;
     // tiles of the frames still decoding: slot-major (slot s = the s-th listed frame)
     const int64_t nact = A.count ? (int64_t)__builtin_amdgcn_readfirstlane(*A.count) : A.B;
     const int64_t ntiles = nact * A.tpf;
     const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
-    auto frame_of = [&](int64_t slot) -> int64_t { return A.list ? (int64_t)A.list[slot] : slot; };
     // frame / in-frame tile counters, advanced without divisions
     const int64_t sb = tw.stride / A.tpf, sk = tw.stride - sb * A.tpf;
-    int64_t fb = tw.first / A.tpf, fk = tw.first - fb * A.tpf;
+    const int64_t fb = tw.first / A.tpf, fk = tw.first - fb * A.tpf;
+    auto next = [&](TilePos p) {
+        p.t += tw.stride;
+        p.b += sb;
+        p.k += sk;
+        if (p.k >= A.tpf) { p.k -= A.tpf; ++p.b; }
+        return p;
+    };
 
-    // this lane's tile slot: {var group, check group, type, variable}, {message, check mask}
-    auto load_info = [&](int64_t k) {
-        SlotIn s;
-        s.inf = A.info[k * 32 + j];
-        s.sl = A.slot[k * 32 + j];
-        return s;
+    // Everything below is branch-free per lane: a load in one arm of a branch whose other arm
+    // writes the same registers makes the compiler wait for the load at the join, and then the
+    // next tile's rows are no longer in flight while this tile computes.
+    // Tile p's slot info, frame (list entry) and still-decoding flag, fetched two tiles ahead.
+    auto ctl_of = [&](const TilePos &p) {
+        TileCtl c;
+        c.inf = A.info[p.k * 32 + j];
+        c.sl = A.slot[p.k * 32 + j];
+        const int64_t slot = p.t < tw.end ? p.b : fb;  // past the end: any valid frame
+        const int32_t *lp = A.list ? A.list + slot : reinterpret_cast<const int32_t *>(A.slot);
+        const int64_t lv = *lp;
+        c.frame = A.list ? lv : slot;
+        const bool chk = A.active && !A.list;  // listed frames are active by construction
+        const uint8_t *ap = chk ? A.active + c.frame : reinterpret_cast<const uint8_t *>(A.slot);
+        const uint8_t av = *ap;
+        c.on = !chk || av != 0;
+        return c;
     };
-    // the frame's "still decoding" flag of tile t (frame b), read ahead of the tile's row loads
-    auto load_on = [&](int64_t t, int64_t b) -> bool {
-        return A.list || !A.active || A.active[t < tw.end ? b : fb];  // listed frames are active
-    };
-    auto load = [&](const SlotIn &si, bool on, int64_t t, int64_t b, int64_t k) {
+    auto load = [&](const TileCtl &c, const TilePos &p) {
         TileIn I;
-        const int4 inf = si.inf;
-        I.ok = si.sl.x >= 0 && t < tw.end;
-        const int m = si.sl.x >= 0 ? si.sl.x : ~si.sl.x;
-        const int64_t bb = frame_of(t < tw.end ? b : fb);
+        const int4 inf = c.inf;
+        I.ok = c.sl.x >= 0 && p.t < tw.end;
+        const int m = c.sl.x >= 0 ? c.sl.x : ~c.sl.x;
+        const int64_t bb = c.frame;
         I.ty = inf.z;
         I.var = inf.w;
         I.one = !layer0 && A.d1 && inf.x < 0;
         I.row = bb * A.E + m;
         I.b = bb;
-        I.on = on;
+        I.on = c.on;
         // A terminated frame (uniform over the tile) loads frame 0's rows instead of its own:
-        // L2 hits, and no branch around the loads -- a branch here makes the compiler wait for
-        // the prefetched rows at the join, which costs ~10 % of the kernel.
+        // L2 hits, and no branch around the loads.
         const int64_t lb = I.on ? bb : 0;
         const int vg = inf.x < 0 ? ~inf.x : inf.x;
-        const char *ma = reinterpret_cast<const char *>(A.Mv + (lb * A.Gv + vg) * H) + 16 * h;
-        const char *mc = reinterpret_cast<const char *>(A.Mc + (lb * A.Gc + inf.y) * H) + 16 * h;
+        const char *mv = reinterpret_cast<const char *>(A.Mv + (lb * A.Gv + vg) * H) + 16 * h;
         if constexpr (!layer0) {
             const char *xr = reinterpret_cast<const char *>(A.x_in + (lb * A.E + m) * H) + 16 * h;
+            // a degree-1 var group's g is x itself (its emb part is in D1): the same rows again
+            const char *ma = I.one ? xr : mv;
 #pragma unroll
             for (int s = 0; s < 4; ++s) I.xf[s] = ld8(xr + 32 * s);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
             I.l = 0.0f;
         } else {
             I.l = A.llr[lb * A.N + I.var];
-        }
-        if (layer0 || !A.d1 || inf.x >= 0) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s) I.af[s] = ld8(ma + 32 * s);
-        } else {  // degree-1 var group: g = x, its emb part is in D1
-#pragma unroll
-            for (int s = 0; s < 4; ++s) I.af[s] = I.xf[s];
+            for (int s = 0; s < 4; ++s) I.af[s] = ld8(mv + 32 * s);
         }
         if constexpr (itc) {
-            I.cmask = (uint32_t)si.sl.y;
+            I.cmask = (uint32_t)c.sl.y;
             I.cinv = A.inv_c[inf.y];
-            const float *mbr = A.memb_c + (int64_t)inf.y * H + 8 * h;
+            const char *mbr = reinterpret_cast<const char *>(A.memb_c + (int64_t)inf.y * H) + 16 * h;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const float4 u = *reinterpret_cast<const float4 *>(mbr + 16 * s);
-                const float4 v = *reinterpret_cast<const float4 *>(mbr + 16 * s + 4);
-                I.mb[8 * s] = u.x; I.mb[8 * s + 1] = u.y; I.mb[8 * s + 2] = u.z; I.mb[8 * s + 3] = u.w;
-                I.mb[8 * s + 4] = v.x; I.mb[8 * s + 5] = v.y; I.mb[8 * s + 6] = v.z; I.mb[8 * s + 7] = v.w;
-            }
+            for (int s = 0; s < 4; ++s) I.mb[s] = ld8(mbr + 32 * s);
         } else {
+            const char *mc = reinterpret_cast<const char *>(A.Mc + (lb * A.Gc + inf.y) * H) + 16 * h;
 #pragma unroll
             for (int s = 0; s < 4; ++s) I.cf[s] = ld8(mc + 32 * s);
         }
@@ -492,7 +512,7 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
         for (int s = 0; s < 4; ++s) {
             bf16x8 o;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] = (__bf16)fmaf(sum[s >> 1][8 * (s & 1) + i], I.cinv, I.mb[8 * s + i]);
+            for (int i = 0; i < 8; ++i) o[i] = (__bf16)fmaf(sum[s >> 1][8 * (s & 1) + i], I.cinv, (float)I.mb[s][i]);
             I.cf[s] = o;
         }
     };
@@ -566,7 +586,7 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
                 part = fmaf(y1[r], wo[32 + 16 * h + r], part);
             }
             part += __shfl_xor(part, 32, 64);
-            if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo[0];
+            if (I.ok && h == 0) A.msg_out[I.row] = part + bo_out;
         } else {
             if (A.kd_last) {  // early termination: project with the last layer's output head
                 const float *wo = tail + 128;
@@ -577,7 +597,7 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
                     part = fmaf(y1[r], wo[32 + 16 * h + r], part);
                 }
                 part += __shfl_xor(part, 32, 64);
-                if (I.ok && h == 0) A.msg_out[I.row] = part + A.bo_last[0];
+                if (I.ok && h == 0) A.msg_out[I.row] = part + bo_out;
             }
             if (!I.ok) return;
             char *xo = reinterpret_cast<char *>(A.x_out + I.row * H) + 16 * h;
@@ -589,27 +609,24 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_bf16_mlp_kernel(MlpArgs A)
     };
 
     if (tw.first >= tw.end) return;
-    {
-        // rows are prefetched one tile ahead; the small per-tile items (message info, frame
-        // flag) two tiles ahead, so the row loads never wait behind an index load
-        TileIn cur = load(load_info(fk), load_on(tw.first, fb), tw.first, fb, fk);
-        int64_t nb = fb + sb, nk = fk + sk;
-        if (nk >= A.tpf) { nk -= A.tpf; ++nb; }
-        SlotIn inf_n = load_info(nk);
-        bool on_n = load_on(tw.first + tw.stride, nb);
-        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-            int64_t nb2 = nb + sb, nk2 = nk + sk;
-            if (nk2 >= A.tpf) { nk2 -= A.tpf; ++nb2; }
-            const SlotIn inf_nn = load_info(nk2);
-            const bool on_nn = load_on(t + 2 * tw.stride, nb2);
-            const TileIn nxt = load(inf_n, on_n, t + tw.stride, nb, nk);
-            compute(cur);
-            cur = nxt;
-            inf_n = inf_nn;
-            on_n = on_nn;
-            nb = nb2;
-            nk = nk2;
-        }
+    // rows one tile ahead, the per-tile items two tiles ahead; unrolled by two so that the tile
+    // in flight lives in its own registers (no copies that would wait for its loads)
+    TilePos p0{tw.first, fb, fk};
+    TilePos p1 = next(p0);
+    TileIn ta = load(ctl_of(p0), p0), tb;
+    TileCtl c1 = ctl_of(p1);
+    for (;;) {
+        const TilePos p2 = next(p1);
+        const TileCtl c2 = ctl_of(p2);
+        tb = load(c1, p1);
+        compute(ta);
+        if (p1.t >= tw.end) break;
+        const TilePos p3 = next(p2);
+        c1 = ctl_of(p3);
+        ta = load(c2, p2);
+        compute(tb);
+        if (p2.t >= tw.end) break;
+        p1 = p3;
     }
 }
 
@@ -696,6 +713,7 @@ __global__ void fill_i32_kernel(int32_t *p, int64_t n, int32_t v) {
 
 struct Bf16Ws {
     float *kd, *memb, *msg_out;
+    __bf16 *memb16;
     int32_t *csr, *alist, *acount, *cg_var;
     int4 *info;
     int2 *slot;
@@ -706,7 +724,7 @@ struct Bf16Ws {
 
 Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *base) {
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
-    const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4);
+    const int64_t kd = al(L * kd_floats(T) * 4), memb = al((int64_t)L * (p->Gv + p->Gc) * H * 4) * 3 / 2;
     const int64_t xa = L > 1 ? al(B * p->E * H * 2) : 0, xb = L > 2 ? xa : 0;
     const int64_t mv = al(B * p->Gv * H * 2), mc = al(B * p->Gc * H * 2), vs = al(B * p->E * 4);
     const int64_t nslot = (int64_t)p->n_ctiles * 32;
@@ -720,6 +738,7 @@ Bf16Ws carve_bf16(const ldpc_gnn_plan *p, int N, int64_t B, int T, int L, void *
     w.csr = reinterpret_cast<int32_t *>(c + kd + memb + xa + xb + mv + mc + vs + inf + act);
     w.kd = reinterpret_cast<float *>(c);
     w.memb = reinterpret_cast<float *>(c + kd);
+    w.memb16 = reinterpret_cast<__bf16 *>(c + kd + al((int64_t)L * (p->Gv + p->Gc) * H * 4));
     w.xa = reinterpret_cast<__bf16 *>(c + kd + memb);
     w.xb = reinterpret_cast<__bf16 *>(c + kd + memb + xa);
     w.Mv = reinterpret_cast<__bf16 *>(c + kd + memb + xa + xb);
@@ -826,7 +845,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
     hipLaunchKernelGGL(gnn_bf16_kconst_kernel, dim3(L, T + 2), dim3(128), 0, s, d_weights, T, w.kd);
     LDPC_CHECK_LAUNCH("gnn_bf16_kconst_kernel");
     hipLaunchKernelGGL(gnn_bf16_memb_kernel, dim3((unsigned)(((int64_t)L * p->n_gtiles + 3) / 4)), dim3(256), 0, s,
-                       d_weights, T, L, d_msg_type, G, Gtot, w.memb);
+                       d_weights, T, L, d_msg_type, G, Gtot, w.memb, w.memb16);
     LDPC_CHECK_LAUNCH("gnn_bf16_memb_kernel");
     if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
     if (d_iters) {
@@ -895,7 +914,7 @@ int gnn_bf16_forward(const ldpc_gnn_plan *p, int T, int L, const float *d_weight
         m.info = w.info;
         m.slot = w.slot;
         m.inv_c = p->inv_c;
-        m.memb_c = w.memb + ((int64_t)l * Gtot + p->Gv) * H;
+        m.memb_c = w.memb16 + ((int64_t)l * Gtot + p->Gv) * H;
         m.llr = d_llr + b0 * N;
         m.w1v = lw.w1v;
         m.w1c = lw.w1c;
