@@ -116,6 +116,11 @@ struct GnnLayer {
     // training backward (gnn_project_groups): the projection kernel also writes the group means
     // it projects, (B, Gv, H) / (B, Gc, H)
     float *gsave_v = nullptr, *gsave_c = nullptr;
+    // gnn_mlp2s_kernel message tiles in the plan's order (gnn.hpp mt_perm: degree-1 var groups'
+    // messages first): tperm[32 k + j] = message of slot j of a frame's tile k (-1 = padding), its
+    // first ntile_v1 tiles hold degree-1 messages only.  Null: tiles of 32 consecutive messages.
+    const int32_t *tperm = nullptr;
+    int ntile_pf = 0, ntile_v1 = 0;
 };
 __device__ __forceinline__ float4 hyb_x(float4 f, float v, float4 w, float4 c) {
     return make_float4((v * w.x + c.x) + f.x, (v * w.y + c.y) + f.y, (v * w.z + c.z) + f.z, (v * w.w + c.w) + f.w);
@@ -792,11 +797,15 @@ constexpr int kS6OffW2 = 6 * kS6Img;                               // W1L (side,
 constexpr int kS6Bytes = 12 * kS6Img * 2;                          // 12 images
 constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo
 constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][kPS]
-inline size_t mlp2s_lds_bytes(int T) { return (size_t)(kS6OffEmb + T * kPS) * 4; }
+// then, with degree-1 tiles (GnnLayer tperm), the three split images of W1v_left + W1v_right
+__host__ __device__ inline int s6_off_d1(int T) { return ((kS6OffEmb + T * kPS) * 4 + 15) / 16 * 16; }
+inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d1 ? 3 * kS6Img * 2 : 0); }
 
-// PF (LDPC_MLP2S_PF=1 builds, with 2 waves per SIMD): the next tile's feature rows are loaded
-// while the current tile computes (32 more VGPRs); layer 0 and the hybrid decoder's rows are not
-template <int NT, int WPS, bool HYB = false, bool PF = false>
+// Degree-1 tiles (tperm set, var side): a degree-1 var group's mean is the message's own c, so
+// W1v [c; g] = (W1v_left + W1v_right) c -- one fp32 sum per weight, rounded once and split like the
+// other weights -- and GEMM1 starts from b1v instead of a projected row, which the projection
+// kernel then does not write for those groups (ProjTiles first = n_ptiles_v1).
+template <int NT, int WPS, bool HYB = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __bf16 *img = reinterpret_cast<__bf16 *>(lds);
@@ -808,6 +817,12 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         for (int q = 0; q < 4; ++q)  // q: W1v, W1c, W2v, W2c -> images 3q .. 3q + 2
             split_store(w[q], img + 3 * q * kS6Img + o * kS6Row + p, kS6Img);
     }
+    __bf16 *img_d1 = reinterpret_cast<__bf16 *>(reinterpret_cast<char *>(lds) + s6_off_d1(P.T));
+    if (P.tperm && P.vside)
+        for (int i = tid; i < 64 * 64; i += NT) {
+            const int o = i >> 6, p = i & 63, u = pi16(p);
+            split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_d1 + o * kS6Row + p, kS6Img);
+        }
     if (tid < 64) {
         lds[kS6OffB + tid] = P.vside ? P.b2v[tid] : 0.0f;
         lds[kS6OffB + 64 + tid] = P.b2c[tid];
@@ -820,38 +835,32 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
     const int64_t R = P.B * P.E;
-    const int64_t ntiles = (R + 31) / 32;
+    const int64_t tpf = P.tperm ? P.ntile_pf : 1;
+    const int64_t ntiles = P.tperm ? P.B * tpf : (R + 31) / 32;
     const float bo = P.last ? P.bo[0] : 0.0f;
     const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
     const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
-    constexpr bool pf = PF && !HYB;
-    auto load_x = [&](int64_t t, float (&xo)[4][8]) {
-        const int64_t row = t * 32 + j;
-        const float *xr = P.x_in + (row < R ? row : R - 1) * 64 + 4 * half;
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const float4 v = *reinterpret_cast<const float4 *>(xr + 32 * (s >> 1) + 16 * (s & 1) + 8 * q);
-                xo[s][4 * q] = v.x; xo[s][4 * q + 1] = v.y; xo[s][4 * q + 2] = v.z; xo[s][4 * q + 3] = v.w;
-            }
-    };
-    float xnext[4][8];
-    if (pf && P.x_in && tw.first < tw.end) load_x(tw.first, xnext);
     for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-        const int64_t row = t * 32 + j;
-        const bool ok = row < R;
-        const int64_t rr = ok ? row : R - 1;
-        const int64_t b = rr / P.E, m = rr - b * P.E;
+        int64_t rr, b, m;
+        bool ok, d1t = false;
+        if (P.tperm) {  // slot j of the frame's tile k (padding: the tile's first message, not written)
+            b = t / tpf;
+            const int64_t k = t - b * tpf;
+            const int32_t mm = P.tperm[k * 32 + j];
+            ok = mm >= 0;
+            m = ok ? mm : P.tperm[k * 32];
+            rr = b * P.E + m;
+            d1t = k < P.ntile_v1;
+        } else {
+            const int64_t row = t * 32 + j;
+            ok = row < R;
+            rr = ok ? row : R - 1;
+            b = rr / P.E;
+            m = rr - b * P.E;
+        }
         // x[s][i] = feature pi16(16 s + 8 h + i) before the type embedding (float4 pairs)
         float x[4][8];
-        if (pf && P.x_in) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int i = 0; i < 8; ++i) x[s][i] = xnext[s][i];
-            if (t + tw.stride < tw.end) load_x(t + tw.stride, xnext);
-        } else if (P.x_in) {
+        if (P.x_in) {
             const float *xr = P.x_in + rr * 64 + 4 * half;
             const float hv = HYB && P.hv2c ? P.hv2c[rr] : 0.0f;
 #pragma unroll
@@ -877,7 +886,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 }
         }
         const float *e = lds + kS6OffEmb + P.msg_type[m] * kPS;
-        const float *pv = P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
+        // a degree-1 tile's var side starts from b1v (its group half is in the combined W1v image)
+        const float *pv = d1t ? P.b1v + 4 * half : P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
         const float *pc = P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
         f32x16 y0 = {}, y1 = {};
 #pragma unroll
@@ -892,7 +902,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 h0[4 * q] = a.x; h0[4 * q + 1] = a.y; h0[4 * q + 2] = a.z; h0[4 * q + 3] = a.w;
                 h1[4 * q] = c.x; h1[4 * q + 1] = c.y; h1[4 * q + 2] = c.z; h1[4 * q + 3] = c.w;
             }
-            const __bf16 *W1 = img + 3 * side * kS6Img + abase, *W2 = img + kS6OffW2 + 3 * side * kS6Img + abase;
+            const __bf16 *W1 = (side == 0 && d1t ? img_d1 : img + 3 * side * kS6Img) + abase;
+            const __bf16 *W2 = img + kS6OffW2 + 3 * side * kS6Img + abase;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {  // GEMM1: h += W1_left c, c = x + emb[type]
                 float c[8];
@@ -936,7 +947,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) part += vv[i] * wo[o0 + i];
                 }
-                if (ok && P.x_out) *reinterpret_cast<float4 *>(P.x_out + row * 64 + o0) = v;
+                if (ok && P.x_out) *reinterpret_cast<float4 *>(P.x_out + rr * 64 + o0) = v;
             }
         }
         if (P.last) {
@@ -1162,9 +1173,6 @@ constexpr int kMlp2Wps = LDPC_MLP2_WPS, kMlp2Nt = LDPC_MLP2_NT;
 #endif
 #ifndef LDPC_MLP2S_NT
 #define LDPC_MLP2S_NT 768
-#endif
-#ifndef LDPC_MLP2S_PF
-#define LDPC_MLP2S_PF 0
 #endif
 constexpr int kMlp2sWps = LDPC_MLP2S_WPS, kMlp2sNt = LDPC_MLP2S_NT;
 // LDPC_GNN_SPLIT=0: the projected-group MLP on v_mfma_f32_32x32x2_f32 (gnn_mlp2_kernel); default:
@@ -1577,9 +1585,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     // projection workgroups of 12 waves (one LDS weight image for 12 waves' gathers) when the
     // type table leaves room, else 4
     const int proj_nt = LDPC_PROJ_NT != 256 && proj_lds_bytes(types, LDPC_PROJ_NT / 64) <= 160 * 1024 ? LDPC_PROJ_NT : 256;
-    const bool split = split_path() && mlp2s_lds_bytes(types) <= 160 * 1024;
+    const bool split = split_path() && mlp2s_lds_bytes(types, false) <= 160 * 1024;
+    // degree-1 message tiles first (gnn_mlp2s_kernel) when the combined image fits
+    const bool d1t = split && p->n_mtiles_v1 > 0 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
-                 mlp2_lds = split ? mlp2s_lds_bytes(types) : mlp2_lds_bytes(types);
+                 mlp2_lds = split ? mlp2s_lds_bytes(types, d1t) : mlp2_lds_bytes(types);
     const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
     int mlp2_per_cu = 1, proj_per_cu = 1;
@@ -1591,7 +1601,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
-        LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, LDPC_MLP2S_PF != 0>)
+        LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>)
                                            : reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
     }
@@ -1628,7 +1638,12 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.d1 = H == 64 && gm_tiles() && d1_skip() && !p->weighted;
         if (proj) {
             L.d1 = 0;
-            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, 0};
+            if (d1t) {
+                L.tperm = p->mt_perm;
+                L.ntile_pf = p->n_mtiles;
+                L.ntile_v1 = p->n_mtiles_v1;
+            }
+            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, d1t ? p->n_ptiles_v1 : 0};
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;
             const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
@@ -1637,11 +1652,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             else
                 hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds, st, L, T);
             LDPC_CHECK_LAUNCH("gnn_group_proj_kernel");
-            const int64_t tiles = (nb * p->E + 31) / 32;
+            const int64_t tiles = d1t ? nb * p->n_mtiles : (nb * p->E + 31) / 32;
             constexpr int wpb = kMlp2Nt / 64;
             const unsigned grid = (unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu);
             if (split)
-                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, LDPC_MLP2S_PF != 0>),
+                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>),
                                    dim3((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus)),
                                    dim3(kMlp2sNt), mlp2_lds, st, L);
             else
@@ -1819,8 +1834,8 @@ extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, i
         LDPC_HIP(hipGetDevice(&dev));
         LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    const bool split = split_path() && mlp2s_lds_bytes(types) <= 160 * 1024;
-    const size_t proj_lds = proj_lds_bytes(types, 4), mlp2_lds = split ? mlp2s_lds_bytes(types) : mlp2_lds_bytes(types);
+    const bool split = split_path() && mlp2s_lds_bytes(types, false) <= 160 * 1024;
+    const size_t proj_lds = proj_lds_bytes(types, 4), mlp2_lds = split ? mlp2s_lds_bytes(types, false) : mlp2_lds_bytes(types);
     if (proj_lds > 160 * 1024 || mlp2_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_group_proj_kernel<256, true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));

@@ -804,15 +804,48 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
             }
     };
     if constexpr (H64 && NJT >= LDPC_OUTER_PIPE_MIN_NJT) {
-        // software-pipelined: the next batch's rows load while this batch's MFMAs run
+        // software-pipelined: the next batch's rows load while this batch's MFMAs run.  Branch-free
+        // loads (rows clamped to the range, the rows past it zeroed at use) and two batch buffers
+        // used alternately: a load under a branch, or a batch copied register to register, makes
+        // the compiler wait for the next batch's loads before this batch's MFMAs.
         if (r_begin < r_end) {
-            Batch cur;
-            load_batch(r_begin, cur);
-            for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * KU) {
-                Batch nxt;
-                if (r0 + 2 * KU < r_end) load_batch(r0 + 2 * KU, nxt);
-                mfma_batch(cur);
-                cur = nxt;
+            const int64_t rlast = r_end - 1;
+            auto load_h = [&](int64_t r0, Batch &B) {
+#pragma unroll
+                for (int u = 0; u < KU; ++u) {
+                    const int64_t r = r0 + 2 * u + k < rlast ? r0 + 2 * u + k : rlast;
+#pragma unroll
+                    for (int it = 0; it < NIT; ++it) B.a[u][it] = P.A[r * 64 + 32 * it + col];
+#pragma unroll
+                    for (int jt = 0; jt < NJT; ++jt) B.z[u][jt] = zval(r, 0, 0, 32 * jt + col);
+                }
+            };
+            auto mfma_h = [&](int64_t r0, const Batch &B) {
+#pragma unroll
+                for (int u = 0; u < KU; ++u) {
+                    const bool ok = r0 + 2 * u + k < r_end;
+#pragma unroll
+                    for (int it = 0; it < NIT; ++it) {
+                        const float a = ok ? B.a[u][it] : 0.0f;
+                        bsum[it] += a;
+#pragma unroll
+                        for (int jt = 0; jt < NJT; ++jt)
+                            acc[it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, B.z[u][jt], acc[it][jt], 0, 0, 0);
+                    }
+                }
+            };
+            Batch b0, b1;
+            load_h(r_begin, b0);
+            // (sched_barrier: the scheduler would otherwise sink each load next to its first use)
+            for (int64_t r0 = r_begin;;) {
+                load_h(r0 + 2 * KU, b1);
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_h(r0, b0);
+                if ((r0 += 2 * KU) >= r_end) break;
+                load_h(r0 + 2 * KU, b0);
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_h(r0, b1);
+                if ((r0 += 2 * KU) >= r_end) break;
             }
         }
     } else {
@@ -857,7 +890,7 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
 // splits on v_mfma_f32_32x32x16_bf16 (gnn.hpp split3): K = 16 rows per MFMA step, lane (i, half)
 // holding rows r0 + 8 half .. + 7 of column 32 it + i (A) / 32 jt + i (Z); 6 x 32 instead of
 // 8 x 64 MFMA cycles per 16 rows.  Same reduction epilogue as train_outer_mfma_kernel.
-__global__ __launch_bounds__(256, 2) void train_outer_split_kernel(OuterT P) {
+__global__ __launch_bounds__(256, 1) void train_outer_split_kernel(OuterT P) {
     constexpr int NIT = 2, NJT = 4;
     const int lane = threadIdx.x & 63, col = lane & 31, hf = lane >> 5;
     const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -870,25 +903,31 @@ __global__ __launch_bounds__(256, 2) void train_outer_split_kernel(OuterT P) {
         for (int jt = 0; jt < NJT; ++jt) acc[it][jt] = f32x16{};
     float bsum[NIT] = {};
     struct Step { float a[NIT][8], z[NJT][8]; };
+    // branch-free loads (rows clamped, the rows past the range zeroed at use) into two alternating
+    // buffers, so the next step's loads stay in flight across this step's MFMAs (as above)
+    const int64_t rlast = r_end - 1;
     auto load = [&](int64_t r0, Step &S) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const int64_t r = r0 + 8 * hf + q;
-            const bool ok = r < r_end;
+            const int64_t r = r0 + 8 * hf + q < rlast ? r0 + 8 * hf + q : rlast;
 #pragma unroll
-            for (int it = 0; it < NIT; ++it) S.a[it][q] = ok ? P.A[r * 64 + 32 * it + col] : 0.0f;
+            for (int it = 0; it < NIT; ++it) S.a[it][q] = P.A[r * 64 + 32 * it + col];
 #pragma unroll
             for (int jt = 0; jt < NJT; ++jt)
-                S.z[jt][q] = ok ? (jt < 2 ? P.zsrc[r * 64 + 32 * jt + col] : P.zsrc2[r * 64 + 32 * (jt - 2) + col]) : 0.0f;
+                S.z[jt][q] = jt < 2 ? P.zsrc[r * 64 + 32 * jt + col] : P.zsrc2[r * 64 + 32 * (jt - 2) + col];
         }
     };
-    auto step = [&](const Step &S) {
+    auto step = [&](int64_t r0, const Step &S) {
         bf16x8_t as[NIT][3];
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
+            float a[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) bsum[it] += S.a[it][q];
-            split3(S.a[it], as[it][0], as[it][1], as[it][2]);
+            for (int q = 0; q < 8; ++q) {
+                a[q] = r0 + 8 * hf + q < r_end ? S.a[it][q] : 0.0f;
+                bsum[it] += a[q];
+            }
+            split3(a, as[it][0], as[it][1], as[it][2]);
         }
 #pragma unroll
         for (int jt = 0; jt < NJT; ++jt) {  // one column tile's Z split live at a time
@@ -907,13 +946,17 @@ __global__ __launch_bounds__(256, 2) void train_outer_split_kernel(OuterT P) {
         }
     };
     if (r_begin < r_end) {
-        Step cur;
-        load(r_begin, cur);
-        for (int64_t r0 = r_begin; r0 < r_end; r0 += 16) {
-            Step nxt;
-            if (r0 + 16 < r_end) load(r0 + 16, nxt);
-            step(cur);
-            cur = nxt;
+        Step s0, s1;
+        load(r_begin, s0);
+        for (int64_t r0 = r_begin;;) {
+            load(r0 + 16, s1);
+            __builtin_amdgcn_sched_barrier(0);
+            step(r0, s0);
+            if ((r0 += 16) >= r_end) break;
+            load(r0 + 16, s0);
+            __builtin_amdgcn_sched_barrier(0);
+            step(r0, s1);
+            if ((r0 += 16) >= r_end) break;
         }
     }
     // D[i][j]: register q of lane l holds i = 8 (q >> 2) + 4 hf + (q & 3), j = col (as the fp32 kernel)
@@ -941,6 +984,13 @@ __global__ __launch_bounds__(256, 2) void train_outer_split_kernel(OuterT P) {
     }
     if (P.bias && threadIdx.x < 64) atomicAdd(&P.bias[threadIdx.x], bred[threadIdx.x]);
     if (P.bias2 && threadIdx.x < 64) atomicAdd(&P.bias2[threadIdx.x], bred[threadIdx.x]);
+}
+
+// workgroups per CU of the weight-gradient reductions (LDPC_GNN_OUTER_WGS, default 4); read per call
+int outer_wgs() {
+    const char *e = std::getenv("LDPC_GNN_OUTER_WGS");
+    const int v = e ? std::atoi(e) : 4;
+    return v >= 1 && v <= 16 ? v : 4;
 }
 
 // LDPC_GNN_OUTER_SPLIT=0: dW2 on the fp32 MFMA (train_outer_mfma_kernel<2, 4, true>); read per call
@@ -1188,7 +1238,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     }
     auto blocks = [](int64_t work, int per) { return dim3((unsigned)((work + per - 1) / per)); };
-    const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * 4);
+    const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * outer_wgs());
 
     // head: dz, dX_L, dwo, dbo
     const float *WL[11];
