@@ -578,44 +578,54 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
 
 // PJ backward: the group part of dz averaged over a group, formed per group --
 // Mda[b][g][k] = inv[g] sum_u W1v[u][64 + k] S_v[b][g][u] with S the group sums of dh (Mdb: the
-// check side with W1c).  One wave per 4 rows of a side, lanes = k, W1_right in LDS.
+// check side with W1c).  32-row tiles of a side on v_mfma_f32_32x32x2_f32, C[row][k] =
+// sum_u S[row][u] W1_right[u][k]: the A fragment of step s is S[row j][32 half + s] (each lane
+// reads 128 contiguous bytes of its row), the B fragments W1_right[32 half + s][32 kt + j] stay in
+// registers for the whole side.  (A lane-per-unit VALU form with readlane broadcasts ran at
+// 1.3 TB/s: half-rate SGPR-operand FMAs.)
 __global__ __launch_bounds__(256) void train_group_back_kernel(const float *__restrict__ Sv, const float *__restrict__ Sc,
                                                                const float *__restrict__ w1v, const float *__restrict__ w1c,
                                                                const float *__restrict__ inv_v,
                                                                const float *__restrict__ inv_c, int Gv, int Gc, int64_t B,
                                                                float *__restrict__ Mda, float *__restrict__ Mdb) {
-    __shared__ float W[2 * 64 * 64];
-    for (int i = threadIdx.x; i < 2 * 4096; i += 256) {
-        const int side = i >> 12, u = (i >> 6) & 63, k = i & 63;
-        W[i] = (side ? w1c : w1v)[u * 128 + 64 + k];
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    const int lane = threadIdx.x & 63, j = lane & 31, half = lane >> 5, wave = threadIdx.x >> 6;
     for (int side = 0; side < 2; ++side) {
         const int G = side ? Gc : Gv;
-        const int64_t rows = B * G, quads = (rows + 3) / 4;
-        const float *S = side ? Sc : Sv, *inv = side ? inv_c : inv_v;
+        const int64_t rows = B * G;
+        const float *S = side ? Sc : Sv, *inv = side ? inv_c : inv_v, *w1 = side ? w1c : w1v;
         float *out = side ? Mdb : Mda;
-        const float *Ws = W + side * 4096 + lane;
-        for (int64_t q = wave; q < quads; q += nw) {
-            int sv[4];
-            float acc[4] = {};
+        float wr[2][32];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = 4 * q + r;
-                sv[r] = __float_as_int(row < rows ? S[row * 64 + lane] : 0.0f);
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int s = 0; s < 32; ++s) wr[kt][s] = w1[(32 * half + s) * 128 + 64 + 32 * kt + j];
+        const TileWalk tw = xcd_tiles((rows + 31) / 32, 4, wave);
+        for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+            const int64_t ra = t * 32 + j < rows ? t * 32 + j : rows - 1;
+            float a[32];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const float4 v = *reinterpret_cast<const float4 *>(S + ra * 64 + 32 * half + 4 * q);
+                a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
             }
-#pragma unroll 8
-            for (int u = 0; u < 64; ++u) {
-                const float w = Ws[u * 64];
+            f32x16 c0 = {}, c1 = {};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[r] = fmaf(w, __int_as_float(__builtin_amdgcn_readlane(sv[r], u)), acc[r]);
+            for (int s = 0; s < 32; ++s) {
+                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], wr[0][s], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], wr[1][s], c1, 0, 0, 0);
             }
+            // register r: row t * 32 + crow(r, half), unit j (+ 32)
+            int g0 = (int)((t * 32) % G);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = 4 * q + r;
-                if (row < rows) out[row * 64 + lane] = acc[r] * inv[row % G];
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = t * 32 + crow_t(r, half);
+                int g = g0 + crow_t(r, half);
+                while (g >= G) g -= G;
+                if (row < rows) {
+                    const float iv = inv[g];
+                    out[row * 64 + j] = c0[r] * iv;
+                    out[row * 64 + 32 + j] = c1[r] * iv;
+                }
             }
         }
     }
@@ -1367,8 +1377,8 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
                 gs.inv = side ? p->inv_c : p->inv_v; gs.G = side ? p->Gc : p->Gv; gs.dst = side ? Mc : Mv;
                 if (int rc = launch_group_mean(gs, s)) return rc;
             }
-            const int64_t quads = (B * p->Gv + 3) / 4 + (B * p->Gc + 3) / 4;
-            const unsigned ggrid = (unsigned)std::min<int64_t>((quads + 3) / 4, (int64_t)g_cus_t * 8);
+            const int64_t gtiles = (B * std::max(p->Gv, p->Gc) + 31) / 32;
+            const unsigned ggrid = (unsigned)std::min<int64_t>((gtiles + 3) / 4, (int64_t)g_cus_t * 4);
             hipLaunchKernelGGL(train_group_back_kernel, dim3(ggrid), dim3(256), 0, s, Mv, Mc, W[1], W[5], p->inv_v,
                                p->inv_c, p->Gv, p->Gc, B, w.Mda, w.Mdb);
             LDPC_CHECK_LAUNCH("train_group_back_kernel");

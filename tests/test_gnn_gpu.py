@@ -144,9 +144,13 @@ torch.save(p.detach().cpu(), sys.argv[3])
 
 
 def test_fp32_group_mean_variants_bit_identical(cuda, tmp_path):
-    """The group-tile group-mean kernel and the degree-1 skip (defaults) give the same probs,
-    bit for bit, as the per-group kernel with every Mv row written (LDPC_GNN_GM=0 LDPC_GNN_D1=0).
-    The knobs are read once per process, so the reference run is a child process."""
+    """Per-message [c; g] kernels (LDPC_GNN_PROJ=0): the group-tile group-mean kernel and the
+    degree-1 skip give the same probs, bit for bit, as the per-group kernel with every Mv row
+    written (LDPC_GNN_GM=0 LDPC_GNN_D1=0).  Default (projected) path: its degree-1 message tiles
+    (layer 0: one combined W1v_left + W1v_right weight, rounded once) and its in-tile check means
+    (layers >= 1) against projected group rows for every message (LDPC_GNN_D1=0, LDPC_GNN_ITC=0):
+    fp32 rounding apart, |dp| <= 1e-5.  The knobs are read once per
+    process, so each variant runs in a child process."""
     import os
     import subprocess
     import sys
@@ -161,8 +165,17 @@ def test_fp32_group_mean_variants_bit_identical(cuda, tmp_path):
             conv.var_to_check_adjacency, conv.check_to_var_adjacency).detach().cpu()
     pkg = os.path.dirname(os.path.dirname(os.path.abspath(
         sys.modules["ldpc_neural_decoder"].__file__)))
-    env = dict(os.environ, LDPC_GNN_GM="0", LDPC_GNN_D1="0")
-    subprocess.run([sys.executable, "-c", _KNOB_SCRIPT, pkg, str(tmp_path / "in.pt"),
-                    str(tmp_path / "out.pt")], env=env, check=True, timeout=180)
-    q = torch.load(tmp_path / "out.pt", weights_only=True)
-    assert torch.equal(p, q)
+    def child(name, **knobs):
+        env = dict(os.environ, **knobs)
+        subprocess.run([sys.executable, "-c", _KNOB_SCRIPT, pkg, str(tmp_path / "in.pt"),
+                        str(tmp_path / name)], env=env, check=True, timeout=180)
+        return torch.load(tmp_path / name, weights_only=True)
+
+    q_gm = child("gm.pt", LDPC_GNN_PROJ="0")
+    q_pergroup = child("pergroup.pt", LDPC_GNN_PROJ="0", LDPC_GNN_GM="0", LDPC_GNN_D1="0")
+    assert torch.equal(q_gm, q_pergroup)
+    for name, knobs in (("nod1.pt", {"LDPC_GNN_D1": "0"}), ("noitc.pt", {"LDPC_GNN_ITC": "0"}),
+                        ("neither.pt", {"LDPC_GNN_D1": "0", "LDPC_GNN_ITC": "0"})):
+        d = (p - child(name, **knobs)).abs().max().item()
+        print(f"projected path vs {knobs}: max |dp| {d:.2e}")
+        assert d <= 1e-5
