@@ -507,6 +507,7 @@ def main():
         # (two sides x (W1 over [c; g]: 4 H^2 + W2: 2 H^2)); W1's group half is applied once per group
         # (gnn.hip, gnn_group_proj_kernel), so 8 H^2 per message + 2 H^2 per var / check group
         fwd_flops = 8 * 64 * 64 * E + 2 * 64 * 64 * (g_n + g_m)
+        mlp_flops = 8 * 64 * 64 * E  # of which on the MLP kernel (bf16x6 splits)
         nominal_flops = 12 * 64 * 64 * E
         if kind == "hybrid-gnn":
             # check side only: 4 H^2 per message (W1 over c + W2) + 2 H^2 per check group (projection)
@@ -626,7 +627,7 @@ def main():
             if split:
                 # gnn_mlp2s_kernel: the per-message products (8 H^2 E) as six bf16 products each on the
                 # bf16 MFMA; the group projection (2 H^2 (N + M)) stays on the fp32 MFMA
-                mlp_bf16 = 6 * 8 * 64 * 64 * E * B * iters * reps
+                mlp_bf16 = 6 * mlp_flops * B * iters * reps
                 notes["mlp_products"] = ("bf16x6 split (fp32-accurate, tests/test_gnn_depth_gpu.py::"
                                          "test_split_mlp_is_fp32_accurate)")
                 notes["mlp_bf16_mfma_flops_per_launch"] = mlp_bf16

@@ -67,15 +67,6 @@ int mlp_threads() {
     }();
     return t;
 }
-// LDPC_GNN_ITC=0: the fp32 split MLP reads projected check-group rows on every layer (A/B runs);
-// default: check means in check-aligned tiles from layer 1 (gnn_mlp2s_kernel<ITC>)
-bool itc_path() {
-    static bool t = [] {
-        const char *e = std::getenv("LDPC_GNN_ITC");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return t;
-}
 // LDPC_GNN_D1=0 keeps the Mv rows of degree-1 var groups (A/B runs)
 bool d1_skip() {
     static bool t = [] {
@@ -130,11 +121,6 @@ struct GnnLayer {
     // first ntile_v1 tiles hold degree-1 messages only.  Null: tiles of 32 consecutive messages.
     const int32_t *tperm = nullptr;
     int ntile_pf = 0, ntile_v1 = 0;
-    // gnn_mlp2s_kernel<ITC>: check-aligned tiles (gnn.hpp ct_m0, ctpf per frame) whose check-group
-    // means are formed in the tile; memb_c = this layer's mean type embedding per check group
-    const int32_t *ct_m0 = nullptr;
-    int ctpf = 0;
-    const float *memb_c = nullptr;
 };
 __device__ __forceinline__ float4 hyb_x(float4 f, float v, float4 w, float4 c) {
     return make_float4((v * w.x + c.x) + f.x, (v * w.y + c.y) + f.y, (v * w.z + c.z) + f.z, (v * w.w + c.w) + f.w);
@@ -809,30 +795,17 @@ constexpr int kS6Row = 72;                                         // bf16 per i
 constexpr int kS6Img = 64 * kS6Row;                                // bf16 per split image
 constexpr int kS6OffW2 = 6 * kS6Img;                               // W1L (side, split), then W2
 constexpr int kS6Bytes = 12 * kS6Img * 2;                          // 12 images
-constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo, b1c
-constexpr int kS6OffEmb = kS6OffB + 4 * 64;                        // floats: emb [T][kPS]
-// then three more split images: W1v_left + W1v_right (degree-1 tiles) or W1c_right (ITC)
-__host__ __device__ inline int s6_off_x(int T) { return ((kS6OffEmb + T * kPS) * 4 + 15) / 16 * 16; }
-inline size_t mlp2s_lds_bytes(int T, bool extra) { return (size_t)s6_off_x(T) + (extra ? 3 * kS6Img * 2 : 0); }
+constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo
+constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][kPS]
+// then, with degree-1 tiles (GnnLayer tperm), the three split images of W1v_left + W1v_right
+__host__ __device__ inline int s6_off_d1(int T) { return ((kS6OffEmb + T * kPS) * 4 + 15) / 16 * 16; }
+inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d1 ? 3 * kS6Img * 2 : 0); }
 
 // Degree-1 tiles (tperm set, var side): a degree-1 var group's mean is the message's own c, so
 // W1v [c; g] = (W1v_left + W1v_right) c -- one fp32 sum per weight, rounded once and split like the
 // other weights -- and GEMM1 starts from b1v instead of a projected row, which the projection
 // kernel then does not write for those groups (ProjTiles first = n_ptiles_v1).
-//
-// ITC (layers >= 1 of a plan whose check groups are contiguous message runs of at most 32, the
-// reference's check-major order): the tiles are the plan's check-aligned ones (gnn.hpp ct_m0), so
-// each holds its messages' whole check groups, and the check side's group mean is formed here
-// from the tile's own rows instead of a projected group row (message_gnn_decoder.py:116-118):
-//   sum_c = X S  on v_mfma_f32_32x32x16_bf16 as three split products (X exact in three bf16 terms,
-//           S[k][j] = 1 when slots k and j share a check, exact): A = the tile's rows transposed,
-//           lane (unit i, half h) reading slot rows 8 h .. 8 h + 7 of each K = 16 step straight
-//           from global memory (the rows this tile has just read: L2 hits); the accumulator holds
-//           unit 32 rt + crow(r, h) of message j -- GEMM1's B-operand order, as h for GEMM2
-//   g = sum_c / |group| + the group's mean type embedding (memb_c)
-//   h_c = b1c + W1c_left c + W1c_right g   (GEMM1 over K = 128; W1c_right in the extra images)
-// The projection kernel then runs the var side only.  fp32 throughout, up to summation order.
-template <int NT, int WPS, bool HYB = false, bool ITC = false>
+template <int NT, int WPS, bool HYB = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __bf16 *img = reinterpret_cast<__bf16 *>(lds);
@@ -844,22 +817,16 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         for (int q = 0; q < 4; ++q)  // q: W1v, W1c, W2v, W2c -> images 3q .. 3q + 2
             split_store(w[q], img + 3 * q * kS6Img + o * kS6Row + p, kS6Img);
     }
-    __bf16 *img_x = reinterpret_cast<__bf16 *>(reinterpret_cast<char *>(lds) + s6_off_x(P.T));
-    if (ITC)
+    __bf16 *img_d1 = reinterpret_cast<__bf16 *>(reinterpret_cast<char *>(lds) + s6_off_d1(P.T));
+    if (P.tperm && P.vside)
         for (int i = tid; i < 64 * 64; i += NT) {
             const int o = i >> 6, p = i & 63, u = pi16(p);
-            split_store(P.w1c[o * 128 + 64 + u], img_x + o * kS6Row + p, kS6Img);
-        }
-    else if (P.tperm && P.vside)
-        for (int i = tid; i < 64 * 64; i += NT) {
-            const int o = i >> 6, p = i & 63, u = pi16(p);
-            split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_x + o * kS6Row + p, kS6Img);
+            split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_d1 + o * kS6Row + p, kS6Img);
         }
     if (tid < 64) {
         lds[kS6OffB + tid] = P.vside ? P.b2v[tid] : 0.0f;
         lds[kS6OffB + 64 + tid] = P.b2c[tid];
         lds[kS6OffB + 128 + tid] = P.last ? P.wo[tid] : 0.0f;
-        lds[kS6OffB + 192 + tid] = P.b1c[tid];
     }
     // emb rows kPS = 68 floats apart: lanes of different types read different rows (64 apart, every
     // row would sit on the same banks)
@@ -868,24 +835,15 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
     const int64_t R = P.B * P.E;
-    const int64_t tpf = ITC ? P.ctpf : P.tperm ? P.ntile_pf : 1;
-    const int64_t ntiles = ITC || P.tperm ? P.B * tpf : (R + 31) / 32;
+    const int64_t tpf = P.tperm ? P.ntile_pf : 1;
+    const int64_t ntiles = P.tperm ? P.B * tpf : (R + 31) / 32;
     const float bo = P.last ? P.bo[0] : 0.0f;
     const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
     const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
     for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
         int64_t rr, b, m;
         bool ok, d1t = false;
-        int m0 = 0, nm = 0;  // ITC: the tile's messages m0 .. m0 + nm - 1
-        if (ITC) {
-            b = t / tpf;
-            const int64_t k = t - b * tpf;
-            m0 = P.ct_m0[k];
-            nm = P.ct_m0[k + 1] - m0;
-            ok = j < nm;
-            m = m0 + (ok ? j : nm - 1);
-            rr = b * P.E + m;
-        } else if (P.tperm) {  // slot j of the frame's tile k (padding: the tile's first message, not written)
+        if (P.tperm) {  // slot j of the frame's tile k (padding: the tile's first message, not written)
             b = t / tpf;
             const int64_t k = t - b * tpf;
             const int32_t mm = P.tperm[k * 32 + j];
@@ -930,94 +888,21 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         const float *e = lds + kS6OffEmb + P.msg_type[m] * kPS;
         // a degree-1 tile's var side starts from b1v (its group half is in the combined W1v image)
         const float *pv = d1t ? P.b1v + 4 * half : P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
-        const float *pc = ITC ? pv : P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
+        const float *pc = P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
         f32x16 y0 = {}, y1 = {};
-        // ITC: the check side first, while y is still zero (no y registers live across its means)
 #pragma unroll
-        for (int sidx = 0; sidx < 2; ++sidx) {
-            const int side = ITC ? 1 - sidx : sidx;
+        for (int side = 0; side < 2; ++side) {
             if (side == 0 && !P.vside) continue;
-            const bool itc = ITC && side == 1;
-            // from the projected group row W1_right g + b1 (ITC check side: from b1c, + W1c_right g below)
-            const float *pr = itc ? lds + kS6OffB + 192 + 4 * half : side == 0 ? pv : pc;
-            f32x16 h0, h1;
-            auto init_h = [&]() {
+            const float *pr = side == 0 ? pv : pc;
+            f32x16 h0, h1;  // from the projected group row W1_right g + b1
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 a = *reinterpret_cast<const float4 *>(pr + 8 * q);
-                    const float4 c = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q);
-                    h0[4 * q] = a.x; h0[4 * q + 1] = a.y; h0[4 * q + 2] = a.z; h0[4 * q + 3] = a.w;
-                    h1[4 * q] = c.x; h1[4 * q + 1] = c.y; h1[4 * q + 2] = c.z; h1[4 * q + 3] = c.w;
-                }
-            };
-            if (!itc) init_h();
-            if constexpr (ITC) {
-                if (itc) {
-                    // the lane's check group as a mask of tile slots (a contiguous run)
-                    const int cg = P.cgroup[m];
-                    const int c0 = P.cg_ptr[cg], dg = P.cg_ptr[cg + 1] - c0;
-                    const uint32_t cmask = (dg >= 32 ? 0xFFFFFFFFu : ((1u << dg) - 1u)) << (P.cg_mem[c0] - m0);
-                    const float cinv = P.inv_c[cg];
-                    // A: unit 32 rt + j of slot rows 16 ks + 8 half + e (clamped to the tile's last
-                    // message: S never selects a padding slot)
-                    const float *xt = P.x_in + (b * P.E + m0) * 64 + j;
-                    float xa[2][2][8];
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                        for (int e8 = 0; e8 < 8; ++e8) {
-                            const int sl = 16 * ks + 8 * half + e8;
-                            const float *xs = xt + (int64_t)(sl < nm ? sl : nm - 1) * 64;
-#pragma unroll
-                            for (int rt = 0; rt < 2; ++rt) xa[ks][rt][e8] = xs[32 * rt];
-                        }
-                    f32x16 sum0 = {}, sum1 = {};
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks) {
-                        // B = S: element e of lane (j, half) is slot 16 ks + 8 half + e in j's check
-                        const uint32_t bits = (cmask >> (16 * ks + 8 * half)) & 0xFFu;
-                        bf16x8_t sop;
-#pragma unroll
-                        for (int e8 = 0; e8 < 8; ++e8) sop[e8] = (bits >> e8) & 1u ? (__bf16)1.0f : (__bf16)0.0f;
-#pragma unroll
-                        for (int rt = 0; rt < 2; ++rt) {
-                            bf16x8_t a0, a1, a2;
-                            split3(xa[ks][rt], a0, a1, a2);
-                            f32x16 sacc = rt ? sum1 : sum0;
-                            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, sop, sacc, 0, 0, 0);
-                            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, sop, sacc, 0, 0, 0);
-                            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, sop, sacc, 0, 0, 0);
-                            if (rt) sum1 = sacc; else sum0 = sacc;
-                        }
-                    }
-                    // g = sum / |group| + mean embedding; register 4 q + i of tile rt: unit 32 rt + 8 q + 4 half + i
-                    const float *mb = P.memb_c + (int64_t)cg * 64 + 4 * half;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 a = *reinterpret_cast<const float4 *>(mb + 8 * q);
-                        const float4 c = *reinterpret_cast<const float4 *>(mb + 32 + 8 * q);
-                        sum0[4 * q] = fmaf(sum0[4 * q], cinv, a.x); sum0[4 * q + 1] = fmaf(sum0[4 * q + 1], cinv, a.y);
-                        sum0[4 * q + 2] = fmaf(sum0[4 * q + 2], cinv, a.z); sum0[4 * q + 3] = fmaf(sum0[4 * q + 3], cinv, a.w);
-                        sum1[4 * q] = fmaf(sum1[4 * q], cinv, c.x); sum1[4 * q + 1] = fmaf(sum1[4 * q + 1], cinv, c.y);
-                        sum1[4 * q + 2] = fmaf(sum1[4 * q + 2], cinv, c.z); sum1[4 * q + 3] = fmaf(sum1[4 * q + 3], cinv, c.w);
-                    }
-                    // GEMM1's group half: h = b1c + W1c_right g (k-step s = registers 8 (s&1) .. of g_{s>>1})
-                    init_h();
-                    const __bf16 *WR = img_x + abase;
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        float gv[8];
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) gv[i] = s < 2 ? sum0[8 * (s & 1) + i] : sum1[8 * (s & 1) + i];
-                        bf16x8_t g0, g1, g2;
-                        split3(gv, g0, g1, g2);
-                        h0 = mfma6(WR + 16 * s, g0, g1, g2, h0, kS6Img);
-                        h1 = mfma6(WR + 32 * kS6Row + 16 * s, g0, g1, g2, h1, kS6Img);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
+            for (int q = 0; q < 4; ++q) {
+                const float4 a = *reinterpret_cast<const float4 *>(pr + 8 * q);
+                const float4 c = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q);
+                h0[4 * q] = a.x; h0[4 * q + 1] = a.y; h0[4 * q + 2] = a.z; h0[4 * q + 3] = a.w;
+                h1[4 * q] = c.x; h1[4 * q + 1] = c.y; h1[4 * q + 2] = c.z; h1[4 * q + 3] = c.w;
             }
-            const __bf16 *W1 = (side == 0 && d1t ? img_x : img + 3 * side * kS6Img) + abase;
+            const __bf16 *W1 = (side == 0 && d1t ? img_d1 : img + 3 * side * kS6Img) + abase;
             const __bf16 *W2 = img + kS6OffW2 + 3 * side * kS6Img + abase;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {  // GEMM1: h += W1_left c, c = x + emb[type]
@@ -1179,25 +1064,9 @@ __global__ void gnn_fill_kernel(int32_t *p, int64_t n, int32_t v) {
 
 int64_t layer_floats(int H, int T) { return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1; }
 
-// memb[l][g][u] = inv_c[g] * sum over check group g's members (ascending) of emb_l[type][u], H = 64
-// (gnn_mlp2s_kernel<ITC>: the embedding part of the in-tile check means)
-__global__ void gnn_memb_c_kernel(const float *__restrict__ emb0, int64_t lstride, int L, const int32_t *__restrict__ msg_type,
-                                  const int32_t *__restrict__ cg_ptr, const int32_t *__restrict__ cg_mem,
-                                  const float *__restrict__ inv_c, int Gc, float *__restrict__ memb) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)L * Gc * 64) return;
-    const int64_t lg = i >> 6;
-    const int l = (int)(lg / Gc), g = (int)(lg - (int64_t)l * Gc), u = (int)(i & 63);
-    const float *emb = emb0 + l * lstride;
-    float s = 0.0f;
-    for (int q = cg_ptr[g]; q < cg_ptr[g + 1]; ++q) s += emb[msg_type[cg_mem[q]] * 64 + u];
-    memb[i] = s * inv_c[g];
-}
-
 struct Ws {
     float *xa, *xb, *Mv, *Mc, *msg_out;
     int32_t *csr;
-    float *memb;  // (layers, Gc, H): each layer's mean type embedding per check group (ITC)
     int64_t bytes;
 };
 
@@ -1217,9 +1086,7 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     w.Mc = reinterpret_cast<float *>(c + xb + xb2 + mv);
     w.msg_out = reinterpret_cast<float *>(c + xb + xb2 + mv + mc);
     w.csr = reinterpret_cast<int32_t *>(c + xb + xb2 + mv + mc + vs);
-    const int64_t mb = al((int64_t)layers * p->Gc * H * 4);
-    w.memb = reinterpret_cast<float *>(c + xb + xb2 + mv + mc + vs + cs);
-    w.bytes = xb + xb2 + mv + mc + vs + cs + mb;
+    w.bytes = xb + xb2 + mv + mc + vs + cs;
     return w;
 }
 
@@ -1721,11 +1588,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     const bool split = split_path() && mlp2s_lds_bytes(types, false) <= 160 * 1024;
     // degree-1 message tiles first (gnn_mlp2s_kernel) when the combined image fits
     const bool d1t = split && p->n_mtiles_v1 > 0 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
-    // in-tile check means from layer 1 (check-aligned plans, H = 64)
-    const bool itc_ok = proj && split && p->ct_aligned && p->n_ctiles > 0 && itc_path() &&
-                        mlp2s_lds_bytes(types, true) <= 160 * 1024;
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
-                 mlp2_lds = split ? mlp2s_lds_bytes(types, d1t || itc_ok) : mlp2_lds_bytes(types);
+                 mlp2_lds = split ? mlp2s_lds_bytes(types, d1t) : mlp2_lds_bytes(types);
     const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
     int mlp2_per_cu = 1, proj_per_cu = 1;
@@ -1740,15 +1604,6 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>)
                                            : reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
-        if (itc_ok) {
-            LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
-            const int64_t nm = (int64_t)layers * p->Gc * 64;
-            hipLaunchKernelGGL(gnn_memb_c_kernel, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s,
-                               d_weights + 2 * H, layer_floats(H, types), layers, d_msg_type, p->cg_ptr, p->cg_mem,
-                               p->inv_c, p->Gc, w.memb);
-            LDPC_CHECK_LAUNCH("gnn_memb_c_kernel");
-        }
     }
     // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
     const GnnLayer L0 = L;
@@ -1783,17 +1638,12 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.d1 = H == 64 && gm_tiles() && d1_skip() && !p->weighted;
         if (proj) {
             L.d1 = 0;
-            // layers >= 1 of a check-aligned plan: check means in the MLP tiles, projection of the
-            // var side only; otherwise degree-1 tiles first when enabled
-            const bool itc = itc_ok && l > 0, d1l = d1t && !itc;
-            L.tperm = d1l ? p->mt_perm : nullptr;
-            L.ntile_pf = d1l ? p->n_mtiles : 0;
-            L.ntile_v1 = d1l ? p->n_mtiles_v1 : 0;
-            L.ct_m0 = p->ct_m0;
-            L.ctpf = p->n_ctiles;
-            L.memb_c = w.memb + (int64_t)l * p->Gc * H;
-            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, itc ? p->n_ptiles_v : p->n_ptiles,
-                              d1l ? p->n_ptiles_v1 : 0};
+            if (d1t) {
+                L.tperm = p->mt_perm;
+                L.ntile_pf = p->n_mtiles;
+                L.ntile_v1 = p->n_mtiles_v1;
+            }
+            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, d1t ? p->n_ptiles_v1 : 0};
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;
             const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
@@ -1802,14 +1652,13 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             else
                 hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds, st, L, T);
             LDPC_CHECK_LAUNCH("gnn_group_proj_kernel");
-            const int64_t tiles = itc ? nb * p->n_ctiles : d1l ? nb * p->n_mtiles : (nb * p->E + 31) / 32;
+            const int64_t tiles = d1t ? nb * p->n_mtiles : (nb * p->E + 31) / 32;
             constexpr int wpb = kMlp2Nt / 64;
             const unsigned grid = (unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu);
-            const dim3 sgrid((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus));
-            if (split && itc)
-                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>), sgrid, dim3(kMlp2sNt), mlp2_lds, st, L);
-            else if (split)
-                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>), sgrid, dim3(kMlp2sNt), mlp2_lds, st, L);
+            if (split)
+                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>),
+                                   dim3((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus)),
+                                   dim3(kMlp2sNt), mlp2_lds, st, L);
             else
                 hipLaunchKernelGGL((gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>), dim3(grid), dim3(kMlp2Nt), mlp2_lds, st, L);
             LDPC_CHECK_LAUNCH("gnn_mlp2_kernel");
