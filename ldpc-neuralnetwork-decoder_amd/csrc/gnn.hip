@@ -840,23 +840,35 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     const float bo = P.last ? P.bo[0] : 0.0f;
     const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
     const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
+    // (frame, in-frame tile) of the tperm walk, advanced without divisions: tw.stride = sb frames + sk tiles
+    const int64_t sb = tw.stride / tpf, sk = tw.stride - sb * tpf;
+    int64_t tb = tw.first / tpf, tk = tw.first - tb * tpf;
+    // (frame, message) of row t * 32 + j of the plain walk, likewise (row stride 32 tw.stride)
+    const int64_t rs = 32 * tw.stride, rsb = rs / P.E, rsm = rs - rsb * P.E;
+    int64_t pb = (tw.first * 32 + j) / P.E, pm = tw.first * 32 + j - pb * P.E;
     for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
         int64_t rr, b, m;
         bool ok, d1t = false;
         if (P.tperm) {  // slot j of the frame's tile k (padding: the tile's first message, not written)
-            b = t / tpf;
-            const int64_t k = t - b * tpf;
+            b = tb;
+            const int64_t k = tk;
             const int32_t mm = P.tperm[k * 32 + j];
             ok = mm >= 0;
             m = ok ? mm : P.tperm[k * 32];
             rr = b * P.E + m;
             d1t = k < P.ntile_v1;
+            tb += sb;
+            tk += sk;
+            if (tk >= tpf) { tk -= tpf; ++tb; }
         } else {
             const int64_t row = t * 32 + j;
             ok = row < R;
             rr = ok ? row : R - 1;
-            b = rr / P.E;
-            m = rr - b * P.E;
+            b = ok ? pb : P.B - 1;
+            m = ok ? pm : P.E - 1;
+            pb += rsb;
+            pm += rsm;
+            if (pm >= P.E) { pm -= P.E; ++pb; }
         }
         // x[s][i] = feature pi16(16 s + 8 h + i) before the type embedding (float4 pairs)
         float x[4][8];
@@ -889,32 +901,43 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         // a degree-1 tile's var side starts from b1v (its group half is in the combined W1v image)
         const float *pv = d1t ? P.b1v + 4 * half : P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
         const float *pc = P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
-        f32x16 y0 = {}, y1 = {};
+        // GEMM1 of both sides per k-step over one split of c (c = x + emb[type] is the same for
+        // both), each side's accumulators from its projected group row W1_right g + b1
+        f32x16 hs[2][2];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             if (side == 0 && !P.vside) continue;
             const float *pr = side == 0 ? pv : pc;
-            f32x16 h0, h1;  // from the projected group row W1_right g + b1
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float4 a = *reinterpret_cast<const float4 *>(pr + 8 * q);
                 const float4 c = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q);
-                h0[4 * q] = a.x; h0[4 * q + 1] = a.y; h0[4 * q + 2] = a.z; h0[4 * q + 3] = a.w;
-                h1[4 * q] = c.x; h1[4 * q + 1] = c.y; h1[4 * q + 2] = c.z; h1[4 * q + 3] = c.w;
+                hs[side][0][4 * q] = a.x; hs[side][0][4 * q + 1] = a.y; hs[side][0][4 * q + 2] = a.z; hs[side][0][4 * q + 3] = a.w;
+                hs[side][1][4 * q] = c.x; hs[side][1][4 * q + 1] = c.y; hs[side][1][4 * q + 2] = c.z; hs[side][1][4 * q + 3] = c.w;
             }
-            const __bf16 *W1 = (side == 0 && d1t ? img_d1 : img + 3 * side * kS6Img) + abase;
+        }
+        const __bf16 *W1v = (d1t ? img_d1 : img) + abase, *W1c = img + 3 * kS6Img + abase;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            float c[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[i] = x[s][i] + e[pi16(16 * s + 8 * half + i)];
+            bf16x8_t c0, c1, c2;
+            split3(c, c0, c1, c2);
+            if (P.vside) {
+                hs[0][0] = mfma6(W1v + 16 * s, c0, c1, c2, hs[0][0], kS6Img);
+                hs[0][1] = mfma6(W1v + 32 * kS6Row + 16 * s, c0, c1, c2, hs[0][1], kS6Img);
+            }
+            hs[1][0] = mfma6(W1c + 16 * s, c0, c1, c2, hs[1][0], kS6Img);
+            hs[1][1] = mfma6(W1c + 32 * kS6Row + 16 * s, c0, c1, c2, hs[1][1], kS6Img);
+            __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
+        }
+        f32x16 y0 = {}, y1 = {};
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            if (side == 0 && !P.vside) continue;
+            const f32x16 &h0 = hs[side][0], &h1 = hs[side][1];
             const __bf16 *W2 = img + kS6OffW2 + 3 * side * kS6Img + abase;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {  // GEMM1: h += W1_left c, c = x + emb[type]
-                float c[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) c[i] = x[s][i] + e[pi16(16 * s + 8 * half + i)];
-                bf16x8_t c0, c1, c2;
-                split3(c, c0, c1, c2);
-                h0 = mfma6(W1 + 16 * s, c0, c1, c2, h0, kS6Img);
-                h1 = mfma6(W1 + 32 * kS6Row + 16 * s, c0, c1, c2, h1, kS6Img);
-                __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
-            }
 #pragma unroll
             for (int s = 0; s < 4; ++s) {  // GEMM2: y += W2 relu(h); k-step s = registers 8 (s&1) .. of h_{s>>1}
                 float hr[8];
@@ -940,8 +963,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 for (int i = 0; i < 4; ++i) {
                     const float acc = ot == 0 ? y0[4 * q + i] : y1[4 * q + i];
                     vv[i] = (acc + b2v[o0 + i]) + b2c[o0 + i];
-                    // residual: register 4 q + i of tile ot is x[2 ot + (q >> 1)][4 (q & 1) + i]
-                    if (P.residual) vv[i] += x[2 * ot + (q >> 1)][4 * (q & 1) + i];
+                }
+                // residual: register 4 q + i of tile ot is x[2 ot + (q >> 1)][4 (q & 1) + i]
+                if (P.residual) {
+                    v.x += x[2 * ot + (q >> 1)][4 * (q & 1)];
+                    v.y += x[2 * ot + (q >> 1)][4 * (q & 1) + 1];
+                    v.z += x[2 * ot + (q >> 1)][4 * (q & 1) + 2];
+                    v.w += x[2 * ot + (q >> 1)][4 * (q & 1) + 3];
                 }
                 if (P.last) {
 #pragma unroll
@@ -1168,11 +1196,13 @@ __global__ void custom_output_kernel(const float *__restrict__ msg_out, const in
 int g_num_cus = 0;
 
 constexpr int kMlp2Wps = LDPC_MLP2_WPS, kMlp2Nt = LDPC_MLP2_NT;
+// 2 waves per SIMD: both sides' GEMM1 share one split of c (226 VGPRs, no spills); 51.6 k vs 49.9 k
+// cw/s for the per-side form at 3 waves per SIMD (168 VGPRs, spilling), profiles/r04
 #ifndef LDPC_MLP2S_WPS
-#define LDPC_MLP2S_WPS 3
+#define LDPC_MLP2S_WPS 2
 #endif
 #ifndef LDPC_MLP2S_NT
-#define LDPC_MLP2S_NT 768
+#define LDPC_MLP2S_NT 512
 #endif
 constexpr int kMlp2sWps = LDPC_MLP2S_WPS, kMlp2sNt = LDPC_MLP2S_NT;
 // LDPC_GNN_SPLIT=0: the projected-group MLP on v_mfma_f32_32x32x2_f32 (gnn_mlp2_kernel); default:

@@ -417,7 +417,7 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
                         in[4 * q + 2] = (w.z * l + bi.z) + ev.z; in[4 * q + 3] = (w.w * l + bi.w) + ev.w;
                     }
                 }
-                if (side == 0 && ok) {
+                if (side == 0 && ok && A.cbuf) {
                     float4 *cb = reinterpret_cast<float4 *>(A.cbuf + row * H + 32 * half);
 #pragma unroll
                     for (int q = 0; q < 8; ++q)
@@ -885,6 +885,153 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     if (P.bias && threadIdx.x < H) atomicAdd(&P.bias[threadIdx.x], bred[threadIdx.x]);
 }
 
+// dW1_left of both sides in one pass over the rows (H = 64, projected-group backward):
+//   gw1s[i][j] += sum_r dh_s[r][i] c_r[j],  gb1s[i] += sum_r dh_s[r][i]   (s = v, c; j < 64)
+// with c_r = x_r + emb[type(m)] (ZM 1; x = the saved features of the layer's input) or
+// (w_in llr + b_in) + emb[type(m)] (ZM 2, layer 0) formed here in the MLP backward's float order
+// (the same c, bit for bit), so the backward MLP writes no copy of c and c is read once for both
+// sides.  Layout and pipelining as train_outer_mfma_kernel<2, 2, true>: lane (col, k) loads rows
+// r0 + 2u + k, batches of KU k-steps double-buffered, the type embedding in LDS.
+struct Dw1T {
+    const float *dhv, *dhc, *x, *emb, *llr, *w_in, *b_in;
+    const int32_t *msg_type, *msg_var;
+    float *gv, *gc, *bv, *bc;
+    int T, N;
+    int64_t E, R;
+};
+inline size_t dw1_lds(int T) { return (size_t)std::max(T * 64, 2 * 64 * 64 + 2 * 64) * 4; }
+
+template <int ZM>
+__global__ __launch_bounds__(256, 2) void train_dw1_kernel(Dw1T P) {
+    extern __shared__ __attribute__((aligned(16))) float sh[];
+    for (int i = threadIdx.x; i < P.T * 64; i += 256) sh[i] = P.emb[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, col = lane & 31, k = lane >> 5;
+    const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t per = ((P.R + nw - 1) / nw + 1) & ~1LL;
+    const int64_t r_begin = w * per, r_end = r_begin + per < P.R ? r_begin + per : P.R;
+    f32x16 acc[2][2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt) acc[s][it][jt] = f32x16{};
+    float bsum[2][2] = {};
+    float win[2] = {}, bin[2] = {};
+    if (ZM == 2)
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            win[jt] = P.w_in[32 * jt + col];
+            bin[jt] = P.b_in[32 * jt + col];
+        }
+    constexpr int KU = 4;
+    struct Batch { float a[KU][2][2], z[KU][2], l[KU]; int ty[KU]; };
+    if (r_begin < r_end) {
+        const int64_t rlast = r_end - 1;
+        int64_t bq = r_begin / P.E, mq = r_begin - bq * P.E;  // (frame, message) of the batch's first row
+        const int64_t bl = rlast / P.E, ml = rlast - bl * P.E;  // ... and of the range's last row
+        auto load = [&](int64_t r0, int64_t b0, int64_t m0, Batch &Bt) {
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                // rows past the range read the last row (their A values are zeroed at use)
+                const bool in = r0 + 2 * u + k <= rlast;
+                const int64_t r = in ? r0 + 2 * u + k : rlast;
+                int64_t mu = m0 + 2 * u + k, bu = b0;
+                if (mu >= P.E) { mu -= P.E; ++bu; }
+                mu = in ? mu : ml;
+                bu = in ? bu : bl;
+#pragma unroll
+                for (int it = 0; it < 2; ++it) {
+                    Bt.a[u][0][it] = P.dhv[r * 64 + 32 * it + col];
+                    Bt.a[u][1][it] = P.dhc[r * 64 + 32 * it + col];
+                }
+                Bt.ty[u] = P.msg_type[mu];
+                if (ZM == 1) {
+#pragma unroll
+                    for (int jt = 0; jt < 2; ++jt) Bt.z[u][jt] = P.x[r * 64 + 32 * jt + col];
+                } else {
+                    Bt.l[u] = P.llr[bu * P.N + P.msg_var[mu]];
+                }
+            }
+        };
+        auto mfma = [&](int64_t r0, const Batch &Bt) {
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const bool ok = r0 + 2 * u + k < r_end;
+                float z[2];
+#pragma unroll
+                for (int jt = 0; jt < 2; ++jt) {
+                    const float xv = ZM == 1 ? Bt.z[u][jt] : win[jt] * Bt.l[u] + bin[jt];
+                    z[jt] = xv + sh[Bt.ty[u] * 64 + 32 * jt + col];
+                }
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int it = 0; it < 2; ++it) {
+                        const float a = ok ? Bt.a[u][s][it] : 0.0f;
+                        bsum[s][it] += a;
+#pragma unroll
+                        for (int jt = 0; jt < 2; ++jt)
+                            acc[s][it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, z[jt], acc[s][it][jt], 0, 0, 0);
+                    }
+            }
+        };
+        auto step = [&]() {
+            mq += 2 * KU;
+            if (mq >= P.E) { mq -= P.E; ++bq; }
+        };
+        Batch b0, b1;
+        load(r_begin, bq, mq, b0);
+        for (int64_t r0 = r_begin;;) {
+            int64_t nb = bq, nm = mq + 2 * KU;
+            if (nm >= P.E) { nm -= P.E; ++nb; }
+            load(r0 + 2 * KU, nb, nm, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma(r0, b0);
+            step();
+            if ((r0 += 2 * KU) >= r_end) break;
+            nb = bq; nm = mq + 2 * KU;
+            if (nm >= P.E) { nm -= P.E; ++nb; }
+            load(r0 + 2 * KU, nb, nm, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma(r0, b1);
+            step();
+            if ((r0 += 2 * KU) >= r_end) break;
+        }
+    }
+    // the four waves' tiles summed in LDS (the embedding image is no longer read), then one
+    // global atomic per gradient entry per workgroup; D[i][j]: register q of lane (col, k) holds
+    // i = 8 (q >> 2) + 4 k + (q & 3), j = col
+    __syncthreads();
+    float *red = sh, *bred = sh + 2 * 64 * 64;
+    for (int e = threadIdx.x; e < 2 * 64 * 64 + 2 * 64; e += 256) sh[e] = 0.0f;
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int i = 32 * it + 8 * (q >> 2) + 4 * k + (q & 3);
+                    atomicAdd(&red[s * 4096 + i * 64 + 32 * jt + col], acc[s][it][jt][q]);
+                }
+            const float sm = bsum[s][it] + __shfl_xor(bsum[s][it], 32, 64);
+            if (k == 0) atomicAdd(&bred[s * 64 + 32 * it + col], sm);
+        }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * 4096; e += 256) {
+        const int s = e >> 12, i = (e >> 6) & 63, j = e & 63;
+        atomicAdd(&(s ? P.gc : P.gv)[i * 128 + j], red[e]);
+    }
+    if (threadIdx.x < 128) {
+        const int s = threadIdx.x >> 6, i = threadIdx.x & 63;
+        atomicAdd(&(s ? P.bc : P.bv)[i], bred[threadIdx.x]);
+    }
+}
+
 // workgroups per CU of the weight-gradient reductions (LDPC_GNN_OUTER_WGS, default 2: 40.1 vs 41.0
 // ms per step at 4 and 43.6 at 8, profiles/r04); read per call
 int outer_wgs() {
@@ -1268,7 +1415,8 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         m.Mv = Mv; m.Mc = Mc; m.dX = w.dX;
         m.msg_type = d_msg_type; m.msg_var = d_msg_var; m.vgroup = p->vgroup; m.cgroup = p->cgroup;
         m.emb = W[0]; m.w1v = W[1]; m.b1v = W[2]; m.w2v = W[3]; m.w1c = W[5]; m.b1c = W[6]; m.w2c = W[7];
-        m.cbuf = w.cbuf; m.hv = w.hv; m.hc = w.hc; m.dhv = w.dhv; m.dhc = w.dhc;
+        m.cbuf = pj ? nullptr : w.cbuf;  // PJ: train_dw1_kernel forms c itself
+        m.hv = w.hv; m.hc = w.hc; m.dhv = w.dhv; m.dhc = w.dhc;
         m.dco = w.dco; m.da = w.da; m.db = w.db;
         m.H = H; m.N = N; m.Gv = p->Gv; m.Gc = p->Gc; m.E = E; m.R = R;
         if (H == 64 && bwd_mfma()) {  // LDPC_GNN_TRAIN_MFMA=0 selects the VALU kernel (A/B runs)
@@ -1334,16 +1482,30 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         // dW1_s = sum_m dh_s[m] (x) [c_m; g_s(group(m))]: the c half row by row; the group half as
         // sum_groups (sum_{m in group} dh_s[m]) (x) g_s(group) -- contiguous group rows instead of
         // a gathered group row per message (Mda / Mdb are free again after the combine step)
+        if (pj) {  // the c half of both sides in one pass, c formed from x (no stored copy)
+            Dw1T d{};
+            d.dhv = w.dhv; d.dhc = w.dhc; d.x = x; d.emb = W[0]; d.llr = d_llr;
+            d.w_in = d_weights; d.b_in = d_weights + H; d.msg_type = d_msg_type; d.msg_var = d_msg_var;
+            d.gv = Gw[1]; d.gc = Gw[5]; d.bv = Gw[2]; d.bc = Gw[6];
+            d.T = T; d.N = N; d.E = E; d.R = R;
+            if (x)
+                hipLaunchKernelGGL(train_dw1_kernel<1>, dim3(red_grid), dim3(256), dw1_lds(T), s, d);
+            else
+                hipLaunchKernelGGL(train_dw1_kernel<2>, dim3(red_grid), dim3(256), dw1_lds(T), s, d);
+            LDPC_CHECK_LAUNCH("train_dw1_kernel");
+        }
         for (int side = 0; side < 2; ++side) {
             // PJ: the group means are in Gsv / Gsc and the group sums of dh already in Mv / Mc
             const float *dh = side ? w.dhc : w.dhv, *Gs = pj ? (side ? Gsc : Gsv) : side ? w.Mc : w.Mv;
             float *dhsum = pj ? (side ? Mc : Mv) : side ? w.Mdb : w.Mda;
             float *gw = side ? Gw[5] : Gw[1], *gb = side ? Gw[6] : Gw[2];
             const int Gn = side ? p->Gc : p->Gv;
-            OuterT c{};
-            c.H = H; c.E = E; c.R = R; c.A = dh; c.zsrc = w.cbuf; c.J = H; c.ld = 2 * H; c.col0 = 0;
-            c.out = gw; c.bias = gb;
-            if (int rc = launch_outer(c, red_grid, s)) return rc;
+            if (!pj) {
+                OuterT c{};
+                c.H = H; c.E = E; c.R = R; c.A = dh; c.zsrc = w.cbuf; c.J = H; c.ld = 2 * H; c.col0 = 0;
+                c.out = gw; c.bias = gb;
+                if (int rc = launch_outer(c, red_grid, s)) return rc;
+            }
             if (!pj) {
                 GmT gs{};
                 gs.src = dh; gs.src_mode = 0; gs.sum_only = 1; gs.H = H; gs.N = N; gs.E = E; gs.B = B;
