@@ -668,6 +668,38 @@ __global__ void train_combine4_kernel(float4 *__restrict__ dco, const float4 *__
     }
 }
 
+// The combine step fused with the first pass of the embedding gradients (projected-group backward):
+// one thread per (message, unit) walks the frames in order, forms dc as train_combine4_kernel does
+// (the same float sequence), writes dx_l and sums dc over the frames (demb's first pass,
+// train_colsum_kernel<0>: the same order, so the same sums), and at layer 0 also sum dc * llr
+// (train_colsum_kernel<1>).  dc itself is never stored: 2 of the step's 6 passes over (B, E, H).
+template <bool L0>
+__global__ void train_combine_sum_kernel(const float *__restrict__ dco, const float *__restrict__ Mda,
+                                         const float *__restrict__ Mdb, const float *__restrict__ dX,
+                                         const int32_t *__restrict__ vgroup, const int32_t *__restrict__ cgroup,
+                                         const int32_t *__restrict__ msg_var, const float *__restrict__ llr, int H,
+                                         int Gv, int Gc, int N, int64_t E, int64_t B, int residual,
+                                         float *__restrict__ dx_out, float *__restrict__ Sdc, float *__restrict__ Sdl) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t EH = E * H;
+    if (t >= EH) return;
+    const int64_t m = t / H;
+    const int u = (int)(t - m * H);
+    const int64_t vg = vgroup[m], cg = cgroup[m];
+    const int var = L0 ? msg_var[m] : 0;
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll 4
+    for (int64_t b = 0; b < B; ++b) {
+        const int64_t i = b * EH + t;
+        const float dc = (dco[i] + Mda[(b * Gv + vg) * H + u]) + Mdb[(b * Gc + cg) * H + u];
+        dx_out[i] = residual ? dc + dX[i] : dc;
+        s0 += dc;
+        if (L0) s1 = fmaf(dc, llr[b * N + var], s1);
+    }
+    Sdc[t] = s0;
+    if (L0) Sdl[t] = s1;
+}
+
 // ------------------------------------------------------------------------ weight gradients
 // out[i][j] += sum_r A[r][i] Z_r[j] (i < H, j < J), bias[i] += sum_r A[r][i];
 // Z_r = zsrc[r] (J = H), or [zsrc[r]; G[b][grp(m)]] (J = 2H, the concatenated MLP input)
@@ -1147,6 +1179,21 @@ __global__ __launch_bounds__(256) void train_vecfinal_kernel(VecT P, const float
     }
 }
 
+// the second pass alone, from frame sums S0 (and S1) formed elsewhere
+int launch_vecfinal(const VecT &v, const float *S0, const float *S1, hipStream_t s) {
+    const dim3 g2((unsigned)((v.E + kChunkV - 1) / kChunkV));
+    const size_t lds = vecfinal_lds(v.T, v.H);
+    if (lds > 64 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the embedding gradient");
+    if (v.mode == 0)
+        hipLaunchKernelGGL(train_vecfinal_kernel<0>, g2, dim3(256), lds, s, v, S0, S1);
+    else if (v.mode == 1)
+        hipLaunchKernelGGL(train_vecfinal_kernel<1>, g2, dim3(256), lds, s, v, S0, S1);
+    else
+        hipLaunchKernelGGL(train_vecfinal_kernel<2>, g2, dim3(256), lds, s, v, S0, S1);
+    LDPC_CHECK_LAUNCH("train_vecfinal_kernel");
+    return LDPC_OK;
+}
+
 int launch_vec(const VecT &v, float *S0, float *S1, hipStream_t s) {
     const int64_t EH = v.E * v.H;
     const dim3 g1((unsigned)((EH + 255) / 256)), g2((unsigned)((v.E + kChunkV - 1) / kChunkV));
@@ -1460,7 +1507,10 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
             d.src = w.db; d.ptr = p->cg_ptr; d.mem = p->cg_mem; d.inv = p->inv_c; d.G = p->Gc; d.dst = w.Mdb;
             if (int rc = launch_group_mean(d, s)) return rc;
         }
-        if (H % 4 == 0)
+        if (pj) {
+            // combined with the embedding gradient's frame sums after the weight gradients (below),
+            // into hv / hc once dW2 has read them
+        } else if (H % 4 == 0)
             hipLaunchKernelGGL(train_combine4_kernel, blocks(n / 4, 256), dim3(256), 0, s,
                                reinterpret_cast<float4 *>(w.dco), reinterpret_cast<const float4 *>(w.Mda),
                                reinterpret_cast<const float4 *>(w.Mdb), reinterpret_cast<const float4 *>(w.dX),
@@ -1523,11 +1573,30 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         VecT v{};
         v.src = w.dco; v.llr = d_llr; v.msg_type = d_msg_type; v.msg_var = d_msg_var;
         v.H = H; v.T = T; v.N = N; v.E = E; v.R = R;
-        v.mode = 0; v.g0 = Gw[0];
-        if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
-        if (l == 0) {
-            v.mode = 1; v.g0 = d_grad_weights; v.g1 = d_grad_weights + H;
+        if (pj) {  // dx_l, and the frame sums of dc (hv) and of dc * llr (hc, layer 0)
+            const int64_t EH = E * H;
+            if (l == 0)
+                hipLaunchKernelGGL(train_combine_sum_kernel<true>, blocks(EH, 256), dim3(256), 0, s, w.dco, w.Mda,
+                                   w.Mdb, w.dX, p->vgroup, p->cgroup, d_msg_var, d_llr, H, p->Gv, p->Gc, N, E, B, 0,
+                                   w.dXp, w.hv, w.hc);
+            else
+                hipLaunchKernelGGL(train_combine_sum_kernel<false>, blocks(EH, 256), dim3(256), 0, s, w.dco, w.Mda,
+                                   w.Mdb, w.dX, p->vgroup, p->cgroup, d_msg_var, d_llr, H, p->Gv, p->Gc, N, E, B, 1,
+                                   w.dXp, w.hv, w.hc);
+            LDPC_CHECK_LAUNCH("train_combine_sum_kernel");
+            v.mode = 0; v.g0 = Gw[0];
+            if (int rc = launch_vecfinal(v, w.hv, w.hc, s)) return rc;
+            if (l == 0) {  // dw_in from sum dc * llr, db_in from sum dc
+                v.mode = 1; v.g0 = d_grad_weights; v.g1 = d_grad_weights + H;
+                if (int rc = launch_vecfinal(v, w.hc, w.hv, s)) return rc;
+            }
+        } else {
+            v.mode = 0; v.g0 = Gw[0];
             if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
+            if (l == 0) {
+                v.mode = 1; v.g0 = d_grad_weights; v.g1 = d_grad_weights + H;
+                if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
+            }
         }
         std::swap(w.dX, w.dXp);
     }
