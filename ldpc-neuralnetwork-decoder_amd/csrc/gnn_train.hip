@@ -1096,6 +1096,8 @@ struct VecT {
     float *g0, *g1;  // mode 0: demb; 1: dw_in, db_in; 2: dwo, dbo
     int H, T, N, mode;
     int64_t E, R;
+    float *part = nullptr;  // per-workgroup partial sums (scratch), capacity part_cap floats
+    int64_t part_cap = 0;
 };
 
 // The same three reductions in two coalesced passes: first over the frames, per (message, unit)
@@ -1132,10 +1134,11 @@ __global__ void train_colsum_kernel(VecT P, float *__restrict__ S0, float *__res
 }
 
 // Second pass: a workgroup of 4 waves per kChunkV messages (wave w takes every fourth, lanes =
-// units).  Mode 0 sums per type in LDS (ds_add) and adds each nonzero entry to demb once per
-// workgroup; modes 1 / 2 sum per lane, then over the waves in LDS, one global add per unit.  (One
-// global atomic per (message, unit) serialised ~200 deep per address at L2: 0.15 ms per call.)
-constexpr int kChunkV = 256;
+// units).  Mode 0 sums per type in LDS (ds_add); modes 1 / 2 sum per lane, then over the waves in
+// LDS.  Each workgroup then writes its partial vector to scratch and train_vecreduce_kernel sums
+// the workgroups per entry, one global add each.  (Float atomics into the gradient from every
+// workgroup serialise per cache line at L2: 0.17 ms per call whatever the workgroup count.)
+constexpr int kChunkV = 64;
 inline size_t vecfinal_lds(int T, int H) { return (size_t)std::max(T * H, 2 * 4 * H) * 4; }
 
 template <int MODE>
@@ -1167,23 +1170,49 @@ __global__ __launch_bounds__(256) void train_vecfinal_kernel(VecT P, const float
         }
     }
     __syncthreads();
+    const bool part = P.part != nullptr;  // else (scratch too small) straight into the gradient
     if constexpr (MODE == 0) {
-        for (int i = threadIdx.x; i < n; i += 256)
-            if (acc[i] != 0.0f) atomicAdd(&P.g0[i], acc[i]);
+        for (int i = threadIdx.x; i < n; i += 256) {
+            if (part) P.part[(int64_t)blockIdx.x * n + i] = acc[i];
+            else if (acc[i] != 0.0f) atomicAdd(&P.g0[i], acc[i]);
+        }
     } else if (w == 0 && on) {
         const float s0 = ((acc[u] + acc[P.H + u]) + acc[2 * P.H + u]) + acc[3 * P.H + u];
         const float s1 = ((acc[4 * P.H + u] + acc[5 * P.H + u]) + acc[6 * P.H + u]) + acc[7 * P.H + u];
-        atomicAdd(&P.g0[u], s0);
-        if (MODE == 1) atomicAdd(&P.g1[u], s1);
-        else if (u == 0) atomicAdd(&P.g1[0], s1);  // dbo: S1 is the same for every unit
+        if (part) {
+            P.part[(int64_t)blockIdx.x * 2 * P.H + u] = s0;
+            P.part[(int64_t)blockIdx.x * 2 * P.H + P.H + u] = s1;
+        } else {
+            atomicAdd(&P.g0[u], s0);
+            if (MODE == 1) atomicAdd(&P.g1[u], s1);
+            else if (u == 0) atomicAdd(&P.g1[0], s1);  // dbo: S1 is the same for every unit
+        }
     }
 }
 
+// sum of the workgroups' partial vectors per entry (ascending workgroups), into the gradient
+template <int MODE>
+__global__ void train_vecreduce_kernel(VecT P, int nblk) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = MODE == 0 ? P.T * P.H : 2 * P.H;
+    if (i >= n) return;
+    float s = 0.0f;
+    for (int b = 0; b < nblk; ++b) s += P.part[(int64_t)b * n + i];
+    if (MODE == 0) atomicAdd(&P.g0[i], s);
+    else if (i < P.H) atomicAdd(&P.g0[i], s);
+    else if (MODE == 1) atomicAdd(&P.g1[i - P.H], s);
+    else if (i == P.H) atomicAdd(&P.g1[0], s);  // dbo: S1 is the same for every unit
+}
+
 // the second pass alone, from frame sums S0 (and S1) formed elsewhere
-int launch_vecfinal(const VecT &v, const float *S0, const float *S1, hipStream_t s) {
-    const dim3 g2((unsigned)((v.E + kChunkV - 1) / kChunkV));
-    const size_t lds = vecfinal_lds(v.T, v.H);
+int launch_vecfinal(const VecT &v0, const float *S0, const float *S1, hipStream_t s) {
+    const int nblk = (int)((v0.E + kChunkV - 1) / kChunkV);
+    const dim3 g2((unsigned)nblk);
+    const size_t lds = vecfinal_lds(v0.T, v0.H);
     if (lds > 64 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the embedding gradient");
+    const int n = v0.mode == 0 ? v0.T * v0.H : 2 * v0.H;
+    VecT v = v0;
+    if ((int64_t)nblk * n > v.part_cap) v.part = nullptr;
     if (v.mode == 0)
         hipLaunchKernelGGL(train_vecfinal_kernel<0>, g2, dim3(256), lds, s, v, S0, S1);
     else if (v.mode == 1)
@@ -1191,6 +1220,13 @@ int launch_vecfinal(const VecT &v, const float *S0, const float *S1, hipStream_t
     else
         hipLaunchKernelGGL(train_vecfinal_kernel<2>, g2, dim3(256), lds, s, v, S0, S1);
     LDPC_CHECK_LAUNCH("train_vecfinal_kernel");
+    if (v.part) {
+        const dim3 gr((unsigned)((n + 255) / 256));
+        if (v.mode == 0) hipLaunchKernelGGL(train_vecreduce_kernel<0>, gr, dim3(256), 0, s, v, nblk);
+        else if (v.mode == 1) hipLaunchKernelGGL(train_vecreduce_kernel<1>, gr, dim3(256), 0, s, v, nblk);
+        else hipLaunchKernelGGL(train_vecreduce_kernel<2>, gr, dim3(256), 0, s, v, nblk);
+        LDPC_CHECK_LAUNCH("train_vecreduce_kernel");
+    }
     return LDPC_OK;
 }
 
@@ -1199,18 +1235,16 @@ int launch_vec(const VecT &v, float *S0, float *S1, hipStream_t s) {
     const dim3 g1((unsigned)((EH + 255) / 256)), g2((unsigned)((v.E + kChunkV - 1) / kChunkV));
     const size_t lds = vecfinal_lds(v.T, v.H);
     if (lds > 64 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the embedding gradient");
-    if (v.mode == 0) {
+    (void)g2;
+    (void)lds;
+    if (v.mode == 0)
         hipLaunchKernelGGL(train_colsum_kernel<0>, g1, dim3(256), 0, s, v, S0, S1);
-        hipLaunchKernelGGL(train_vecfinal_kernel<0>, g2, dim3(256), lds, s, v, S0, S1);
-    } else if (v.mode == 1) {
+    else if (v.mode == 1)
         hipLaunchKernelGGL(train_colsum_kernel<1>, g1, dim3(256), 0, s, v, S0, S1);
-        hipLaunchKernelGGL(train_vecfinal_kernel<1>, g2, dim3(256), lds, s, v, S0, S1);
-    } else {
+    else
         hipLaunchKernelGGL(train_colsum_kernel<2>, g1, dim3(256), 0, s, v, S0, S1);
-        hipLaunchKernelGGL(train_vecfinal_kernel<2>, g2, dim3(256), lds, s, v, S0, S1);
-    }
-    LDPC_CHECK_LAUNCH("train_vec_kernel");
-    return LDPC_OK;
+    LDPC_CHECK_LAUNCH("train_colsum_kernel");
+    return launch_vecfinal(v, S0, S1, s);
 }
 
 
@@ -1377,6 +1411,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
     LDPC_CHECK_LAUNCH("train_dx_last_kernel");
     {
         VecT v{};
+        v.part = w.dhv; v.part_cap = R * H;
         v.src = d_saved + (int64_t)(L - 1) * n;
         v.dz = w.dz;
         v.msg_type = d_msg_type;
@@ -1422,6 +1457,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
                                n, w.dX, 1);
             LDPC_CHECK_LAUNCH("train_dx_last_kernel");
             VecT v{};
+            v.part = w.dhv; v.part_cap = R * H;
             v.src = d_saved + (int64_t)l * n;
             v.dz = w.dz; v.msg_type = d_msg_type; v.msg_var = d_msg_var; v.g0 = GL[9]; v.g1 = GL[10];
             v.H = H; v.T = T; v.N = N; v.mode = 2; v.E = E; v.R = R;
@@ -1571,6 +1607,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         }
         if (ovl) LDPC_HIP(hipEventRecord(ev_free[l & 1], s));  // this layer's set is free again
         VecT v{};
+        v.part = w.dhv; v.part_cap = R * H;
         v.src = w.dco; v.llr = d_llr; v.msg_type = d_msg_type; v.msg_var = d_msg_var;
         v.H = H; v.T = T; v.N = N; v.E = E; v.R = R;
         if (pj) {  // dx_l, and the frame sums of dc (hv) and of dc * llr (hc, layer 0)
