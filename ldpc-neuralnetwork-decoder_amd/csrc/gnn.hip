@@ -778,6 +778,10 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
     }
 }
 
+// ReLU as one integer max on the bits (a negative float, -0 included, is a negative int32): the
+// same value as fmaxf(v, 0) for every non-NaN v, without the canonicalising v_max fmaxf needs
+__device__ __forceinline__ float relu_i(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
+
 // ------------------------------------------------------------------------ MLP over projected groups, fp32 by bf16x6
 // gnn_mlp2_kernel's math with every fp32 product on v_mfma_f32_32x32x16_bf16: each fp32 operand is
 // split into three bf16 terms, v = v0 + v1 + v2 (v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 -
@@ -942,7 +946,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             for (int s = 0; s < 4; ++s) {  // GEMM2: y += W2 relu(h); k-step s = registers 8 (s&1) .. of h_{s>>1}
                 float hr[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) hr[i] = fmaxf(s < 2 ? h0[8 * (s & 1) + i] : h1[8 * (s & 1) + i], 0.0f);
+                for (int i = 0; i < 8; ++i) hr[i] = relu_i(s < 2 ? h0[8 * (s & 1) + i] : h1[8 * (s & 1) + i]);
                 bf16x8_t r0, r1, r2;
                 split3(hr, r0, r1, r2);
                 y0 = mfma6(W2 + 16 * s, r0, r1, r2, y0, kS6Img);
