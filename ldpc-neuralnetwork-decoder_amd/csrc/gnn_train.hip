@@ -1064,6 +1064,101 @@ __global__ __launch_bounds__(256, 2) void train_dw1_kernel(Dw1T P) {
     }
 }
 
+// dW2 of both sides in one pass over dX (H = 64): gw2s[i][j] += sum_r dX[r][i] h_s[r][j],
+// gb2s[i] += sum_r dX[r][i] (the same bias sums for both sides); h_v = hv, h_c = hc.  The layout
+// and pipelining of train_dw1_kernel, with one A and two Z sources; dX is read once instead of
+// twice.
+struct Dw2T {
+    const float *dX, *hv, *hc;
+    float *gv, *gc, *bv, *bc;
+    int64_t R;
+};
+
+__global__ __launch_bounds__(256, 2) void train_dw2_kernel(Dw2T P) {
+    __shared__ __attribute__((aligned(16))) float sh[2 * 64 * 64 + 64];
+    const int lane = threadIdx.x & 63, col = lane & 31, k = lane >> 5;
+    const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t per = ((P.R + nw - 1) / nw + 1) & ~1LL;
+    const int64_t r_begin = w * per, r_end = r_begin + per < P.R ? r_begin + per : P.R;
+    f32x16 acc[2][2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt) acc[s][it][jt] = f32x16{};
+    float bsum[2] = {};
+    constexpr int KU = 4;
+    struct Batch { float a[KU][2], z[KU][2][2]; };
+    if (r_begin < r_end) {
+        const int64_t rlast = r_end - 1;
+        auto load = [&](int64_t r0, Batch &Bt) {
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const int64_t r = r0 + 2 * u + k <= rlast ? r0 + 2 * u + k : rlast;
+#pragma unroll
+                for (int it = 0; it < 2; ++it) Bt.a[u][it] = P.dX[r * 64 + 32 * it + col];
+#pragma unroll
+                for (int jt = 0; jt < 2; ++jt) {
+                    Bt.z[u][0][jt] = P.hv[r * 64 + 32 * jt + col];
+                    Bt.z[u][1][jt] = P.hc[r * 64 + 32 * jt + col];
+                }
+            }
+        };
+        auto mfma = [&](int64_t r0, const Batch &Bt) {
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const bool ok = r0 + 2 * u + k < r_end;
+#pragma unroll
+                for (int it = 0; it < 2; ++it) {
+                    const float a = ok ? Bt.a[u][it] : 0.0f;
+                    bsum[it] += a;
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+#pragma unroll
+                        for (int jt = 0; jt < 2; ++jt)
+                            acc[s][it][jt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bt.z[u][s][jt], acc[s][it][jt], 0, 0, 0);
+                }
+            }
+        };
+        Batch b0, b1;
+        load(r_begin, b0);
+        for (int64_t r0 = r_begin;;) {
+            load(r0 + 2 * KU, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma(r0, b0);
+            if ((r0 += 2 * KU) >= r_end) break;
+            load(r0 + 2 * KU, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma(r0, b1);
+            if ((r0 += 2 * KU) >= r_end) break;
+        }
+    }
+    float *red = sh, *bred = sh + 2 * 64 * 64;
+    for (int e = threadIdx.x; e < 2 * 64 * 64 + 64; e += 256) sh[e] = 0.0f;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int i = 32 * it + 8 * (q >> 2) + 4 * k + (q & 3);
+                    atomicAdd(&red[s * 4096 + i * 64 + 32 * jt + col], acc[s][it][jt][q]);
+                }
+        const float sm = bsum[it] + __shfl_xor(bsum[it], 32, 64);
+        if (k == 0) atomicAdd(&bred[32 * it + col], sm);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * 4096; e += 256) atomicAdd(&((e >> 12) ? P.gc : P.gv)[e & 4095], red[e]);
+    if (threadIdx.x < 64) {
+        atomicAdd(&P.bv[threadIdx.x], bred[threadIdx.x]);
+        atomicAdd(&P.bc[threadIdx.x], bred[threadIdx.x]);
+    }
+}
+
 // workgroups per CU of the weight-gradient reductions (LDPC_GNN_OUTER_WGS, default 2: 40.1 vs 41.0
 // ms per step at 4 and 43.6 at 8, profiles/r04); read per call
 int outer_wgs() {
@@ -1559,12 +1654,16 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         // weight gradients
         OuterT o{};
         o.H = H; o.E = E; o.R = R;
-        // dW2v and dW2c in two passes over dX: one pass with both (J = 128) needs 128 accumulator
-        // registers, and at one wave per SIMD it ran at 2.9 TB/s against 5.6 TB/s for each of these
-        o.A = w.dX; o.zsrc = w.hv; o.J = H; o.out = Gw[3]; o.bias = Gw[4];
-        if (int rc = launch_outer(o, red_grid, s)) return rc;
-        o.zsrc = w.hc; o.out = Gw[7]; o.bias = Gw[8];
-        if (int rc = launch_outer(o, red_grid, s)) return rc;
+        if (H == 64 && outer_h64()) {  // dW2v and dW2c in one pass over dX
+            Dw2T d2{w.dX, w.hv, w.hc, Gw[3], Gw[7], Gw[4], Gw[8], R};
+            hipLaunchKernelGGL(train_dw2_kernel, dim3(red_grid), dim3(256), 0, s, d2);
+            LDPC_CHECK_LAUNCH("train_dw2_kernel");
+        } else {  // general H: two passes
+            o.A = w.dX; o.zsrc = w.hv; o.J = H; o.out = Gw[3]; o.bias = Gw[4];
+            if (int rc = launch_outer(o, red_grid, s)) return rc;
+            o.zsrc = w.hc; o.out = Gw[7]; o.bias = Gw[8];
+            if (int rc = launch_outer(o, red_grid, s)) return rc;
+        }
         // dW1_s = sum_m dh_s[m] (x) [c_m; g_s(group(m))]: the c half row by row; the group half as
         // sum_groups (sum_{m in group} dh_s[m]) (x) g_s(group) -- contiguous group rows instead of
         // a gathered group row per message (Mda / Mdb are free again after the combine step)
