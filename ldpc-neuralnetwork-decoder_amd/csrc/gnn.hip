@@ -48,6 +48,8 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMfmaH = 64;
+// other hidden widths run on gnn_mlp_generic_kernel: 4 waves x 4 H floats of LDS (64 KB at 1024)
+constexpr int kMaxGenericH = 1024;
 #ifndef LDPC_MLP2_WPS
 #define LDPC_MLP2_WPS 3
 #endif
@@ -990,16 +992,17 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 }
 
 // ------------------------------------------------------------------------ fused MLP, any H
-// one wave per message, lanes = output units (H <= 64 per pass); VALU fp32.
+// one wave per message, lanes = output units (lane, lane + 64, ...); VALU fp32.
 __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H) {
     extern __shared__ __attribute__((aligned(16))) float sh[];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float *in = sh + w * (4 * H);  // [c (H) | a or b (H) | h (H) | spare]
+    float *in = sh + w * (4 * H);  // [c (H) | a or b (H) | h (H) | y (H)]
+    float *y = in + 3 * H;         // both sides' second Linear, summed per unit
     const int64_t R = P.B * P.E;
     for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
         const int64_t b = row / P.E, m = row - b * P.E;
         const int ty = P.msg_type[m];
-        float y[2] = {0.0f, 0.0f};  // units lane and lane + 64
+        for (int o = lane; o < H; o += 64) y[o] = 0.0f;
         for (int side = 0; side < 2; ++side) {
             const float *W1 = side ? P.w1c : P.w1v, *b1 = side ? P.b1c : P.b1v;
             const float *W2 = side ? P.w2c : P.w2v, *b2 = side ? P.b2c : P.b2v;
@@ -1015,16 +1018,16 @@ __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H)
                 in[2 * H + o] = fmaxf(s, 0.0f);
             }
             __builtin_amdgcn_wave_barrier();
-            for (int o = lane, i = 0; o < H; o += 64, ++i) {
+            for (int o = lane; o < H; o += 64) {
                 float s = b2[o];
                 for (int u = 0; u < H; ++u) s += W2[o * H + u] * in[2 * H + u];
-                y[i] += s;
+                y[o] += s;
             }
             __builtin_amdgcn_wave_barrier();
         }
         float part = 0.0f;
-        for (int o = lane, i = 0; o < H; o += 64, ++i) {
-            float v = y[i];
+        for (int o = lane; o < H; o += 64) {
+            float v = y[o];
             if (P.residual) v += P.x_in[row * H + o];
             if (P.last) part += v * P.wo[o];
             if (P.x_out) P.x_out[row * H + o] = v;
@@ -1606,7 +1609,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     L.Mv = w.Mv; L.Mc = w.Mc;
     L.vside = 1;
     const bool mfma = H == kMfmaH;
-    if (!mfma && H > 128) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be 64 (MFMA path) or <= 128");
+    if (!mfma && H > kMaxGenericH) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be <= " + std::to_string(kMaxGenericH));
     const size_t mfma_lds = (size_t)(kOffEmb + types * kEmbStride) * 4;
     if (mfma && mfma_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
     const int mt = mlp_threads();

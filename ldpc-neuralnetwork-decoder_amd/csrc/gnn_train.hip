@@ -20,10 +20,11 @@
 //          (the group-mean operator is symmetric, so its transpose is itself)
 //     demb[t] += dc;  dx_l = dc (+ dX if l > 0);   layer 0: dw_in += dc llr, db_in += dc
 //
-// Kernels (lanes = hidden units, H <= 64; VALU fp32 -- a training batch is small next to the
-// decode batches, and every product is an exact fp32 fma chain):
+// Kernels (lanes = hidden units, looping over units past 64; VALU fp32 -- a training batch is small
+// next to the decode batches, and every product is an exact fp32 fma chain):
 //   train_group_mean_kernel  group means of c (or of any (B, E, H) array), one wave per group
 //   train_mlp_bwd_kernel     recompute u, h; dh, dz; writes c, h_v, h_c, dh_v, dh_c, dz parts
+//   train_mlp_bwd_wide_kernel  the same for H > 64 (weights read through the caches, not LDS)
 //   train_mlp_bwd_mfma_kernel  the same for H = 64 on fp32 MFMA (default; bit-for-bit fmaf chains
 //                            in a different summation order than the VALU kernel)
 //   train_combine_kernel     dc and dx_l
@@ -39,7 +40,8 @@
 namespace ldpc {
 namespace {
 
-constexpr int kMaxH = 64;
+constexpr int kMaxH = 64;         // widest H of the LDS-image kernels (train_mlp_bwd_kernel, train_outer_kernel)
+constexpr int kMaxTrainH = 1024;  // widest H trained (train_mlp_bwd_wide_kernel's per-wave LDS rows)
 
 struct TW {  // one layer's weights in the blob (see ldpc_amd.h)
     const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
@@ -122,13 +124,14 @@ __device__ __forceinline__ float c_value(const GmT &A, int64_t b, int64_t m, int
 
 __global__ __launch_bounds__(256) void train_group_mean_kernel(GmT A) {
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int u = threadIdx.x & 63;
-    if (w >= A.B * A.G || u >= A.H) return;
+    if (w >= A.B * A.G) return;
     const int64_t b = w / A.G;
     const int g = (int)(w - b * A.G);
-    float s = 0.0f;
-    for (int q = A.ptr[g]; q < A.ptr[g + 1]; ++q) s += c_value(A, b, A.mem[q], u);
-    A.dst[w * A.H + u] = A.sum_only ? s : s * A.inv[g];
+    for (int u = threadIdx.x & 63; u < A.H; u += 64) {
+        float s = 0.0f;
+        for (int q = A.ptr[g]; q < A.ptr[g + 1]; ++q) s += c_value(A, b, A.mem[q], u);
+        A.dst[w * A.H + u] = A.sum_only ? s : s * A.inv[g];
+    }
 }
 
 // H = 64: 16 lanes per group (float4 each), 4 groups per wave, members unrolled by 4 (the
@@ -311,6 +314,122 @@ __global__ __launch_bounds__(256) void train_mlp_bwd_kernel(MlpT A) {
             for (int q = 0; q < H; ++q) {
                 const float wv0 = W1v[q * S1 + u], wv1 = W1v[q * S1 + H + u];
                 const float wc0 = W1c[q * S1 + u], wc1 = W1c[q * S1 + H + u];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    const float dv = dh[(i * 2) * H + q], dc = dh[(i * 2 + 1) * H + q];
+                    zv0[i] = fmaf(wv0, dv, zv0[i]);
+                    zv1[i] = fmaf(wv1, dv, zv1[i]);
+                    zc0[i] = fmaf(wc0, dc, zc0[i]);
+                    zc1[i] = fmaf(wc1, dc, zc1[i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) {
+                const int64_t r = r0 + i;
+                if (r < A.R) {
+                    A.dco[r * H + u] = zv0[i] + zc0[i];
+                    A.da[r * H + u] = zv1[i];
+                    A.db[r * H + u] = zc1[i];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// H > 64: the same products and fma order as train_mlp_bwd_kernel (lanes = units, each lane
+// looping over units lane, lane + 64, ...), with the weights read from global memory -- the
+// [H][2H + 1] LDS image stops fitting past H = 64 -- and only the per-wave rows in LDS: c | a | q,
+// dX and dh of kNM rows (24 H floats per wave).  GEMM2' and GEMM3' read W rows across the lanes
+// (coalesced); GEMM1 walks each lane's own W1 row (one cache line per lane per 32 k).
+inline size_t mlp_bwd_wide_lds(int H, int waves) { return (size_t)waves * kNM * 6 * H * 4; }
+
+__global__ __launch_bounds__(256) void train_mlp_bwd_wide_kernel(MlpT A) {
+    extern __shared__ float sm[];
+    const int H = A.H, H2 = 2 * H, nw = blockDim.x >> 6;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *z = sm + wave * kNM * 6 * H, *dXs = z + kNM * 3 * H, *dh = dXs + kNM * H;
+    const int64_t step = (int64_t)gridDim.x * nw * kNM;
+    for (int64_t r0 = ((int64_t)blockIdx.x * nw + wave) * kNM; r0 - wave * kNM < A.R; r0 += step) {
+        for (int u = lane; u < H; u += 64) {
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) {
+                const int64_t r = r0 + i;
+                if (r < A.R) {
+                    const int64_t b = r / A.E, m = r - b * A.E;
+                    const float c = (A.x ? A.x[r * H + u] : A.w_in[u] * A.llr[b * A.N + A.msg_var[m]] + A.b_in[u]) +
+                                    A.emb[A.msg_type[m] * H + u];
+                    z[i * 3 * H + u] = c;
+                    z[i * 3 * H + H + u] = A.Mv[(b * A.Gv + A.vgroup[m]) * H + u];
+                    z[i * 3 * H + H2 + u] = A.Mc[(b * A.Gc + A.cgroup[m]) * H + u];
+                    dXs[i * H + u] = A.dX[r * H + u];
+                    A.cbuf[r * H + u] = c;
+                } else {
+                    z[i * 3 * H + u] = z[i * 3 * H + H + u] = z[i * 3 * H + H2 + u] = 0.0f;
+                    dXs[i * H + u] = 0.0f;
+                }
+            }
+        }
+        __syncthreads();
+        for (int u = lane; u < H; u += 64) {
+            // u_s = W1s [c; g_s] + b1s (row u of W1s)
+            float uv[kNM], uc[kNM];
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) { uv[i] = A.b1v[u]; uc[i] = A.b1c[u]; }
+            const float *w1v = A.w1v + (int64_t)u * H2, *w1c = A.w1c + (int64_t)u * H2;
+            for (int k = 0; k < H; ++k) {
+                const float wv = w1v[k], wc = w1c[k];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    const float c = z[i * 3 * H + k];
+                    uv[i] = fmaf(wv, c, uv[i]);
+                    uc[i] = fmaf(wc, c, uc[i]);
+                }
+            }
+            for (int k = 0; k < H; ++k) {
+                const float wv = w1v[H + k], wc = w1c[H + k];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    uv[i] = fmaf(wv, z[i * 3 * H + H + k], uv[i]);
+                    uc[i] = fmaf(wc, z[i * 3 * H + H2 + k], uc[i]);
+                }
+            }
+            // dh_s = (W2s^T dX) * [u_s > 0] (column u of W2s)
+            float gv[kNM], gc[kNM];
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) gv[i] = gc[i] = 0.0f;
+            for (int o = 0; o < H; ++o) {
+                const float wv = A.w2v[(int64_t)o * H + u], wc = A.w2c[(int64_t)o * H + u];
+#pragma unroll
+                for (int i = 0; i < kNM; ++i) {
+                    const float d = dXs[i * H + o];
+                    gv[i] = fmaf(wv, d, gv[i]);
+                    gc[i] = fmaf(wc, d, gc[i]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) {
+                const int64_t r = r0 + i;
+                const float dv = uv[i] > 0.0f ? gv[i] : 0.0f, dc = uc[i] > 0.0f ? gc[i] : 0.0f;
+                dh[(i * 2) * H + u] = dv;
+                dh[(i * 2 + 1) * H + u] = dc;
+                if (r < A.R) {
+                    A.hv[r * H + u] = fmaxf(uv[i], 0.0f);
+                    A.hc[r * H + u] = fmaxf(uc[i], 0.0f);
+                    A.dhv[r * H + u] = dv;
+                    A.dhc[r * H + u] = dc;
+                }
+            }
+        }
+        __syncthreads();
+        for (int u = lane; u < H; u += 64) {
+            // dz_s[k] = sum_q W1s[q][k] dh_s[q] for k = u (c part) and k = H + u (group part)
+            float zv0[kNM], zv1[kNM], zc0[kNM], zc1[kNM];
+#pragma unroll
+            for (int i = 0; i < kNM; ++i) zv0[i] = zv1[i] = zc0[i] = zc1[i] = 0.0f;
+            for (int q = 0; q < H; ++q) {
+                const float *rv = A.w1v + (int64_t)q * H2, *rc = A.w1c + (int64_t)q * H2;
+                const float wv0 = rv[u], wv1 = rv[H + u], wc0 = rc[u], wc1 = rc[H + u];
 #pragma unroll
                 for (int i = 0; i < kNM; ++i) {
                     const float dv = dh[(i * 2) * H + q], dc = dh[(i * 2 + 1) * H + q];
@@ -710,6 +829,9 @@ struct OuterT {
     int H, J, Gn;
     int ld = 0, col0 = 0;  // out[i * ld + col0 + j] (ld 0 = J): one half of a [H][2H] gradient
     int64_t E, R;
+    // one output tile (H > 64 or J > 128, see launch_outer): rows i0 .. i0 + ni of the gradient,
+    // columns j0 .. j0 + nj of Z (ni / nj 0: all H / J)
+    int i0 = 0, j0 = 0, ni = 0, nj = 0;
 };
 constexpr int kRB = 16;  // rows staged per step
 
@@ -783,6 +905,8 @@ template <int NIT, int NJT, bool H64 = false>
 __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     const int lane = threadIdx.x & 63, col = lane & 31, k = lane >> 5;
     const int H = H64 ? 64 : P.H, J = H64 ? 32 * NJT : P.J;
+    const int NI = H64 ? 64 : P.ni ? P.ni : H, NJ = H64 ? J : P.nj ? P.nj : J;  // this tile's extent
+    const int i0 = H64 ? 0 : P.i0, j0 = H64 ? 0 : P.j0;
     const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t per = ((P.R + nw - 1) / nw + 1) & ~1LL;  // even: whole k-steps
     const int64_t r_begin = w * per, r_end = r_begin + per < P.R ? r_begin + per : P.R;
@@ -794,7 +918,8 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     float bsum[NIT] = {};
     auto zval = [&](int64_t r, int64_t b, int64_t m, int j) -> float {
         if constexpr (H64) return P.zsrc[r * 64 + j];
-        if (j >= J) return 0.0f;
+        if (j >= NJ) return 0.0f;
+        j += j0;
         if (j < H) return P.zsrc[r * H + j];
         return P.G[(b * P.Gn + P.grp[m]) * H + (j - H)];
     };
@@ -815,7 +940,7 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
                 const int i = 32 * it + col;
-                B.a[u][it] = ok && (H64 || i < H) ? P.A[r * H + i] : 0.0f;
+                B.a[u][it] = ok && (H64 || i < NI) ? P.A[r * H + i0 + i] : 0.0f;
             }
 #pragma unroll
             for (int jt = 0; jt < NJT; ++jt) B.z[u][jt] = ok ? zval(r, bu, mu, 32 * jt + col) : 0.0f;
@@ -910,11 +1035,11 @@ __global__ __launch_bounds__(256) void train_outer_mfma_kernel(OuterT P) {
     __syncthreads();
     for (int e = threadIdx.x; e < NIT * 32 * NJT * 32; e += 256) {
         const int i = e / (NJT * 32), j = e - i * (NJT * 32);
-        if (i < H && j < J) {
-            atomicAdd(&P.out[i * (P.ld ? P.ld : J) + P.col0 + j], red[e]);
+        if (i < NI && j < NJ) {
+            atomicAdd(&P.out[(i0 + i) * (P.ld ? P.ld : J) + P.col0 + j0 + j], red[e]);
         }
     }
-    if (P.bias && threadIdx.x < H) atomicAdd(&P.bias[threadIdx.x], bred[threadIdx.x]);
+    if (P.bias && threadIdx.x < NI) atomicAdd(&P.bias[i0 + threadIdx.x], bred[threadIdx.x]);
 }
 
 // dW1_left of both sides in one pass over the rows (H = 64, projected-group backward):
@@ -1168,6 +1293,26 @@ int outer_wgs() {
 }
 
 int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
+    if (o.H > 64 || o.J > 128) {  // tiles of 64 gradient rows x 128 Z columns, one launch each
+        for (int i0 = 0; i0 < o.H; i0 += 64)
+            for (int j0 = 0; j0 < o.J; j0 += 128) {
+                OuterT t = o;
+                t.i0 = i0; t.ni = std::min(64, o.H - i0);
+                t.j0 = j0; t.nj = std::min(128, o.J - j0);
+                if (j0) t.bias = nullptr;  // the bias sums once per gradient row
+                const int nit = (t.ni + 31) / 32, njt = (t.nj + 31) / 32;
+                if (nit == 2 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4>), dim3(grid), dim3(256), 0, s, t);
+                else if (nit == 2 && njt == 3) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 3>), dim3(grid), dim3(256), 0, s, t);
+                else if (nit == 2 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2>), dim3(grid), dim3(256), 0, s, t);
+                else if (nit == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 1>), dim3(grid), dim3(256), 0, s, t);
+                else if (njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<1, 4>), dim3(grid), dim3(256), 0, s, t);
+                else if (njt == 3) hipLaunchKernelGGL((train_outer_mfma_kernel<1, 3>), dim3(grid), dim3(256), 0, s, t);
+                else if (njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<1, 2>), dim3(grid), dim3(256), 0, s, t);
+                else hipLaunchKernelGGL((train_outer_mfma_kernel<1, 1>), dim3(grid), dim3(256), 0, s, t);
+                LDPC_CHECK_LAUNCH("train_outer_mfma_kernel (tile)");
+            }
+        return LDPC_OK;
+    }
     const int nit = (o.H + 31) / 32, njt = (o.J + 31) / 32;
     // H = 64 from plain row sources: the specialised kernels (no per-load source / bounds checks)
     const bool h64 = o.H == 64 && !o.G && o.J == 64 && outer_h64();
@@ -1240,26 +1385,24 @@ template <int MODE>
 __global__ __launch_bounds__(256) void train_vecfinal_kernel(VecT P, const float *__restrict__ S0,
                                                              const float *__restrict__ S1) {
     extern __shared__ float acc[];
-    const int u = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool on = u < P.H;
+    const int w = threadIdx.x >> 6;
     const int n = MODE == 0 ? P.T * P.H : 2 * 4 * P.H;
     for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.0f;
     __syncthreads();
     const int64_t m0 = (int64_t)blockIdx.x * kChunkV, m1 = min<int64_t>(m0 + kChunkV, P.E);
-    float a0 = 0.0f, a1 = 0.0f;
+    for (int u = threadIdx.x & 63; u < P.H; u += 64) {  // lanes = units (and + 64, ... past 64)
+        float a0 = 0.0f, a1 = 0.0f;
 #pragma unroll 8
-    for (int64_t m = m0 + w; m < m1; m += 4) {
-        if (!on) continue;
-        const float v = S0[m * P.H + u];
-        if constexpr (MODE == 0) {
-            atomicAdd(&acc[P.msg_type[m] * P.H + u], v);
-        } else {
-            a0 += v;
-            a1 += S1[m * P.H + u];
+        for (int64_t m = m0 + w; m < m1; m += 4) {
+            const float v = S0[m * P.H + u];
+            if constexpr (MODE == 0) {
+                atomicAdd(&acc[P.msg_type[m] * P.H + u], v);
+            } else {
+                a0 += v;
+                a1 += S1[m * P.H + u];
+            }
         }
-    }
-    if constexpr (MODE != 0) {
-        if (on) {
+        if constexpr (MODE != 0) {
             acc[w * P.H + u] = a0;
             acc[(4 + w) * P.H + u] = a1;
         }
@@ -1271,7 +1414,8 @@ __global__ __launch_bounds__(256) void train_vecfinal_kernel(VecT P, const float
             if (part) P.part[(int64_t)blockIdx.x * n + i] = acc[i];
             else if (acc[i] != 0.0f) atomicAdd(&P.g0[i], acc[i]);
         }
-    } else if (w == 0 && on) {
+    } else if (w == 0) {
+      for (int u = threadIdx.x; u < P.H; u += 64) {
         const float s0 = ((acc[u] + acc[P.H + u]) + acc[2 * P.H + u]) + acc[3 * P.H + u];
         const float s1 = ((acc[4 * P.H + u] + acc[5 * P.H + u]) + acc[6 * P.H + u]) + acc[7 * P.H + u];
         if (part) {
@@ -1282,6 +1426,7 @@ __global__ __launch_bounds__(256) void train_vecfinal_kernel(VecT P, const float
             if (MODE == 1) atomicAdd(&P.g1[u], s1);
             else if (u == 0) atomicAdd(&P.g1[0], s1);  // dbo: S1 is the same for every unit
         }
+      }
     }
 }
 
@@ -1425,8 +1570,8 @@ int bwd_mfma() {
 using namespace ldpc;
 
 extern "C" int64_t ldpc_gnn_train_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers) {
-    if (!p || hidden <= 0 || hidden > kMaxH || N <= 0 || B < 0 || layers <= 0)
-        return fail(LDPC_EINVAL, "bad arguments (training needs hidden_dim <= 64)");
+    if (!p || hidden <= 0 || hidden > kMaxTrainH || N <= 0 || B < 0 || layers <= 0)
+        return fail(LDPC_EINVAL, "bad arguments (training needs hidden_dim <= 1024)");
     const int64_t fwd = ldpc_gnn_workspace_size(p, hidden, N, B, layers, 0);
     const int64_t bwd = carve_train(p, hidden, N, B, nullptr).bytes;
     return fwd > bwd ? fwd : bwd;
@@ -1438,8 +1583,8 @@ extern "C" int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int ty
                                       void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
-    if (hidden <= 0 || hidden > kMaxH || types <= 0 || layers <= 0 || N <= 0 || B < 0)
-        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 64)");
+    if (hidden <= 0 || hidden > kMaxTrainH || types <= 0 || layers <= 0 || N <= 0 || B < 0)
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 1024)");
     if (B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_saved)
         return fail(LDPC_EINVAL, "NULL tensor");
@@ -1456,8 +1601,8 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     const int H = hidden, T = types, L = layers;
-    if (H <= 0 || H > kMaxH || T <= 0 || L <= 0 || N <= 0 || B < 0)
-        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 64)");
+    if (H <= 0 || H > kMaxTrainH || T <= 0 || L <= 0 || N <= 0 || B < 0)
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 1024)");
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_grad_probs || !d_saved || !d_grad_weights)
         return fail(LDPC_EINVAL, "NULL tensor");
     if ((d_layer_probs == nullptr) != (d_grad_layer_probs == nullptr))
@@ -1477,8 +1622,16 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
     }
     const int64_t E = p->E, R = B * E, n = R * H;
     const size_t lds_mlp = mlp_bwd_lds(H);
-    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_kernel),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_mlp));
+    // H > 64: train_mlp_bwd_wide_kernel with as many waves per workgroup (<= 4) as its LDS rows allow
+    const int wide_waves = (int)std::max<size_t>(1, std::min<size_t>(4, (size_t)(160 * 1024) / mlp_bwd_wide_lds(H, 1)));
+    if (H > kMaxH) {
+        if (mlp_bwd_wide_lds(H, 1) > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "hidden_dim too wide for the backward's LDS rows");
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_wide_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_wide_lds(H, wide_waves)));
+    } else {
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_mlp));
+    }
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<512>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<256>),
@@ -1609,6 +1762,12 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
             else
                 hipLaunchKernelGGL(train_mlp_bwd_mfma_kernel<512>, dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);
             LDPC_CHECK_LAUNCH("train_mlp_bwd_mfma_kernel");
+        } else if (H > kMaxH) {
+            const int rows = wide_waves * kNM;
+            const unsigned mgrid = (unsigned)std::min<int64_t>((R + rows - 1) / rows, (int64_t)g_cus_t * 8 / wide_waves);
+            hipLaunchKernelGGL(train_mlp_bwd_wide_kernel, dim3(mgrid), dim3(64 * wide_waves), mlp_bwd_wide_lds(H, wide_waves),
+                               s, m);
+            LDPC_CHECK_LAUNCH("train_mlp_bwd_wide_kernel");
         } else {
             const unsigned mgrid = (unsigned)std::min<int64_t>((R + 4 * kNM - 1) / (4 * kNM), (int64_t)g_cus_t * 2);
             hipLaunchKernelGGL(train_mlp_bwd_kernel, dim3(mgrid), dim3(256), lds_mlp, s, m);
@@ -1760,7 +1919,7 @@ extern "C" int ldpc_gnn_layer_probs(const ldpc_gnn_plan *p, int hidden, int type
                                     void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     const int H = hidden, T = types, L = layers;
-    if (H <= 0 || H > kMaxH || T <= 0 || L <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
+    if (H <= 0 || H > kMaxTrainH || T <= 0 || L <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
     if (L < 2 || B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_var || !d_llr || !d_saved || !d_layer_probs) return fail(LDPC_EINVAL, "NULL tensor");
     const int64_t E = p->E, R = B * E, mo = (R + 63) / 64 * 64;

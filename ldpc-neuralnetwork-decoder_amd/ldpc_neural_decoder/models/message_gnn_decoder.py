@@ -365,8 +365,8 @@ class _NativeGnnTrain(torch.autograd.Function):
         dev = llr.device
         H, L = dec.hidden_dim, len(dec.gnn_layers)
         T = dec.gnn_layers[0].message_type_embeddings.shape[0]
-        if H > 64:
-            raise NotImplementedError("the native backward supports hidden_dim <= 64")
+        if H > 1024:
+            raise NotImplementedError("the native backward supports hidden_dim <= 1024")
         B, Nv = llr.shape
         E = dec.num_messages
         blob = torch.cat([p.detach().reshape(-1).to(dev, torch.float32) for p in params]).contiguous()
