@@ -262,6 +262,14 @@ int ldpc_gather_minsum_backward(const float *d_grad_out, const float *d_in, int6
                                 float *d_grad_in, void *stream);
 int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t B, int n_in, const int32_t *d_idx,
                     int n_out, int K, float *d_out, void *stream);
+/* ldpc_var_groups_sum: the same VariableLayer outputs (layers.py:78-125) when the index is a set of
+ * contiguous variable groups -- every edge's row holds exactly the other edges of its variable in
+ * ascending order, and each variable's edges are a run [gptr[g], gptr[g + 1]) tiling [0, n)
+ * (n_in == n_out == n), as create_LLR_mapping builds it.  Sums in the row's order, bit-identical
+ * to ldpc_gather_sum.  d_out must not alias d_msgs or d_llr.  LDPC_EUNSUPPORTED when a row does
+ * not fit LDS. */
+int ldpc_var_groups_sum(const float *d_llr, const float *d_msgs, int64_t B, int n, const int32_t *d_gptr, int G,
+                        float *d_out, void *stream);
 int ldpc_gather_sum_backward(const float *d_grad_out, int64_t B, int n_in, const int32_t *d_idx, int n_out,
                              int K, float *d_grad_msgs, void *stream);
 int ldpc_residual(const float *d_llr, const float *d_w_ch, const float *d_cm, const float *d_w_res,

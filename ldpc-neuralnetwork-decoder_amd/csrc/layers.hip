@@ -217,6 +217,132 @@ __global__ __launch_bounds__(512) void check_group_kernel(const float *__restric
     }
 }
 
+// VariableLayer when its (compacted) index is a set of contiguous variable groups (every edge's row
+// = the other edges of its variable, ascending, as create_LLR_mapping builds it; detected once in
+// Python): out[b][i] = llr[b][i] + the sum of the other members in ascending order --
+// gather_sum_kernel's sequence, so the same bits.  The frame row is staged in LDS; per (group,
+// frame) one thread walks the members in order, keeping the running prefix P_q = m_s + ... + m_{q-1}
+// (the fold every later member starts from) and adding each member's tail, and writes member q's
+// sum over m_q in place (the prefix has already taken m_q, and later tails read only members past
+// q).  Then the row goes out coalesced with the LLR added (llr + sum).  The gathered kernel re-read
+// every group member from global memory per edge and frame (address-bound at 1.7 TB/s).  Measured
+// and not kept: one thread per edge (its run bounds or check list through dependent global loads
+// per frame: slower), and a persistent double-buffered walk over frames (the degree-23 runs' serial
+// chains then sit on every frame's critical path: -24 %).
+__global__ __launch_bounds__(512) void var_group_sum_kernel(const float *__restrict__ llr, const float *__restrict__ in,
+                                                            int64_t B, int n, const int32_t *__restrict__ gptr, int G,
+                                                            float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float rows[];  // [n]
+    const int64_t b = blockIdx.x;
+    const bool vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(in + b * n) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(out + b * n) & 15) == 0 &&
+                     (!llr || (reinterpret_cast<uintptr_t>(llr + b * n) & 15) == 0);
+    if (vec) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(in + b * n);
+        float4 *r4 = reinterpret_cast<float4 *>(rows);
+        for (int e = threadIdx.x; e < n / 4; e += blockDim.x) r4[e] = s4[e];
+    } else {
+        for (int e = threadIdx.x; e < n; e += blockDim.x) rows[e] = in[b * n + e];
+    }
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        const int s0 = gptr[g], s1 = gptr[g + 1];
+        float P = 0.0f;
+        for (int q = s0; q < s1; ++q) {
+            const float mq = rows[q];
+            float s = P;
+            for (int t = q + 1; t < s1; ++t) s += rows[t];
+            rows[q] = s;
+            P += mq;
+        }
+    }
+    __syncthreads();
+    if (vec) {
+        const float4 *r4 = reinterpret_cast<const float4 *>(rows);
+        float4 *o4 = reinterpret_cast<float4 *>(out + b * n);
+        const float4 *l4 = reinterpret_cast<const float4 *>(llr + b * n);
+        for (int e = threadIdx.x; e < n / 4; e += blockDim.x) {
+            const float4 s = r4[e];
+            if (llr) {
+                const float4 l = l4[e];
+                o4[e] = make_float4(l.x + s.x, l.y + s.y, l.z + s.z, l.w + s.w);
+            } else {
+                o4[e] = s;
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < n; e += blockDim.x) out[b * n + e] = llr ? llr[b * n + e] + rows[e] : rows[e];
+    }
+}
+
+// check_group_kernel with the check lists in LDS (default): gptr / gmem staged once per workgroup as
+// 16-bit words (n < 65536), then F = 4 frames in turn (row in, checks in place, row out).  The
+// per-frame kernel's per-member index loads came from global memory, one dependent load per member
+// and pass: 93 -> 83 us per BG2 Z = 32 call at B = 4096, +3.6 % on lay-z32 (F = 1 / 2: +3.4 %).
+// Measured and not kept: the member indices in registers (-30 %), one thread per edge over its
+// check's list (-120 %), a persistent double-buffered walk (-85 %).
+template <int F>
+__global__ __launch_bounds__(512) void check_group_idx_kernel(const float *__restrict__ in, int64_t B, int n,
+                                                              const int32_t *__restrict__ gptr,
+                                                              const int32_t *__restrict__ gmem, int G, int K,
+                                                              float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float rows[];  // [n] row | [n] u16 gmem | [G + 1] u16 gptr
+    uint16_t *gm = reinterpret_cast<uint16_t *>(rows + ((n + 3) & ~3)), *gp = gm + ((n + 7) & ~7);
+    for (int e = threadIdx.x; e < n; e += blockDim.x) gm[e] = (uint16_t)gmem[e];
+    for (int e = threadIdx.x; e <= G; e += blockDim.x) gp[e] = (uint16_t)gptr[e];
+    const bool vec0 = (n & 3) == 0;
+    for (int f = 0; f < F; ++f) {
+        const int64_t b = (int64_t)blockIdx.x * F + f;
+        if (b >= B) break;
+        const bool vec = vec0 && (reinterpret_cast<uintptr_t>(in + b * n) & 15) == 0 &&
+                         (reinterpret_cast<uintptr_t>(out + b * n) & 15) == 0;
+        if (vec) {
+            const float4 *s4 = reinterpret_cast<const float4 *>(in + b * n);
+            float4 *r4 = reinterpret_cast<float4 *>(rows);
+            for (int e = threadIdx.x; e < n / 4; e += blockDim.x) r4[e] = s4[e];
+        } else {
+            for (int e = threadIdx.x; e < n; e += blockDim.x) rows[e] = in[b * n + e];
+        }
+        __syncthreads();
+        for (int g = threadIdx.x; g < G; g += blockDim.x) {
+            const int p0 = gp[g], p1 = gp[g + 1];
+            int zeros = 0, nans = 0, neg = 0, pos = -1;
+            float m1 = INFINITY, m2 = INFINITY;
+            for (int p = p0; p < p1; ++p) {
+                const float v = rows[gm[p]];
+                const float sv = v + 1e-10f;
+                zeros += sv == 0.0f;
+                nans += sv != sv;
+                neg ^= sv < 0.0f;
+                float a = fabsf(v);
+                if (a == 0.0f) a = 1e10f;
+                if (a < m1) { m2 = m1; m1 = a; pos = p; }
+                else if (a < m2) m2 = a;
+            }
+            const bool pad = K > p1 - p0 - 1;
+            for (int p = p0; p < p1; ++p) {
+                const int j = gm[p];
+                const float v = rows[j];
+                const float sv = v + 1e-10f;
+                const int z = zeros - (sv == 0.0f), nn = nans - (sv != sv), ng = neg ^ (sv < 0.0f);
+                float m = p == pos ? m2 : m1;
+                if (pad) m = fminf(m, 1e10f);
+                const float sp = z > 0 ? (ng ? -0.0f : 0.0f) : (ng ? -1.0f : 1.0f);
+                rows[j] = nn > 0 ? __builtin_nanf("") : sp * m;
+            }
+        }
+        __syncthreads();
+        if (vec) {
+            const float4 *r4 = reinterpret_cast<const float4 *>(rows);
+            float4 *o4 = reinterpret_cast<float4 *>(out + b * n);
+            for (int e = threadIdx.x; e < n / 4; e += blockDim.x) o4[e] = r4[e];
+        } else {
+            for (int e = threadIdx.x; e < n; e += blockDim.x) out[b * n + e] = rows[e];
+        }
+        __syncthreads();  // the row buffer is reused by the next frame
+    }
+}
+
 bool gather_lds_enabled() {
     static const bool on = [] {
         const char *e = std::getenv("LDPC_GATHER_LDS");
@@ -308,6 +434,26 @@ __global__ void residual_kernel(ResArgs A, float *__restrict__ out) {
     r = r + A.cm[t];
     for (int i = 0; i < A.D; ++i) r = r + A.w_res[i] * A.prev[i][t];
     out[t] = r;
+}
+
+// the same per element, n % 4 == 0 and 16-byte aligned rows: one float4 per thread, frames on
+// blockIdx.y (no 64-bit modulo per element; 114 -> 95 us per BG2 Z = 32 call at B = 4096)
+template <int D>
+__global__ void residual4_kernel(ResArgs A, float *__restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, n4 = A.n >> 2;
+    if (c >= n4) return;
+    const int64_t t = (int64_t)blockIdx.y * n4 + c;
+    const float4 l = reinterpret_cast<const float4 *>(A.llr)[t], w = reinterpret_cast<const float4 *>(A.w_ch)[c];
+    const float4 m = reinterpret_cast<const float4 *>(A.cm)[t];
+    float4 r = make_float4(l.x * w.x, l.y * w.y, l.z * w.z, l.w * w.w);
+    r = make_float4(r.x + m.x, r.y + m.y, r.z + m.z, r.w + m.w);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        const float wr = A.w_res[i];
+        const float4 p = reinterpret_cast<const float4 *>(A.prev[i])[t];
+        r = make_float4(r.x + wr * p.x, r.y + wr * p.y, r.z + wr * p.z, r.w + wr * p.w);
+    }
+    reinterpret_cast<float4 *>(out)[t] = r;
 }
 
 // grads: g_cm = g; g_prev_i = w_res[i] g; g_w_ch[n] = sum_b g llr; g_w_res[i] = sum g prev_i
@@ -440,6 +586,23 @@ extern "C" int ldpc_check_groups_minsum(const float *d_in, int64_t B, int n, con
     }();
     // one frame per workgroup by default: 4 workgroups per CU overlap staging with compute
     // (+1.8 % on lay-z32 over 2 frames; 4 frames, one workgroup per CU, -19 %)
+    static const int idx_f = [] {  // LDPC_CHECK_IDX_F=0: the per-frame kernel (A/B); 1 / 2 / 4 frames per workgroup
+        const char *e = std::getenv("LDPC_CHECK_IDX_F");
+        return e ? std::atoi(e) : 4;
+    }();
+    if (idx_f > 0 && n < 65536 && G < 65536) {
+        const size_t lds = ((size_t)((n + 3) & ~3)) * 4 + ((size_t)((n + 7) & ~7) + G + 1) * 2;
+        if (lds <= 64 * 1024) {
+            hipStream_t s = static_cast<hipStream_t>(stream);
+            const int F = idx_f >= 4 ? 4 : idx_f >= 2 ? 2 : 1;
+            const dim3 grid((unsigned)((B + F - 1) / F));
+            if (F == 4) hipLaunchKernelGGL(check_group_idx_kernel<4>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out);
+            else if (F == 2) hipLaunchKernelGGL(check_group_idx_kernel<2>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out);
+            else hipLaunchKernelGGL(check_group_idx_kernel<1>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out);
+            LDPC_CHECK_LAUNCH("check_group_idx_kernel");
+            return LDPC_OK;
+        }
+    }
     int fpw = gather_fpw(n) ? 1 : 0;
     if (fpw && (fpw_env == 1 || fpw_env == 2 || fpw_env == 4 || fpw_env == 8) &&
         (size_t)fpw_env * n * 4 <= 160 * 1024)
@@ -500,6 +663,20 @@ extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t 
     return LDPC_OK;
 }
 
+extern "C" int ldpc_var_groups_sum(const float *d_llr, const float *d_msgs, int64_t B, int n, const int32_t *d_gptr,
+                                   int G, float *d_out, void *stream) {
+    if (B < 0 || n <= 0 || G <= 0) return fail(LDPC_EINVAL, "bad variable-group dimensions");
+    if (!B) return LDPC_OK;
+    if (!d_msgs || !d_gptr || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
+    if (d_out == d_msgs || (d_llr && d_out == d_llr)) return fail(LDPC_EINVAL, "output aliases an input");
+    const size_t lds = (size_t)n * 4;  // one frame per workgroup (staging overlaps across workgroups)
+    if (lds > 64 * 1024) return fail(LDPC_EUNSUPPORTED, "variable-group rows do not fit LDS");
+    hipLaunchKernelGGL(var_group_sum_kernel, dim3((unsigned)B), dim3(512), lds, static_cast<hipStream_t>(stream), d_llr,
+                       d_msgs, B, n, d_gptr, G, d_out);
+    LDPC_CHECK_LAUNCH("var_group_sum_kernel");
+    return LDPC_OK;
+}
+
 extern "C" int ldpc_gather_sum_backward(const float *d_grad_out, int64_t B, int n_in, const int32_t *d_idx, int n_out,
                                         int K, float *d_grad_msgs, void *stream) {
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
@@ -520,7 +697,24 @@ extern "C" int ldpc_residual(const float *d_llr, const float *d_w_ch, const floa
     ResArgs A{};
     A.llr = d_llr; A.w_ch = d_w_ch; A.cm = d_cm; A.w_res = d_w_res; A.D = depth; A.n = n; A.total = B * n;
     for (int i = 0; i < depth; ++i) A.prev[i] = h_prev[i];
-    hipLaunchKernelGGL(residual_kernel, grid_for(A.total), dim3(256), 0, static_cast<hipStream_t>(stream), A, d_out);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    bool vec = (n & 3) == 0 && B <= 65535;
+    for (const void *q : {(const void *)d_llr, (const void *)d_w_ch, (const void *)d_cm, (const void *)d_out})
+        vec = vec && (reinterpret_cast<uintptr_t>(q) & 15) == 0;
+    for (int i = 0; i < depth; ++i) vec = vec && (reinterpret_cast<uintptr_t>(h_prev[i]) & 15) == 0;
+    if (vec && depth <= 4) {
+        const dim3 grid((unsigned)((n / 4 + 255) / 256), (unsigned)B);
+        switch (depth) {
+            case 0: hipLaunchKernelGGL(residual4_kernel<0>, grid, dim3(256), 0, s, A, d_out); break;
+            case 1: hipLaunchKernelGGL(residual4_kernel<1>, grid, dim3(256), 0, s, A, d_out); break;
+            case 2: hipLaunchKernelGGL(residual4_kernel<2>, grid, dim3(256), 0, s, A, d_out); break;
+            case 3: hipLaunchKernelGGL(residual4_kernel<3>, grid, dim3(256), 0, s, A, d_out); break;
+            default: hipLaunchKernelGGL(residual4_kernel<4>, grid, dim3(256), 0, s, A, d_out); break;
+        }
+        LDPC_CHECK_LAUNCH("residual4_kernel");
+        return LDPC_OK;
+    }
+    hipLaunchKernelGGL(residual_kernel, grid_for(A.total), dim3(256), 0, s, A, d_out);
     LDPC_CHECK_LAUNCH("residual_kernel");
     return LDPC_OK;
 }

@@ -57,6 +57,7 @@ SIGNATURES = {
                                                    _P, _P]),
     "ldpc_check_groups_minsum": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
     "ldpc_gather_sum": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
+    "ldpc_var_groups_sum": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int, _P, ctypes.c_int, _P, _P]),
     "ldpc_gather_sum_backward": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _P]),
     "ldpc_residual": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int, _I64, ctypes.c_int, _P, _P]),
     "ldpc_residual_backward": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int, _I64, ctypes.c_int, _P, _P, _P, _P,

@@ -88,6 +88,62 @@ def _check_groups(idx, n_in):
     return res
 
 
+_VGROUPS = {}  # (prepared index identity, n_in) -> gptr device int32, or None
+
+
+def _var_groups(idx, n_in):
+    """Variable groups of a prepared (compacted) VariableLayer index, or None: usable when every
+    row i holds exactly the other members of a run [s, s + d) containing i, in ascending order, and
+    the runs tile [0, n) -- the structure create_LLR_mapping gives (each edge's row = the other
+    edges of its variable, variable-major edge numbering).  Then summing a row in order equals
+    ldpc_var_groups_sum's prefix-and-tail walk bit for bit.  Returns gptr (G + 1) int32."""
+    key = (id(idx), idx.data_ptr(), n_in)
+    hit = _VGROUPS.get(key)
+    if hit is not None and hit[0] is idx:
+        return hit[1]
+    res = None
+    K, n_out = idx.shape
+    if n_out == n_in:
+        rows = idx.t().cpu().tolist()
+        ptr, i, ok = [0], 0, True
+        while ok and i < n_in:
+            d = len([j for j in rows[i] if j >= 0]) + 1
+            run = list(range(i, i + d))  # i is the first member of its run
+            if i + d > n_in:
+                ok = False
+                break
+            for q in run:
+                if [j for j in rows[q] if j >= 0] != [j for j in run if j != q]:
+                    ok = False
+                    break
+            i += d
+            ptr.append(i)
+        if ok:
+            res = torch.tensor(ptr, dtype=torch.int32, device=idx.device)
+    if len(_VGROUPS) > 16:
+        _VGROUPS.clear()
+    _VGROUPS[key] = (idx, res)
+    return res
+
+
+def _var_sum(llr, msgs, idx):
+    """out = llr + the gathered sums (llr None: the sums alone), through the variable-group kernel
+    when the index has that structure, else the per-edge gather."""
+    B, n_in = msgs.shape
+    K, n_out = idx.shape
+    out = torch.empty((B, n_out), dtype=torch.float32, device=msgs.device)
+    grp = _var_groups(idx, n_in) if B else None
+    if grp is not None:
+        rc = N.lib().ldpc_var_groups_sum(N.ptr(llr) if llr is not None else None, N.ptr(msgs), B, n_in, N.ptr(grp),
+                                         grp.numel() - 1, N.ptr(out), N.stream_ptr(msgs.device))
+        if rc != N.LDPC_EUNSUPPORTED:  # rows too long for LDS: the per-edge gather below
+            N.check(rc)
+            return out
+    N.check(N.lib().ldpc_gather_sum(N.ptr(llr) if llr is not None else None, N.ptr(msgs), B, n_in, N.ptr(idx),
+                                    n_out, K, N.ptr(out), N.stream_ptr(msgs.device)))
+    return out
+
+
 class _CheckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, idx):
@@ -136,10 +192,7 @@ class _VarFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, llr, msgs, idx):
         B, n_in = msgs.shape
-        K, n_out = idx.shape
-        out = torch.empty((B, n_out), dtype=torch.float32, device=msgs.device)
-        N.check(N.lib().ldpc_gather_sum(N.ptr(llr), N.ptr(msgs), B, n_in, N.ptr(idx), n_out, K, N.ptr(out),
-                                        N.stream_ptr(msgs.device)))
+        out = _var_sum(llr, msgs, idx)
         ctx.save_for_backward(idx)
         ctx.shape = (B, n_in)
         return out
@@ -162,10 +215,7 @@ class _SumFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, msgs, idx):
         B, n_in = msgs.shape
-        K, n_out = idx.shape
-        out = torch.empty((B, n_out), dtype=torch.float32, device=msgs.device)
-        N.check(N.lib().ldpc_gather_sum(None, N.ptr(msgs), B, n_in, N.ptr(idx), n_out, K, N.ptr(out),
-                                        N.stream_ptr(msgs.device)))
+        out = _var_sum(None, msgs, idx)
         ctx.save_for_backward(idx)
         ctx.shape = (B, n_in)
         return out

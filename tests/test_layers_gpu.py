@@ -142,6 +142,7 @@ def test_check_layer_groups_equal_gather(cuda, fx, z):
     x[1::5, 5::13] = float("inf")
     x[2::5, 6::13] = -float("inf")
     x[:, 8::17] = 1.5  # ties within a check
+    x[3::5, 9::19] = float("nan")
     x = x.to(cuda)
     with torch.no_grad():
         got = CheckLayer()(x, chk)
@@ -156,3 +157,43 @@ def test_check_layer_groups_equal_gather(cuda, fx, z):
         with torch.no_grad():
             out = CheckLayer()(t(fx["x"], cuda), torch.from_numpy(fx["check_LLR"]))
         assert np.array_equal(out.cpu().numpy(), fx["check_out"])
+
+
+@pytest.mark.parametrize("z", [4, 32])
+def test_variable_layer_groups_equal_gather(cuda, fx, z):
+    """VariableLayer on create_LLR_mapping's index runs the per-variable kernel
+    (ldpc_var_groups_sum: frame row in LDS, prefix + tail per run); its outputs are bit-identical
+    to the per-edge gather kernel (ldpc_gather_sum), with and without the LLR term, on values with
+    exact zeros, -0.0, +-inf and NaN.  An index without that structure keeps the gather."""
+    from ldpc_neural_decoder import _native as N
+    from ldpc_neural_decoder.models.layers import _check_index, _var_groups, gather_sum
+    H = expand_base_matrix(load_base_matrix(code_path(z)), z)
+    _, _, var, _ = create_LLR_mapping(H.T)
+    E = var.shape[0]
+    idx = _check_index(var, E, cuda, compact=True)
+    assert _var_groups(idx, E) is not None
+    g = torch.Generator().manual_seed(z + 1)
+    x = torch.randn(67, E, generator=g) * 4.0
+    x[:, ::7] = 0.0
+    x[:, 3::11] = -0.0
+    x[1::5, 5::13] = float("inf")
+    x[2::5, 6::13] = -float("inf")
+    x[3::5, 9::19] = float("nan")
+    llr = (torch.randn(67, E, generator=g) * 2.0)
+    llr[:, 1::9] = -0.0
+    x, llr = x.to(cuda), llr.to(cuda)
+    K, n_out = idx.shape
+    for with_llr in (True, False):
+        got = VariableLayer()(llr, x, var) if with_llr else gather_sum(x, idx)
+        ref = torch.empty_like(got)
+        N.check(N.lib().ldpc_gather_sum(N.ptr(llr) if with_llr else None, N.ptr(x), x.shape[0], E, N.ptr(idx),
+                                        n_out, K, N.ptr(ref), N.stream_ptr(x.device)))
+        torch.cuda.synchronize()
+        a, b = got.detach().cpu().numpy(), ref.cpu().numpy()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))  # bitwise, incl. -0.0 and NaN
+    # a permuted index (rows no longer the ascending run of their variable) falls back to the gather
+    perm = torch.flip(idx, dims=[0]).contiguous()
+    assert _var_groups(perm, E) is None
+    if z == 4:  # the reference's own vectors (grad path: the same forward kernel)
+        out = VariableLayer()(t(fx["llr"], cuda), t(fx["check_out"], cuda), torch.from_numpy(fx["var_LLR"]))
+        close(out, fx["var_out"], atol=1e-5)
