@@ -197,3 +197,49 @@ def test_variable_layer_groups_equal_gather(cuda, fx, z):
     if z == 4:  # the reference's own vectors (grad path: the same forward kernel)
         out = VariableLayer()(t(fx["llr"], cuda), t(fx["check_out"], cuda), torch.from_numpy(fx["var_LLR"]))
         close(out, fx["var_out"], atol=1e-5)
+
+
+def test_group_kernels_ragged_rows(cuda):
+    """The per-check and per-variable kernels on a small hand-built graph whose edge count is not
+    a multiple of 4 (the unvectorised staging path) and whose groups have degrees 1..5, against the
+    per-edge gather kernels, bitwise (zeros, -0.0, inf and NaN among the values)."""
+    from ldpc_neural_decoder import _native as N
+    from ldpc_neural_decoder.models.layers import _check_groups, _check_index, _var_groups
+    runs = [1, 2, 3, 4, 5, 1, 3]                 # variable runs over edges 0..18 (n = 19)
+    n = sum(runs)
+    var_rows, s = [], 0
+    for d in runs:
+        for i in range(s, s + d):
+            var_rows.append([j for j in range(s, s + d) if j != i])
+        s += d
+    checks = [[0, 5, 9, 14], [1, 3, 18], [2, 6, 10, 15, 17], [4, 7], [8, 11, 12, 13, 16]]
+    chk_rows = [None] * n
+    for c in checks:
+        for i in c:
+            chk_rows[i] = [j for j in c if j != i]
+    K = max(len(r) for r in chk_rows + var_rows)
+    pad = lambda rows: torch.tensor([r + [-1] * (K - len(r)) for r in rows], dtype=torch.int64)
+    chk, var = pad(chk_rows), pad(var_rows)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(37, n, generator=g) * 3.0
+    x[:, ::5] = 0.0
+    x[1::3, 2] = -0.0
+    x[2::4, 7] = float("inf")
+    x[3::6, 11] = float("nan")
+    llr = torch.randn(37, n, generator=g)
+    x, llr = x.to(cuda), llr.to(cuda)
+    cidx = _check_index(chk, n, cuda)
+    vidx = _check_index(var, n, cuda, compact=True)
+    assert _check_groups(cidx, n) is not None and _var_groups(vidx, n) is not None
+    with torch.no_grad():
+        got_c = CheckLayer()(x, chk)
+        got_v = VariableLayer()(llr, x, var)
+    ref_c, ref_v = torch.empty_like(got_c), torch.empty_like(got_v)
+    N.check(N.lib().ldpc_gather_minsum(N.ptr(x), 37, n, N.ptr(cidx), n, cidx.shape[0], N.ptr(ref_c), None,
+                                       N.stream_ptr(x.device)))
+    N.check(N.lib().ldpc_gather_sum(N.ptr(llr), N.ptr(x), 37, n, N.ptr(vidx), n, vidx.shape[0], N.ptr(ref_v),
+                                    N.stream_ptr(x.device)))
+    torch.cuda.synchronize()
+    for a, b in ((got_c, ref_c), (got_v, ref_v)):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
