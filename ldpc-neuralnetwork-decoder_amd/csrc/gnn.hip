@@ -115,6 +115,7 @@ struct GnnLayer {
     // are x = (v2c w_in + b_in) + F, formed where a row is read (custom_combine_kernel's exact
     // float sequence) instead of being written back between the layers
     const float *hv2c = nullptr;  // (B, E)
+    const float *wt = nullptr;    // H != 64, gnn_mlp_tiled_kernel: this layer's W1v^T, W2v^T, W1c^T, W2c^T
     // training backward (gnn_project_groups): the projection kernel also writes the group means
     // it projects, (B, Gv, H) / (B, Gc, H)
     float *gsave_v = nullptr, *gsave_c = nullptr;
@@ -1039,6 +1040,118 @@ __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H)
     }
 }
 
+// H != 64 up to kTiledMaxH: the MLP tiled -- each wave takes kTiledNM = 8 messages at once, lanes =
+// output units, so every weight word is loaded once per 8 messages instead of once per message,
+// from a per-layer transposed copy (gnn_wt_kernel: W1s^T [2H][H], W2s^T [H][H]) whose rows the lanes
+// read coalesced; the 8 messages' inputs sit k-major in LDS ([k][8]: two ds_read_b128 per k) and
+// each product is one fma.  (fp32 with fma chains in k order: within the fp32 bar of the reference,
+// not bit-identical to gnn_mlp_generic_kernel's mul-then-add.)  VALU, not MFMA: H = 64 is the
+// tuned width.
+constexpr int kTiledNM = 8, kTiledMaxH = 256;
+inline int tiled_waves(int H) { return std::max(1, std::min(4, (64 * 1024) / (kTiledNM * 4 * H * 4))); }
+
+__global__ void gnn_wt_kernel(const float *__restrict__ w1v, const float *__restrict__ w2v,
+                              const float *__restrict__ w1c, const float *__restrict__ w2c, int H,
+                              float *__restrict__ wt) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = 3LL * H * H;
+    if (t >= 2 * per) return;
+    const int side = (int)(t / per);
+    const int64_t r = t - side * per;
+    const float *w1 = side ? w1c : w1v, *w2 = side ? w2c : w2v;
+    if (r < 2LL * H * H) {
+        const int k = (int)(r / H), o = (int)(r - (int64_t)k * H);
+        wt[t] = w1[(int64_t)o * 2 * H + k];
+    } else {
+        const int64_t q = r - 2LL * H * H;
+        const int u = (int)(q / H), o = (int)(q - (int64_t)u * H);
+        wt[t] = w2[(int64_t)o * H + u];
+    }
+}
+
+__global__ __launch_bounds__(256) void gnn_mlp_tiled_kernel(GnnLayer P, int H) {
+    extern __shared__ __attribute__((aligned(16))) float sh[];
+    constexpr int NM = kTiledNM;
+    const int nw = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *in = sh + w * NM * 4 * H;  // [2H][NM] c | group mean, then h [H][NM], y [H][NM]
+    float *hh = in + NM * 2 * H, *yy = hh + NM * H;
+    const float4 *in4 = reinterpret_cast<const float4 *>(in), *hh4 = reinterpret_cast<const float4 *>(hh);
+    const int64_t R = P.B * P.E;
+    for (int64_t r0 = ((int64_t)blockIdx.x * nw + w) * NM; r0 < R; r0 += (int64_t)gridDim.x * nw * NM) {
+        for (int o = lane; o < H; o += 64)
+#pragma unroll
+            for (int i = 0; i < NM; ++i) yy[o * NM + i] = 0.0f;
+        for (int side = 0; side < 2; ++side) {
+            const float *W1T = P.wt + (int64_t)side * 3 * H * H, *W2T = W1T + 2LL * H * H;
+            const float *b1 = side ? P.b1c : P.b1v, *b2 = side ? P.b2c : P.b2v;
+            for (int i = 0; i < NM; ++i) {
+                const int64_t row = r0 + i;
+                if (row < R) {
+                    const int64_t b = row / P.E, m = row - b * P.E;
+                    const int ty = P.msg_type[m];
+                    const float *M = side ? P.Mc + (b * P.Gc + P.cgroup[m]) * H : P.Mv + (b * P.Gv + P.vgroup[m]) * H;
+                    for (int u = lane; u < H; u += 64) {
+                        in[u * NM + i] = x_feat(P, b, m, u, H) + P.emb[ty * H + u];
+                        in[(H + u) * NM + i] = M[u];
+                    }
+                } else {
+                    for (int u = lane; u < 2 * H; u += 64) in[u * NM + i] = 0.0f;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int o = lane; o < H; o += 64) {
+                float s[NM];
+#pragma unroll
+                for (int i = 0; i < NM; ++i) s[i] = b1[o];
+                for (int k = 0; k < 2 * H; ++k) {
+                    const float wk = W1T[(int64_t)k * H + o];
+                    const float4 x0 = in4[2 * k], x1 = in4[2 * k + 1];
+                    s[0] = fmaf(wk, x0.x, s[0]); s[1] = fmaf(wk, x0.y, s[1]);
+                    s[2] = fmaf(wk, x0.z, s[2]); s[3] = fmaf(wk, x0.w, s[3]);
+                    s[4] = fmaf(wk, x1.x, s[4]); s[5] = fmaf(wk, x1.y, s[5]);
+                    s[6] = fmaf(wk, x1.z, s[6]); s[7] = fmaf(wk, x1.w, s[7]);
+                }
+                float4 *h4 = reinterpret_cast<float4 *>(hh + o * NM);
+                h4[0] = make_float4(fmaxf(s[0], 0.0f), fmaxf(s[1], 0.0f), fmaxf(s[2], 0.0f), fmaxf(s[3], 0.0f));
+                h4[1] = make_float4(fmaxf(s[4], 0.0f), fmaxf(s[5], 0.0f), fmaxf(s[6], 0.0f), fmaxf(s[7], 0.0f));
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int o = lane; o < H; o += 64) {
+                float s[NM];
+#pragma unroll
+                for (int i = 0; i < NM; ++i) s[i] = b2[o];
+                for (int u = 0; u < H; ++u) {
+                    const float wu = W2T[(int64_t)u * H + o];
+                    const float4 x0 = hh4[2 * u], x1 = hh4[2 * u + 1];
+                    s[0] = fmaf(wu, x0.x, s[0]); s[1] = fmaf(wu, x0.y, s[1]);
+                    s[2] = fmaf(wu, x0.z, s[2]); s[3] = fmaf(wu, x0.w, s[3]);
+                    s[4] = fmaf(wu, x1.x, s[4]); s[5] = fmaf(wu, x1.y, s[5]);
+                    s[6] = fmaf(wu, x1.z, s[6]); s[7] = fmaf(wu, x1.w, s[7]);
+                }
+#pragma unroll
+                for (int i = 0; i < NM; ++i) yy[o * NM + i] += s[i];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (int i = 0; i < NM; ++i) {
+            const int64_t row = r0 + i;
+            if (row >= R) break;  // wave-uniform
+            const int64_t b = row / P.E, m = row - b * P.E;
+            float part = 0.0f;
+            for (int o = lane; o < H; o += 64) {
+                float v = yy[o * NM + i];
+                if (P.residual) v += P.x_in[row * H + o];
+                if (P.last) part += v * P.wo[o];
+                if (P.x_out) P.x_out[row * H + o] = v;
+            }
+            if (P.last) {
+                for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+                if (lane == 0) P.msg_out[b * P.E + m] = part + P.bo[0];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // per-call CSR of msg_var: ints = ptr[N + 1] | cursor[N + 1] | mem[E]
 __global__ void csr_count_kernel(const int32_t *__restrict__ msg_var, int64_t E, int32_t *__restrict__ cnt) {
     const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1100,7 +1213,7 @@ __global__ void gnn_fill_kernel(int32_t *p, int64_t n, int32_t v) {
 int64_t layer_floats(int H, int T) { return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1; }
 
 struct Ws {
-    float *xa, *xb, *Mv, *Mc, *msg_out;
+    float *xa, *xb, *Mv, *Mc, *msg_out, *wt;
     int32_t *csr;
     int64_t bytes;
 };
@@ -1121,7 +1234,11 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     w.Mc = reinterpret_cast<float *>(c + xb + xb2 + mv);
     w.msg_out = reinterpret_cast<float *>(c + xb + xb2 + mv + mc);
     w.csr = reinterpret_cast<int32_t *>(c + xb + xb2 + mv + mc + vs);
-    w.bytes = xb + xb2 + mv + mc + vs + cs;
+    // H != 64 (gnn_mlp_tiled_kernel): every layer's transposed MLP weights, 6 H^2 floats each
+    // (formed once per call, before the frame halves fork onto two streams)
+    const int64_t wtb = H != 64 && H <= kTiledMaxH ? al(6LL * H * H * 4 * layers) : 0;
+    w.wt = wtb ? reinterpret_cast<float *>(c + xb + xb2 + mv + mc + vs + cs) : nullptr;
+    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb;
     return w;
 }
 
@@ -1723,15 +1840,36 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
                 hipLaunchKernelGGL(gnn_mlp_mfma_kernel<256>, dim3(grid), dim3(256), mfma_lds, st, L);
             LDPC_CHECK_LAUNCH("gnn_mlp_mfma_kernel");
         } else {
-            const int64_t want = (nb * p->E + 3) / 4;
-            const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus * 8);
-            hipLaunchKernelGGL(gnn_mlp_generic_kernel, dim3(grid), dim3(256), (size_t)16 * H * 4, st, L, H);
-            LDPC_CHECK_LAUNCH("gnn_mlp_generic_kernel");
+            if (w.wt) {  // tiled: kTiledNM messages per wave over the layer's transposed weights
+                GnnLayer T = L;
+                T.wt = w.wt + 6LL * H * H * l;
+                const int tw = tiled_waves(H);
+                const int64_t want = (nb * p->E + (int64_t)tw * kTiledNM - 1) / ((int64_t)tw * kTiledNM);
+                const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus * 16 / tw);
+                hipLaunchKernelGGL(gnn_mlp_tiled_kernel, dim3(grid), dim3(64 * tw), (size_t)tw * kTiledNM * 4 * H * 4, st,
+                                   T, H);
+                LDPC_CHECK_LAUNCH("gnn_mlp_tiled_kernel");
+            } else {
+                const int64_t want = (nb * p->E + 3) / 4;
+                const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus * 8);
+                hipLaunchKernelGGL(gnn_mlp_generic_kernel, dim3(grid), dim3(256), (size_t)16 * H * 4, st, L, H);
+                LDPC_CHECK_LAUNCH("gnn_mlp_generic_kernel");
+            }
         }
         x_in = L.x_out;
     }
     return LDPC_OK;
     };
+    if (w.wt) {  // the tiled kernel's transposed weights of every layer, on the caller's stream
+        for (int l = 0; l < layers; ++l) {
+            const float *lw = d_weights + 2 * H + (int64_t)l * layer_floats(H, types);
+            const float *w1v = lw + (int64_t)types * H, *w2v = w1v + 2LL * H * H + H;
+            const float *w1c = w2v + (int64_t)H * H + H, *w2c = w1c + 2LL * H * H + H;
+            hipLaunchKernelGGL(gnn_wt_kernel, dim3((unsigned)((6LL * H * H + 255) / 256)), dim3(256), 0, s, w1v, w2v, w1c,
+                               w2c, H, w.wt + 6LL * H * H * l);
+            LDPC_CHECK_LAUNCH("gnn_wt_kernel");
+        }
+    }
     // Two frame halves on two streams (fork / join through events on the caller's stream): every
     // frame's layers stay in order on its stream, and the halves share no data.
     if (gnn_streams() == 2 && B >= 2 * 64) {

@@ -154,12 +154,13 @@ def test_deep_supervision_matches_autograd(cuda, oracle_mod, z, layers, hidden, 
     np.testing.assert_allclose(q.cpu().numpy(), p[-1].detach().cpu().numpy(), atol=2e-6)
 
 
-@pytest.mark.parametrize("hidden", [96, 128, 200])
+@pytest.mark.parametrize("hidden", [96, 128, 200, 320])
 def test_wide_hidden_matches_autograd(cuda, oracle_mod, hidden):
     """hidden_dim past 64 (message_gnn_decoder.py:22 takes any width): the forward on
-    gnn_mlp_generic_kernel, the backward on train_mlp_bwd_wide_kernel and the tiled weight-gradient
-    reductions (64 gradient rows x 128 columns per launch), against autograd through the oracle.
-    96 and 200 leave a partial 64-unit chunk.  Same tolerance as above; inference (no grad, the
+    gnn_mlp_tiled_kernel (H <= 256) or gnn_mlp_generic_kernel (320), the backward on
+    train_mlp_bwd_wide_kernel and the tiled weight-gradient reductions (64 gradient rows x 128
+    columns per launch), against autograd through the oracle.  96, 200 and 320 leave a partial
+    64-unit chunk.  Same tolerance as above; inference (no grad, the
     chunked path) gives the same probs."""
     base, H, dec, conv, types, llr, gt = _setup(4, 2, hidden, 3, seed=5)
     ref_p, ref_loss, ref_g = _oracle_grads(oracle_mod, dec, conv, H, types, llr, gt)
