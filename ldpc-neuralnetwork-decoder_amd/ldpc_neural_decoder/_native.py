@@ -97,12 +97,40 @@ def lib():
                         f"libldpc_amd.so not found at {LIB_PATH}: build it with "
                         f"`make -C ldpc-neuralnetwork-decoder_amd` (or __graft_entry__.build())")
                 handle = ctypes.CDLL(LIB_PATH)
+                missing = []
                 for name, (res, args) in SIGNATURES.items():
-                    fn = getattr(handle, name)
+                    try:
+                        fn = getattr(handle, name)
+                    except AttributeError:
+                        # an older build (A/B runs against a previous library): bind what it has,
+                        # raise only when the absent entry point is actually called
+                        missing.append(name)
+                        continue
                     fn.restype = res
                     fn.argtypes = args
-                _lib = handle
+                _lib = _Lib(handle, missing)
     return _lib
+
+
+class _Lib:
+    """The loaded library.  Entry points declared in ``SIGNATURES`` that this build lacks raise
+    ``NativeError`` when called (not at load time)."""
+
+    def __init__(self, handle, missing):
+        self._handle = handle
+        self.missing = tuple(missing)
+        for name in missing:
+            setattr(self, name, _absent(name))
+
+    def __getattr__(self, name):
+        return getattr(self._handle, name)
+
+
+def _absent(name):
+    def fn(*_args, **_kw):
+        raise NativeError(f"{LIB_PATH} does not export {name} (built from an older source tree?)")
+    fn.__name__ = name
+    return fn
 
 
 def check(rc):

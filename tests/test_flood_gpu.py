@@ -3,6 +3,8 @@
 Bar: min-sum decisions bit-exact (integer-like work: the reference's float32 operation sequence
 is reproduced); BP decisions within a stated tolerance (the reference's torch-CPU tanh/atanh are
 SLEEF approximations, not correctly rounded -- see DESIGN.md "Parity")."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -91,6 +93,24 @@ def test_bp_z4_golden(cuda, H4, es):
         diff += int((bits.cpu().numpy().astype(np.uint8) != ref).sum())
         total += ref.size
         assert it == t[f"bp_es{int(es)}_iters"][k]
+    assert diff <= 1e-3 * total, diff
+
+
+@pytest.mark.parametrize("es", [False, True])
+def test_bp_z32_golden(cuda, H32, es):
+    """BP at Z=32 against the reference's own decisions (bp_z32.npz: B=8, 10 iterations, -6/-4/-2/0
+    dB, where frames keep errors): iteration counts equal, at most 0.1 % of bits differ (the BP bar,
+    as at Z=4)."""
+    t = golden("bp_z32.npz")
+    dec = BeliefPropagationDecoder(H32, max_iterations=10, early_stopping=es)
+    total = diff = 0
+    for k in range(len(t["snrs"])):
+        bits, it = dec.decode(torch.from_numpy(t["llrs"][k]).to(cuda))
+        ref = t[f"bp_es{int(es)}_bits"][k]
+        diff += int((bits.cpu().numpy().astype(np.uint8) != ref).sum())
+        total += ref.size
+        assert it == t[f"bp_es{int(es)}_iters"][k]
+    print(f"bp z32 es={es}: {diff} of {total} bits differ from the reference")
     assert diff <= 1e-3 * total, diff
 
 
@@ -378,3 +398,34 @@ def test_cfg3_full_batch_spot_frames_vs_oracle(cuda, oracle_mod, H32):
     be = int(bits.sum().item())
     fe = int((bits.sum(1) > 0).sum().item())
     assert cnt.tolist() == [be, fe, B, 10 * B]
+
+
+@pytest.mark.parametrize("algo", ["minsum", "bp"])
+def test_cfg3_full_batch_with_errors_every_frame_vs_oracle(cuda, oracle_mod, H32, algo):
+    """cfg3's full per-GPU batch (B = 65 536, BG2 Z=32, 10 iterations) at -4 dB, where most frames
+    still carry errors after the decode, compared with the oracle (traditional_decoders.py:42-109,
+    :177-260) on EVERY frame, so that a workgroup-indexing or batch-tail fault with non-trivial
+    decisions cannot hide.  Min-sum: bit-exact.  BP: the oracle bar
+    (<= 1e-4 of bits; measured 0).  The oracle runs its OpenMP frame loop on the host's share."""
+    from ldpc_neural_decoder.utils import awgn_llr
+    B = 65536
+    llr = awgn_llr(B, 1664, -4.0, seed=424242, frame_offset=0, device=cuda)
+    if algo == "minsum":
+        dec = MinSumScaledDecoder(H32, max_iterations=10, scaling_factor=0.75, early_stopping=False)
+    else:
+        dec = BeliefPropagationDecoder(H32, max_iterations=10, early_stopping=False)
+    cnt = torch.zeros(4, dtype=torch.int64, device=cuda)
+    bits, _ = dec.decode(llr, out_dtype=torch.uint8, counters=cnt)
+    got = bits.cpu().numpy()
+    x = llr.cpu().numpy()
+    del llr
+    oracle_mod.set_threads(min(16, os.cpu_count() or 1))
+    ref, _, _, _ = oracle_mod.flood_decode(oracle_mod.Graph(H32.numpy()), x, algo, 10, 0.75, 0)
+    frame_err = int((ref.sum(1) > 0).sum())
+    assert frame_err > B // 4, f"-4 dB should leave many frames in error (got {frame_err})"
+    if algo == "minsum":
+        bad = np.nonzero((got != ref).any(1))[0]
+        assert bad.size == 0, f"{bad.size} frames differ, first {bad[:8].tolist()}"
+    else:
+        assert (got != ref).mean() <= 1e-4, int((got != ref).sum())
+    assert cnt.tolist() == [int(got.sum()), int((got.sum(1) > 0).sum()), B, 10 * B]

@@ -24,10 +24,19 @@ def test_library_exports_every_header_symbol():
     lib = N.lib()
     syms = header_symbols()
     assert len(syms) >= 15
+    assert lib.missing == ()
     for s in syms:
-        assert hasattr(lib, s), s
+        assert hasattr(lib._handle, s), s
         assert s in N.SIGNATURES, f"{s} not bound in _native.SIGNATURES"
     assert lib.ldpc_version().decode().startswith("ldpc_amd")
+
+
+def test_absent_symbol_raises_when_called():
+    """An older library (A/B runs) loads; an entry point it lacks raises NativeError on use."""
+    lib = N._Lib(N.lib()._handle, ["ldpc_not_in_this_build"])
+    assert lib.ldpc_version().decode().startswith("ldpc_amd")
+    with pytest.raises(N.NativeError, match="ldpc_not_in_this_build"):
+        lib.ldpc_not_in_this_build(1, 2)
 
 
 def test_library_is_gfx950():

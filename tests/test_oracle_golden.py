@@ -74,12 +74,31 @@ def test_minsum_z32_low_snr_matches_reference(oracle_mod, es):
         assert it == t[f"ms_a0.75_es{es}_iters"][k]
 
 
+@pytest.mark.parametrize("es", [0, 1])
+def test_bp_z32_matches_reference(oracle_mod, es):
+    """BeliefPropagationDecoder (traditional_decoders.py:42-109) at Z=32, 10 iterations, -6..0 dB
+    (bp_z32.npz, made by importing the reference): iteration counts equal, decisions within the BP
+    bar (<= 0.1 % of bits: the reference's tanh/atanh are SLEEF approximations)."""
+    g = _graph(oracle_mod, 32)
+    t = golden("bp_z32.npz")
+    diff = total = 0
+    for k in range(len(t["snrs"])):
+        bits, _, it, _ = oracle_mod.flood_decode(g, t["llrs"][k], "bp", 10, 0.0, es)
+        ref = t[f"bp_es{es}_bits"][k]
+        diff += int((bits != ref).sum())
+        total += ref.size
+        assert it == t[f"bp_es{es}_iters"][k], (es, t["snrs"][k])
+    assert diff <= 1e-3 * total, diff
+
+
 def test_fixtures_exercise_errors():
     """The low-SNR fixtures must contain decoding errors, or bit-equality would prove little."""
     t = golden("trad_z32_low.npz")
     assert t["ms_a0.75_es0_bits"][0].sum() > 100  # -6 dB
     t4 = golden("trad_z4.npz")
     assert t4["bp_es0_bits"][0].sum() > 50 and t4["ms_a0.75_es0_bits"][0].sum() > 50
+    b32 = golden("bp_z32.npz")
+    assert b32["bp_es0_bits"][0].sum() > 100  # -6 dB: BP leaves errors too
 
 
 @pytest.mark.parametrize("z", [4, 32])
