@@ -108,6 +108,7 @@ def valu_roofline(B, n, kern_ms, traffic, pmc, pmc_path, alg_bytes):
 PMC_KERNEL_SYMBOL = {
     "minsum-z32": "_ZN4ldpc18flood_fixed_kernelINS_5fixed7BG2_Z32ELi0ELi0E",
     "bp-z32": "_ZN4ldpc18flood_fixed_kernelINS_5fixed7BG2_Z32ELi1ELi0E",
+    "bp-z4": "_ZN4ldpc18flood_fixed_kernelINS_5fixed6BG2_Z4ELi1ELi0E",
 }
 
 
@@ -643,6 +644,11 @@ def main():
                 notes = {"valu": "not measured for this variant (the PMC pass is of the default workload)"}
         if pmc_stale is not None:
             notes = dict(notes or {}, pmc_stale=pmc_stale)
+        if kind in ("minsum", "bp"):
+            # work-normalised rate beside the VALU fraction (which counts instructions, not decoding
+            # work): every edge gets one check-to-variable and one variable-to-check update per iteration
+            notes = dict(notes or {}, edge_updates_per_s=2.0 * g.E * iters * B / (kern_ms * 1e-3),
+                         edge_update_basis="2 E iterations per frame (c2v + v2c), B frames per launch / kernel time")
         # BER / FER of a neural decoder with random weights say nothing about decoding: not reported
         no_rates = kind == "lay" or (weights is not None and weights["checkpoint"] is None)
         if no_rates and weights is not None:
@@ -680,7 +686,11 @@ def main():
             "roofline": {"bound": bound, "kernel": dominant, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": None if achieved is None else achieved / peak, "traffic": traffic,
                          "kernel_ms": kern_ms,
-                         "algorithmic_per_launch": None if bound == "valu" else per_launch_alg},
+                         "algorithmic_per_launch": None if bound == "valu" else per_launch_alg,
+                         # the MEASURED HBM rate beside the algorithmic one: PMC bytes of
+                         # this build per launch / the same live kernel time, and its fraction of peak
+                         "traffic_GBps": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9,
+                         "traffic_frac": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "roofline_notes": notes,
             "avg_layers": avg_layers,
             "avg_iterations": itsum / max(fr, 1) if kind in ("minsum", "bp") else None,

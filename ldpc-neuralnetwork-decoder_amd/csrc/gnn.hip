@@ -124,6 +124,14 @@ struct GnnLayer {
     // first ntile_v1 tiles hold degree-1 messages only.  Null: tiles of 32 consecutive messages.
     const int32_t *tperm = nullptr;
     int ntile_pf = 0, ntile_v1 = 0;
+    // fp32 row walk (gnn_mlp2s_kernel RW, plan rw_*): rw_n check tile groups per frame; the MLP writes
+    // each check's sum of its output rows to S_out (B, Gc, 64) for the next layer, whose projection
+    // forms the check-side means as S_in * inv_c + memb (this layer's mean type embedding per check)
+    const int4 *rw_meta = nullptr;
+    const int32_t *rw_cg = nullptr;
+    int rw_n = 0;
+    float *S_out = nullptr;
+    const float *S_in = nullptr, *memb = nullptr;
 };
 __device__ __forceinline__ float4 hyb_x(float4 f, float v, float4 w, float4 c) {
     return make_float4((v * w.x + c.x) + f.x, (v * w.y + c.y) + f.y, (v * w.z + c.z) + f.z, (v * w.w + c.w) + f.w);
@@ -514,6 +522,23 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
             acc[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
         const int32_t *mem = T.mem + md.z + r4;
+        if (md.x && P.S_in) {
+            // check side after a row-walk MLP: the group's sum of feature rows is one row of S_in, so
+            // the mean of c = x + emb over the group is S * inv + memb (the group's mean type
+            // embedding) -- one 256-B row per group instead of a gather of its members
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int slot = 4 * p + r4, g = T.grp[32 * t + slot];
+                float4 mean = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (g >= 0) {
+                    const float4 sv = *reinterpret_cast<const float4 *>(P.S_in + ((int64_t)b * P.Gc + g) * 64 + c4);
+                    const float4 e = *reinterpret_cast<const float4 *>(P.memb + (int64_t)g * 64 + c4);
+                    const float inv = P.inv_c[g];
+                    mean = make_float4(sv.x * inv + e.x, sv.y * inv + e.y, sv.z * inv + e.z, sv.w * inv + e.w);
+                }
+                *reinterpret_cast<float4 *>(gm + slot * kPS + c4) = mean;
+            }
+        } else {
         if (P.x_in) {
             const float *xb = P.x_in + (int64_t)b * P.E * 64 + c4;
             const float *eb = lds + kPOffEmb + c4;
@@ -588,6 +613,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
             if (P.gsave_v && g >= 0)
                 *reinterpret_cast<float4 *>((md.x ? P.gsave_c + ((int64_t)b * P.Gc + g) * 64
                                                   : P.gsave_v + ((int64_t)b * P.Gv + g) * 64) + c4) = mean;
+        }
         }
         __builtin_amdgcn_wave_barrier();
         // B operand: lane (j, half) <- group j's units 8 q + 4 half + i (q < 8)
@@ -812,7 +838,7 @@ inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d
 // W1v [c; g] = (W1v_left + W1v_right) c -- one fp32 sum per weight, rounded once and split like the
 // other weights -- and GEMM1 starts from b1v instead of a projected row, which the projection
 // kernel then does not write for those groups (ProjTiles first = n_ptiles_v1).
-template <int NT, int WPS, bool HYB = false>
+template <int NT, int WPS, bool HYB = false, bool RW = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __bf16 *img = reinterpret_cast<__bf16 *>(lds);
@@ -825,7 +851,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             split_store(w[q], img + 3 * q * kS6Img + o * kS6Row + p, kS6Img);
     }
     __bf16 *img_d1 = reinterpret_cast<__bf16 *>(reinterpret_cast<char *>(lds) + s6_off_d1(P.T));
-    if (P.tperm && P.vside)
+    if ((P.tperm || RW) && P.ntile_v1 && P.vside)  // the combined image, when degree-1 tiles exist
         for (int i = tid; i < 64 * 64; i += NT) {
             const int o = i >> 6, p = i & 63, u = pi16(p);
             split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_d1 + o * kS6Row + p, kS6Img);
@@ -841,42 +867,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
-    const int64_t R = P.B * P.E;
-    const int64_t tpf = P.tperm ? P.ntile_pf : 1;
-    const int64_t ntiles = P.tperm ? P.B * tpf : (R + 31) / 32;
     const float bo = P.last ? P.bo[0] : 0.0f;
-    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
     const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
-    // (frame, in-frame tile) of the tperm walk, advanced without divisions: tw.stride = sb frames + sk tiles
-    const int64_t sb = tw.stride / tpf, sk = tw.stride - sb * tpf;
-    int64_t tb = tw.first / tpf, tk = tw.first - tb * tpf;
-    // (frame, message) of row t * 32 + j of the plain walk, likewise (row stride 32 tw.stride)
-    const int64_t rs = 32 * tw.stride, rsb = rs / P.E, rsm = rs - rsb * P.E;
-    int64_t pb = (tw.first * 32 + j) / P.E, pm = tw.first * 32 + j - pb * P.E;
-    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
-        int64_t rr, b, m;
-        bool ok, d1t = false;
-        if (P.tperm) {  // slot j of the frame's tile k (padding: the tile's first message, not written)
-            b = tb;
-            const int64_t k = tk;
-            const int32_t mm = P.tperm[k * 32 + j];
-            ok = mm >= 0;
-            m = ok ? mm : P.tperm[k * 32];
-            rr = b * P.E + m;
-            d1t = k < P.ntile_v1;
-            tb += sb;
-            tk += sk;
-            if (tk >= tpf) { tk -= tpf; ++tb; }
-        } else {
-            const int64_t row = t * 32 + j;
-            ok = row < R;
-            rr = ok ? row : R - 1;
-            b = ok ? pb : P.B - 1;
-            m = ok ? pm : P.E - 1;
-            pb += rsb;
-            pm += rsm;
-            if (pm >= P.E) { pm -= P.E; ++pb; }
-        }
+    float S[32];  // row walk: this lane's check's running sum of output rows (its half's 32 units)
+    // One 32-message tile: slot j is message m of frame b (row rr of x); ok = a real message (a padding
+    // slot computes on a valid row and writes nothing); d1t = a degree-1 var tile; pc = the slot's
+    // projected check row (+ 4 half).
+    auto tile = [&](int64_t b, int64_t m, int64_t rr, bool ok, bool d1t, const float *pc) {
         // x[s][i] = feature pi16(16 s + 8 h + i) before the type embedding (float4 pairs)
         float x[4][8];
         if (P.x_in) {
@@ -907,7 +904,6 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         const float *e = lds + kS6OffEmb + P.msg_type[m] * kPS;
         // a degree-1 tile's var side starts from b1v (its group half is in the combined W1v image)
         const float *pv = d1t ? P.b1v + 4 * half : P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
-        const float *pc = P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half;
         // GEMM1 of both sides per k-step over one split of c (c = x + emb[type] is the same for
         // both), each side's accumulators from its projected group row W1_right g + b1
         f32x16 hs[2][2];
@@ -983,12 +979,85 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                     for (int i = 0; i < 4; ++i) part += vv[i] * wo[o0 + i];
                 }
                 if (ok && P.x_out) *reinterpret_cast<float4 *>(P.x_out + rr * 64 + o0) = v;
+                if constexpr (RW) {  // the check's sum of next-layer features (row walk)
+                    S[16 * ot + 4 * q] += v.x; S[16 * ot + 4 * q + 1] += v.y;
+                    S[16 * ot + 4 * q + 2] += v.z; S[16 * ot + 4 * q + 3] += v.w;
+                }
             }
         }
         if (P.last) {
             part += __shfl_xor(part, 32, 64);
             if (ok && half == 0) P.msg_out[b * P.E + m] = part + bo;
         }
+    };
+    if constexpr (RW) {
+        // Row walk (plan rw_*): a unit is one frame's check tile group -- up to 32 consecutive checks of
+        // one degree d whose messages are contiguous runs (the reference's check-major order,
+        // message_gnn_decoder.py:397-406) -- run as d tiles, tile i holding message i of every check
+        // (lane j = check j).  Every tile of the unit reads the same 32 projected check rows, and the
+        // lane sums its check's output rows in registers: the next layer's check-group sums leave the
+        // kernel as one row per check (S_out) instead of being gathered from the feature rows again.
+        const int64_t nunits = P.B * P.rw_n;
+        const TileWalk tw = xcd_tiles(nunits, NT / 64, wave);
+        for (int64_t u = tw.first; u < tw.end; u += tw.stride) {
+            const int64_t b = u / P.rw_n;
+            const int c = (int)(u - b * P.rw_n);
+            const int4 md = P.rw_meta[c];  // {first message, checks, degree, degree-1 tile mask}
+            const bool okc = j < md.y;
+            const int cg = P.rw_cg[32 * c + (okc ? j : 0)];
+            const float *pc = P.Mc + (b * P.Gc + cg) * 64 + 4 * half;
+            const int64_t mj = md.x + (int64_t)(okc ? j : 0) * md.z;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) S[i] = 0.0f;
+            for (int i = 0; i < md.z; ++i) tile(b, mj + i, b * P.E + mj + i, okc, P.ntile_v1 && ((md.w >> i) & 1), pc);
+            if (okc && P.S_out) {
+                float *dst = P.S_out + (b * P.Gc + cg) * 64;
+#pragma unroll
+                for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        *reinterpret_cast<float4 *>(dst + 32 * ot + 8 * q + 4 * half) =
+                            make_float4(S[16 * ot + 4 * q], S[16 * ot + 4 * q + 1], S[16 * ot + 4 * q + 2],
+                                        S[16 * ot + 4 * q + 3]);
+            }
+        }
+        return;
+    }
+    const int64_t R = P.B * P.E;
+    const int64_t tpf = P.tperm ? P.ntile_pf : 1;
+    const int64_t ntiles = P.tperm ? P.B * tpf : (R + 31) / 32;
+    const TileWalk tw = xcd_tiles(ntiles, NT / 64, wave);
+    // (frame, in-frame tile) of the tperm walk, advanced without divisions: tw.stride = sb frames + sk tiles
+    const int64_t sb = tw.stride / tpf, sk = tw.stride - sb * tpf;
+    int64_t tb = tw.first / tpf, tk = tw.first - tb * tpf;
+    // (frame, message) of row t * 32 + j of the plain walk, likewise (row stride 32 tw.stride)
+    const int64_t rs = 32 * tw.stride, rsb = rs / P.E, rsm = rs - rsb * P.E;
+    int64_t pb = (tw.first * 32 + j) / P.E, pm = tw.first * 32 + j - pb * P.E;
+    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+        int64_t rr, b, m;
+        bool ok, d1t = false;
+        if (P.tperm) {  // slot j of the frame's tile k (padding: the tile's first message, not written)
+            b = tb;
+            const int64_t k = tk;
+            const int32_t mm = P.tperm[k * 32 + j];
+            ok = mm >= 0;
+            m = ok ? mm : P.tperm[k * 32];
+            rr = b * P.E + m;
+            d1t = k < P.ntile_v1;
+            tb += sb;
+            tk += sk;
+            if (tk >= tpf) { tk -= tpf; ++tb; }
+        } else {
+            const int64_t row = t * 32 + j;
+            ok = row < R;
+            rr = ok ? row : R - 1;
+            b = ok ? pb : P.B - 1;
+            m = ok ? pm : P.E - 1;
+            pb += rsb;
+            pm += rsm;
+            if (pm >= P.E) { pm -= P.E; ++pb; }
+        }
+        tile(b, m, rr, ok, d1t, P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half);
     }
 }
 
@@ -1210,10 +1279,26 @@ __global__ void gnn_fill_kernel(int32_t *p, int64_t n, int32_t v) {
     if (i < n) p[i] = v;
 }
 
+// Row walk: memb[l][g][u] = (1 / |g|) sum over check group g's messages (ascending) of emb_l[type][u],
+// the mean type embedding each layer's check-side group mean adds to S * inv (gnn_group_proj_kernel)
+__global__ void gnn_memb_kernel(const float *__restrict__ emb0, int64_t layer_stride, const int32_t *__restrict__ msg_type,
+                                const int32_t *__restrict__ cg_ptr, const int32_t *__restrict__ cg_mem,
+                                const float *__restrict__ inv_c, int Gc, int layers, float *__restrict__ memb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)layers * Gc * 64) return;
+    const int64_t l = i / ((int64_t)Gc * 64);
+    const int g = (int)(i / 64 - l * Gc), u = (int)(i & 63);
+    const float *emb = emb0 + l * layer_stride;
+    float s = 0.0f;
+    for (int k = cg_ptr[g]; k < cg_ptr[g + 1]; ++k) s += emb[msg_type[cg_mem[k]] * 64 + u];
+    memb[i] = s * inv_c[g];
+}
+
 int64_t layer_floats(int H, int T) { return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1; }
 
 struct Ws {
     float *xa, *xb, *Mv, *Mc, *msg_out, *wt;
+    float *S, *memb;  // row walk (H = 64, plan rw_*): per-check feature sums (B, Gc, H), mean type embeddings (L, Gc, H)
     int32_t *csr;
     int64_t bytes;
 };
@@ -1238,7 +1323,12 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     // (formed once per call, before the frame halves fork onto two streams)
     const int64_t wtb = H != 64 && H <= kTiledMaxH ? al(6LL * H * H * 4 * layers) : 0;
     w.wt = wtb ? reinterpret_cast<float *>(c + xb + xb2 + mv + mc + vs + cs) : nullptr;
-    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb;
+    const int64_t rwb = H == 64 && p->n_rw > 0 && layers > 1 ? mc : 0;
+    const int64_t mbb = rwb ? al((int64_t)layers * p->Gc * H * es) : 0;
+    char *r = c + xb + xb2 + mv + mc + vs + cs + wtb;
+    w.S = rwb ? reinterpret_cast<float *>(r) : nullptr;
+    w.memb = rwb ? reinterpret_cast<float *>(r + rwb) : nullptr;
+    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb;
     return w;
 }
 
@@ -1334,6 +1424,13 @@ constexpr int kMlp2sWps = LDPC_MLP2S_WPS, kMlp2sNt = LDPC_MLP2S_NT;
 // call (tests compare the two).
 bool split_path() {
     const char *e = std::getenv("LDPC_GNN_SPLIT");
+    return !(e && std::atoi(e) == 0);
+}
+
+// LDPC_GNN_ROWWALK=0 keeps the tile walk of gnn_mlp2s_kernel and the gathered check-side means
+// (A/B runs); default: the row walk when the plan has check tile groups.  Read per call.
+bool rowwalk_path() {
+    const char *e = std::getenv("LDPC_GNN_ROWWALK");
     return !(e && std::atoi(e) == 0);
 }
 
@@ -1497,6 +1594,40 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         for (int64_t m = 32; m < E; m += 32) ct_m0.push_back((int32_t)m);
     }
     ct_m0.push_back((int32_t)E);
+    // fp32 row walk: check tile groups (gnn.hpp rw_*), used when they fill >= 90 % of their tiles
+    std::vector<int32_t> rw_meta, rw_cg;
+    bool rw_d1 = true;
+    if (aligned) {
+        auto vdeg1 = [&](int64_t m) { return vptr[h_vgroup[m] + 1] - vptr[h_vgroup[m]] == 1; };
+        int64_t m = 0, slots = 0, d1_msgs = 0, d1_in_tiles = 0;
+        for (int64_t q = 0; q < E; ++q) d1_msgs += vdeg1(q);
+        while (m < E) {
+            const int d = cptr[h_cgroup[m] + 1] - cptr[h_cgroup[m]];
+            const int64_t m0 = m;
+            int n = 0;
+            while (n < 32 && m < E && cptr[h_cgroup[m] + 1] - cptr[h_cgroup[m]] == d) {
+                rw_cg.push_back(h_cgroup[m]);
+                ++n;
+                m += d;
+            }
+            for (int k = n; k < 32; ++k) rw_cg.push_back(-1);
+            int32_t mask = 0;
+            for (int i = 0; i < d; ++i) {
+                bool all = true;
+                for (int k = 0; k < n && all; ++k) all = vdeg1(m0 + (int64_t)k * d + i);
+                if (all) {
+                    mask |= (int32_t)(1u << i);
+                    d1_in_tiles += n;
+                }
+            }
+            rw_meta.insert(rw_meta.end(), {(int32_t)m0, n, d, mask});
+            slots += 32LL * d;
+        }
+        rw_d1 = d1_in_tiles == d1_msgs;
+        if (!rw_d1)
+            for (size_t c = 0; c < rw_meta.size(); c += 4) rw_meta[c + 3] = 0;
+        if ((double)E < 0.9 * (double)slots) rw_meta.clear(), rw_cg.clear();
+    }
     // fp32 path: projection tiles of 32 groups of one side (gnn.hpp), each side sorted by degree
     std::vector<int32_t> pt;  // meta [4 n] | grp [32 n] | deg [32 n] | mem
     std::vector<int32_t> pt_meta, pt_grp, pt_deg, pt_mem;
@@ -1565,8 +1696,9 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     hipError_t e4 = hipMalloc(&p->d_gt, gt_words * 4);
     hipError_t e5 = hipMalloc(&p->d_pt, pt.size() * 4);
     hipError_t e6 = hipMalloc(&p->d_ct, ct_m0.size() * 4);
+    hipError_t e7 = rw_meta.empty() ? hipSuccess : hipMalloc(&p->d_rw, (rw_meta.size() + rw_cg.size()) * 4);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess ||
-        e6 != hipSuccess) {
+        e6 != hipSuccess || e7 != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan allocation failed");
     }
@@ -1577,10 +1709,17 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
         hipMemcpy(p->d_gt + gt_meta.size() + gt_grp.size(), gt_mem.data(), gt_mem.size() * 4,
                   hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_pt, pt.data(), pt.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->d_ct, ct_m0.data(), ct_m0.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(p->d_ct, ct_m0.data(), ct_m0.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        (p->d_rw && (hipMemcpy(p->d_rw, rw_meta.data(), rw_meta.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                     hipMemcpy(p->d_rw + rw_meta.size(), rw_cg.data(), rw_cg.size() * 4, hipMemcpyHostToDevice) !=
+                         hipSuccess))) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan upload failed");
     }
+    p->n_rw = (int)(rw_meta.size() / 4);
+    p->rw_d1 = p->n_rw > 0 && rw_d1;
+    p->rw_meta = reinterpret_cast<const int4 *>(p->d_rw);
+    p->rw_cg = p->d_rw ? p->d_rw + rw_meta.size() : nullptr;
     p->n_ptiles = (int)(pt_meta.size() / 4);
     p->n_ptiles_v = n_ptiles_v;
     p->n_ptiles_v1 = n_ptiles_v1;
@@ -1680,6 +1819,7 @@ extern "C" int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p) {
     if (p->d_gt) (void)hipFree(p->d_gt);
     if (p->d_pt) (void)hipFree(p->d_pt);
     if (p->d_ct) (void)hipFree(p->d_ct);
+    if (p->d_rw) (void)hipFree(p->d_rw);
     delete p;
     return LDPC_OK;
 }
@@ -1742,8 +1882,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     const bool split = split_path() && mlp2s_lds_bytes(types, false) <= 160 * 1024;
     // degree-1 message tiles first (gnn_mlp2s_kernel) when the combined image fits
     const bool d1t = split && p->n_mtiles_v1 > 0 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
+    // row walk (gnn_mlp2s_kernel RW): check tile groups, per-check sums out of the MLP (w.S set by carve)
+    const bool rw = split && w.S && rowwalk_path();
+    const bool rwd1 = rw && p->rw_d1 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
-                 mlp2_lds = split ? mlp2s_lds_bytes(types, d1t) : mlp2_lds_bytes(types);
+                 mlp2_lds = split ? mlp2s_lds_bytes(types, rw ? rwd1 : d1t) : mlp2_lds_bytes(types);
     const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
     int mlp2_per_cu = 1, proj_per_cu = 1;
@@ -1755,9 +1898,16 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
-        LDPC_HIP(hipFuncSetAttribute(split ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>)
+        LDPC_HIP(hipFuncSetAttribute(split ? (rw ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>)
+                                                 : reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>))
                                            : reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
+    }
+    if (proj && rw) {  // every layer's mean type embedding per check group, once per call
+        const int64_t n = (int64_t)layers * p->Gc * 64;
+        hipLaunchKernelGGL(gnn_memb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_weights + 2 * H,
+                           layer_floats(H, types), d_msg_type, p->cg_ptr, p->cg_mem, p->inv_c, p->Gc, layers, w.memb);
+        LDPC_CHECK_LAUNCH("gnn_memb_kernel");
     }
     // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
     const GnnLayer L0 = L;
@@ -1792,12 +1942,21 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.d1 = H == 64 && gm_tiles() && d1_skip() && !p->weighted;
         if (proj) {
             L.d1 = 0;
-            if (d1t) {
+            if (rw) {
+                L.rw_meta = p->rw_meta;
+                L.rw_cg = p->rw_cg;
+                L.rw_n = p->n_rw;
+                L.ntile_v1 = rwd1;
+                L.S_in = l > 0 ? w.S + b0 * p->Gc * H : nullptr;
+                L.S_out = l + 1 < layers ? w.S + b0 * p->Gc * H : nullptr;
+                L.memb = w.memb + (int64_t)l * p->Gc * H;
+            } else if (d1t) {
                 L.tperm = p->mt_perm;
                 L.ntile_pf = p->n_mtiles;
                 L.ntile_v1 = p->n_mtiles_v1;
             }
-            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, d1t ? p->n_ptiles_v1 : 0};
+            const bool skip_v1 = rw ? rwd1 : d1t;
+            const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, skip_v1 ? p->n_ptiles_v1 : 0};
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;
             const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
@@ -1809,7 +1968,12 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             const int64_t tiles = d1t ? nb * p->n_mtiles : (nb * p->E + 31) / 32;
             constexpr int wpb = kMlp2Nt / 64;
             const unsigned grid = (unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu);
-            if (split)
+            if (rw)
+                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>),
+                                   dim3((unsigned)std::min<int64_t>((nb * p->n_rw + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64),
+                                                                    (int64_t)g_num_cus)),
+                                   dim3(kMlp2sNt), mlp2_lds, st, L);
+            else if (split)
                 hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>),
                                    dim3((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus)),
                                    dim3(kMlp2sNt), mlp2_lds, st, L);

@@ -41,7 +41,7 @@ namespace ldpc {
 namespace {
 
 constexpr int kMaxH = 64;         // widest H of the LDS-image kernels (train_mlp_bwd_kernel, train_outer_kernel)
-constexpr int kMaxTrainH = 1024;  // widest H trained (train_mlp_bwd_wide_kernel's per-wave LDS rows)
+X
 
 struct TW {  // one layer's weights in the blob (see ldpc_amd.h)
     const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
@@ -1571,7 +1571,7 @@ using namespace ldpc;
 
 extern "C" int64_t ldpc_gnn_train_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers) {
     if (!p || hidden <= 0 || hidden > kMaxTrainH || N <= 0 || B < 0 || layers <= 0)
-        return fail(LDPC_EINVAL, "bad arguments (training needs hidden_dim <= 1024)");
+        return fail(LDPC_EINVAL, "bad arguments (training needs hidden_dim <= 256)");
     const int64_t fwd = ldpc_gnn_workspace_size(p, hidden, N, B, layers, 0);
     const int64_t bwd = carve_train(p, hidden, N, B, nullptr).bytes;
     return fwd > bwd ? fwd : bwd;
@@ -1584,7 +1584,7 @@ extern "C" int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int ty
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     if (hidden <= 0 || hidden > kMaxTrainH || types <= 0 || layers <= 0 || N <= 0 || B < 0)
-        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 1024)");
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 256)");
     if (B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_saved)
         return fail(LDPC_EINVAL, "NULL tensor");
@@ -1602,7 +1602,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
     if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     const int H = hidden, T = types, L = layers;
     if (H <= 0 || H > kMaxTrainH || T <= 0 || L <= 0 || N <= 0 || B < 0)
-        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 1024)");
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 256)");
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_grad_probs || !d_saved || !d_grad_weights)
         return fail(LDPC_EINVAL, "NULL tensor");
     if ((d_layer_probs == nullptr) != (d_grad_layer_probs == nullptr))

@@ -159,6 +159,37 @@ int launch_gather_lds(int fpw, const float *in, const float *llr, int64_t B, int
 // the others is min1, or min2 for the edge holding min1, NaN if another edge is NaN, capped at
 // 1e10 when the row has padding (K > degree - 1).  O(degree) per check instead of O(degree^2),
 // and the (K, n) index is not re-read per workgroup.
+// One check of a staged frame row r, members gmem[p0 .. p1): the two passes above, in place.  Shared
+// by check_group_kernel (member indices from global memory, int32) and check_group_idx_kernel (LDS,
+// uint16), so the two cannot drift apart.
+template <typename Idx>
+__device__ __forceinline__ void check_group_minsum(float *r, const Idx *gmem, int p0, int p1, int K) {
+    int zeros = 0, nans = 0, neg = 0, pos = -1;
+    float m1 = INFINITY, m2 = INFINITY;
+    for (int p = p0; p < p1; ++p) {
+        const float v = r[gmem[p]];
+        const float sv = v + 1e-10f;
+        zeros += sv == 0.0f;
+        nans += sv != sv;
+        neg ^= sv < 0.0f;
+        float a = fabsf(v);
+        if (a == 0.0f) a = 1e10f;
+        if (a < m1) { m2 = m1; m1 = a; pos = p; }
+        else if (a < m2) m2 = a;
+    }
+    const bool pad = K > p1 - p0 - 1;
+    for (int p = p0; p < p1; ++p) {
+        const int j = gmem[p];
+        const float v = r[j];
+        const float sv = v + 1e-10f;
+        const int z = zeros - (sv == 0.0f), nn = nans - (sv != sv), ng = neg ^ (sv < 0.0f);
+        float m = p == pos ? m2 : m1;
+        if (pad) m = fminf(m, 1e10f);
+        const float sp = z > 0 ? (ng ? -0.0f : 0.0f) : (ng ? -1.0f : 1.0f);
+        r[j] = nn > 0 ? __builtin_nanf("") : sp * m;
+    }
+}
+
 template <int FPW>
 __global__ __launch_bounds__(512) void check_group_kernel(const float *__restrict__ in, int64_t B, int n,
                                                           const int32_t *__restrict__ gptr,
@@ -181,31 +212,7 @@ __global__ __launch_bounds__(512) void check_group_kernel(const float *__restric
     for (int w = threadIdx.x; w < G * nb; w += blockDim.x) {
         const int g = w / nb, f = w - g * nb;
         float *r = rows + f * n;
-        const int p0 = gptr[g], p1 = gptr[g + 1];
-        int zeros = 0, nans = 0, neg = 0, pos = -1;
-        float m1 = INFINITY, m2 = INFINITY;
-        for (int p = p0; p < p1; ++p) {
-            const float v = r[gmem[p]];
-            const float sv = v + 1e-10f;
-            zeros += sv == 0.0f;
-            nans += sv != sv;
-            neg ^= sv < 0.0f;
-            float a = fabsf(v);
-            if (a == 0.0f) a = 1e10f;
-            if (a < m1) { m2 = m1; m1 = a; pos = p; }
-            else if (a < m2) m2 = a;
-        }
-        const bool pad = K > p1 - p0 - 1;
-        for (int p = p0; p < p1; ++p) {
-            const int j = gmem[p];
-            const float v = r[j];
-            const float sv = v + 1e-10f;
-            const int z = zeros - (sv == 0.0f), nn = nans - (sv != sv), ng = neg ^ (sv < 0.0f);
-            float m = p == pos ? m2 : m1;
-            if (pad) m = fminf(m, 1e10f);
-            const float sp = z > 0 ? (ng ? -0.0f : 0.0f) : (ng ? -1.0f : 1.0f);
-            r[j] = nn > 0 ? __builtin_nanf("") : sp * m;
-        }
+        check_group_minsum(r, gmem, gptr[g], gptr[g + 1], K);
     }
     __syncthreads();
     if (vec) {
@@ -260,10 +267,10 @@ __global__ __launch_bounds__(512) void var_group_sum_kernel(const float *__restr
     if (vec) {
         const float4 *r4 = reinterpret_cast<const float4 *>(rows);
         float4 *o4 = reinterpret_cast<float4 *>(out + b * n);
-        const float4 *l4 = reinterpret_cast<const float4 *>(llr + b * n);
+        const float4 *l4 = llr ? reinterpret_cast<const float4 *>(llr + b * n) : nullptr;
         for (int e = threadIdx.x; e < n / 4; e += blockDim.x) {
             const float4 s = r4[e];
-            if (llr) {
+            if (l4) {
                 const float4 l = l4[e];
                 o4[e] = make_float4(l.x + s.x, l.y + s.y, l.z + s.z, l.w + s.w);
             } else {
@@ -305,31 +312,7 @@ __global__ __launch_bounds__(512) void check_group_idx_kernel(const float *__res
         }
         __syncthreads();
         for (int g = threadIdx.x; g < G; g += blockDim.x) {
-            const int p0 = gp[g], p1 = gp[g + 1];
-            int zeros = 0, nans = 0, neg = 0, pos = -1;
-            float m1 = INFINITY, m2 = INFINITY;
-            for (int p = p0; p < p1; ++p) {
-                const float v = rows[gm[p]];
-                const float sv = v + 1e-10f;
-                zeros += sv == 0.0f;
-                nans += sv != sv;
-                neg ^= sv < 0.0f;
-                float a = fabsf(v);
-                if (a == 0.0f) a = 1e10f;
-                if (a < m1) { m2 = m1; m1 = a; pos = p; }
-                else if (a < m2) m2 = a;
-            }
-            const bool pad = K > p1 - p0 - 1;
-            for (int p = p0; p < p1; ++p) {
-                const int j = gm[p];
-                const float v = rows[j];
-                const float sv = v + 1e-10f;
-                const int z = zeros - (sv == 0.0f), nn = nans - (sv != sv), ng = neg ^ (sv < 0.0f);
-                float m = p == pos ? m2 : m1;
-                if (pad) m = fminf(m, 1e10f);
-                const float sp = z > 0 ? (ng ? -0.0f : 0.0f) : (ng ? -1.0f : 1.0f);
-                rows[j] = nn > 0 ? __builtin_nanf("") : sp * m;
-            }
+            check_group_minsum(rows, gm, gp[g], gp[g + 1], K);
         }
         __syncthreads();
         if (vec) {

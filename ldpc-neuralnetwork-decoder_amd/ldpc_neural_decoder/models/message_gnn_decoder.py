@@ -365,8 +365,9 @@ class _NativeGnnTrain(torch.autograd.Function):
         dev = llr.device
         H, L = dec.hidden_dim, len(dec.gnn_layers)
         T = dec.gnn_layers[0].message_type_embeddings.shape[0]
-        if H > 1024:
-            raise NotImplementedError("the native backward supports hidden_dim <= 1024")
+        if H > 256:
+            raise NotImplementedError("the native backward supports hidden_dim <= 256 (the widths whose forward "
+                                      "products it recomputes bit for bit)")
         B, Nv = llr.shape
         E = dec.num_messages
         blob = torch.cat([p.detach().reshape(-1).to(dev, torch.float32) for p in params]).contiguous()

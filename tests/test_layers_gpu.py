@@ -243,3 +243,59 @@ def test_group_kernels_ragged_rows(cuda):
     for a, b in ((got_c, ref_c), (got_v, ref_v)):
         a, b = a.cpu().numpy(), b.cpu().numpy()
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+_IDX_F_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = sys.argv[2:]
+from conftest import code_path
+from ldpc_neural_decoder.models import CheckLayer
+from ldpc_neural_decoder.utils import create_LLR_mapping, expand_base_matrix, load_base_matrix
+dev = torch.device("cuda", 0)
+out = {}
+runs = [1, 2, 3, 4, 5, 1, 3]
+n = sum(runs)
+checks = [[0, 5, 9, 14], [1, 3, 18], [2, 6, 10, 15, 17], [4, 7], [8, 11, 12, 13, 16]]
+rows = [None] * n
+for c in checks:
+    for i in c:
+        rows[i] = [j for j in c if j != i]
+K = max(len(r) for r in rows)
+graphs = {"ragged": torch.tensor([r + [-1] * (K - len(r)) for r in rows], dtype=torch.int64)}
+H = expand_base_matrix(load_base_matrix(code_path(32)), 32)
+graphs["z32"] = create_LLR_mapping(H.T)[1]
+for name, chk in graphs.items():
+    E = chk.shape[0]
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(41, E, generator=g) * 3.0
+    x[:, ::5] = 0.0
+    x[:, 1::9] = -1e-10
+    x[1::3, 2::7] = -0.0
+    x[2::4, 7::13] = float("inf")
+    x[3::6, 11::17] = float("nan")
+    with torch.no_grad():
+        out[name] = CheckLayer()(x.to(dev), chk).cpu().numpy().view(np.uint32)
+np.savez(sys.argv[1], **out)
+"""
+
+
+def test_check_group_kernels_idx_and_global_bit_equal(tmp_path):
+    """check_group_idx_kernel (member lists staged in LDS, the default) and check_group_kernel (lists
+    from global memory, LDPC_CHECK_IDX_F=0) share one per-check body; run each in a fresh process
+    (the switch is read once) on a ragged graph and on BG2 Z=32, with zeros, -1e-10, -0.0, +-inf and
+    NaN among the values: bit-equal outputs."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT, PKG
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    res = {}
+    for f in ("0", "4"):
+        path = str(tmp_path / f"idx{f}.npz")
+        env = dict(os.environ, LDPC_CHECK_IDX_F=f)
+        subprocess.run([sys.executable, "-c", _IDX_F_SCRIPT, path, os.path.join(ROOT, "tests"), PKG, ROOT],
+                       env=env, check=True, timeout=120)
+        res[f] = np.load(path)
+    for name in ("ragged", "z32"):
+        assert np.array_equal(res["0"][name], res["4"][name]), name

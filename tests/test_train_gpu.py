@@ -154,14 +154,14 @@ def test_deep_supervision_matches_autograd(cuda, oracle_mod, z, layers, hidden, 
     np.testing.assert_allclose(q.cpu().numpy(), p[-1].detach().cpu().numpy(), atol=2e-6)
 
 
-@pytest.mark.parametrize("hidden", [96, 128, 200, 320])
+@pytest.mark.parametrize("hidden", [96, 128, 200, 256])
 def test_wide_hidden_matches_autograd(cuda, oracle_mod, hidden):
     """hidden_dim past 64 (message_gnn_decoder.py:22 takes any width): the forward on
-    gnn_mlp_tiled_kernel (H <= 256) or gnn_mlp_generic_kernel (320), the backward on
+    gnn_mlp_tiled_kernel (H <= 256, the trainable widths), the backward on
     train_mlp_bwd_wide_kernel and the tiled weight-gradient reductions (64 gradient rows x 128
-    columns per launch), against autograd through the oracle.  96, 200 and 320 leave a partial
-    64-unit chunk.  Same tolerance as above; inference (no grad, the
-    chunked path) gives the same probs."""
+    columns per launch), against autograd through the oracle.  96 and 200 leave a partial
+    64-unit chunk; 256 is the widest trainable H.  Same tolerance as above; inference (no grad,
+    the chunked path) gives the same probs."""
     base, H, dec, conv, types, llr, gt = _setup(4, 2, hidden, 3, seed=5)
     ref_p, ref_loss, ref_g = _oracle_grads(oracle_mod, dec, conv, H, types, llr, gt)
     dec = dec.to(cuda)
@@ -175,3 +175,19 @@ def test_wide_hidden_matches_autograd(cuda, oracle_mod, hidden):
     with torch.no_grad():
         q = dec(*args)
     np.testing.assert_allclose(q.cpu().numpy(), probs.detach().cpu().numpy(), atol=1e-6)
+
+
+def test_training_past_256_refuses_inference_runs(cuda, oracle_mod):
+    """Past H = 256 the forward runs gnn_mlp_generic_kernel, whose products the wide backward would
+    not recompute bit for bit: training refuses with a clear error; inference still runs and matches
+    the oracle."""
+    base, H, dec, conv, types, llr, gt = _setup(4, 2, 320, 3, seed=6)
+    ref_p, _, _ = _oracle_grads(oracle_mod, dec, conv, H, types, llr, gt)
+    dec = dec.to(cuda)
+    args = (llr.to(cuda), conv.message_to_var_index(), types, conv.var_to_check_adjacency,
+            conv.check_to_var_adjacency)
+    with pytest.raises(NotImplementedError, match="256"):
+        dec(*args, ground_truth=gt.to(cuda))
+    with torch.no_grad():
+        q = dec(*args)
+    np.testing.assert_allclose(q.cpu().numpy(), ref_p.detach().numpy(), atol=2e-5)

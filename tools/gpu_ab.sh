@@ -1,10 +1,10 @@
-# A/B on one box: the default library against variant libraries (_lib/variants/<name>.so,
+# A/B on one box: the default library against variant libraries (ab/<name>.so or $VARDIR/<name>.so,
 # interleaved, two rounds) on one bench workload, plus the phase timelines of flood timeline builds.
 # Lines land in gpurun_out/ab_<TAG>/.
 # usage: TAG=x bash tools/gpu_ab.sh "<variant names>" "<timeline names>" [bench args]
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/ab_${TAG:-flood}; mkdir -p $O
-V=$R/ldpc-neuralnetwork-decoder_amd/ldpc_neural_decoder/_lib/variants
+V=${VARDIR:-$R/ab}
 VARS=$1; TLS=$2; shift 2
 run() {  # tag lib args...
   local tag=$1 lib=$2; shift 2

@@ -14,7 +14,7 @@ run gnn-z4 --workload gnn-z4 --steps 10 --warmup 3 --cpu-baseline-seconds 10
 run gnn-z4-bf16 --workload gnn-z4-bf16 --steps 10 --warmup 3 --cpu-baseline-seconds 0
 run gnn-z32 --workload gnn-z32 --steps 3 --warmup 1 --cpu-baseline-seconds 10
 run gnn-z32-codewords --workload gnn-z32 --data codewords --steps 3 --warmup 1 --cpu-baseline-seconds 0
-run gnn-z32-bf16 --workload gnn-z32-bf16 --steps 3 --warmup 1 --cpu-baseline-seconds 0
+run gnn-z32-bf16 --workload gnn-z32-bf16 --steps 3 --warmup 1 --cpu-baseline-seconds 10
 run gnn-z32-bf16-codewords --workload gnn-z32-bf16 --data codewords --steps 3 --warmup 1 --cpu-baseline-seconds 0
 run gnn-z32-bf16-noet --workload gnn-z32-bf16 --early-termination off --steps 3 --warmup 1 --cpu-baseline-seconds 0
 run gnn-z32-bf16-codewords-noet --workload gnn-z32-bf16 --data codewords --early-termination off --steps 3 --warmup 1 --cpu-baseline-seconds 0
@@ -23,7 +23,7 @@ run gnn-train-z32 --workload gnn-train-z32 --steps 5 --warmup 2 --cpu-baseline-s
 run gnn-train-z4 --workload gnn-train-z4 --steps 5 --warmup 2 --cpu-baseline-seconds 10
 run lay-z32 --workload lay-z32 --steps 10 --warmup 3 --cpu-baseline-seconds 10
 run gnn-z32-sweep --workload gnn-z32-sweep --steps 1 --warmup 1 --cpu-baseline-seconds 0
-run minsum-z32-stream --workload minsum-z32-stream --steps 10 --warmup 2 --cpu-baseline-seconds 0
+run minsum-z32-stream --workload minsum-z32-stream --steps 10 --warmup 2 --cpu-baseline-seconds 5
 run minsum-z384 --workload minsum-z384 --steps 5 --warmup 2 --cpu-baseline-seconds 0
 run hybrid-minsum-z32 --workload hybrid-minsum-z32 --steps 10 --warmup 2 --cpu-baseline-seconds 0
 run hybrid-gnn-z32 --workload hybrid-gnn-z32 --steps 3 --warmup 1 --cpu-baseline-seconds 0
