@@ -41,7 +41,10 @@ namespace ldpc {
 namespace {
 
 constexpr int kMaxH = 64;         // widest H of the LDS-image kernels (train_mlp_bwd_kernel, train_outer_kernel)
-X
+// widest H trained: the forward runs gnn_mlp_tiled_kernel (fma chains) up to 256, the products the wide
+// backward recomputes; past 256 the forward's generic kernel rounds mul + add, so hv and the ReLU masks
+// the backward rebuilt could differ from the forward's in the last bit
+constexpr int kMaxTrainH = 256;
 
 struct TW {  // one layer's weights in the blob (see ldpc_amd.h)
     const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
