@@ -133,6 +133,8 @@ struct GnnLayer {
     float *S_out = nullptr;
     const float *S_in = nullptr, *memb = nullptr;
 };
+
+
 __device__ __forceinline__ float4 hyb_x(float4 f, float v, float4 w, float4 c) {
     return make_float4((v * w.x + c.x) + f.x, (v * w.y + c.y) + f.y, (v * w.z + c.z) + f.z, (v * w.w + c.w) + f.w);
 }
@@ -870,6 +872,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     const float bo = P.last ? P.bo[0] : 0.0f;
     const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
     float S[32];  // row walk: this lane's check's running sum of output rows (its half's 32 units)
+
     // One 32-message tile: slot j is message m of frame b (row rr of x); ok = a real message (a padding
     // slot computes on a valid row and writes nothing); d1t = a degree-1 var tile; pc = the slot's
     // projected check row (+ 4 half).
@@ -1015,10 +1018,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 #pragma unroll
                 for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        *reinterpret_cast<float4 *>(dst + 32 * ot + 8 * q + 4 * half) =
-                            make_float4(S[16 * ot + 4 * q], S[16 * ot + 4 * q + 1], S[16 * ot + 4 * q + 2],
-                                        S[16 * ot + 4 * q + 3]);
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 v = make_float4(S[16 * ot + 4 * q], S[16 * ot + 4 * q + 1], S[16 * ot + 4 * q + 2],
+                                                     S[16 * ot + 4 * q + 3]);
+                        *reinterpret_cast<float4 *>(dst + 32 * ot + 8 * q + 4 * half) = v;
+                    }
             }
         }
         return;
