@@ -20,6 +20,8 @@ Workloads (BASELINE.json configs):
   gnn-z32-bf16 cfg5 per GPU: same code, 15 layers, bf16 features + bf16 MFMA (fp32 accumulate),
               per-frame early-termination syndrome check after every layer (avg_layers reported)
   gnn-z32-bf16-i10  cfg4 shape (10 layers) on the bf16 path: the north-star "10 iterations" GNN line
+  gnn-z32-h128  cfg4's code and depth at hidden_dim 128 (the reference builds any width, MGD:22/:162):
+              the MFMA row GEMMs of gnn_wide.hip, fp32, random weights
   gnn-z32-sweep  cfg4 as BASELINE states it: the on-device SNR sweep 0..6 dB step 1 (sweep.py
               evaluate_message_gnn = run_comparison_all.py:245-295), fp32, B frames per GPU per SNR;
               one step = one whole sweep (channel + decode + counters, RCCL all-reduce at the end)
@@ -51,6 +53,8 @@ VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 VALU instructions/s (1e9): 1024 SIMDs
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X fp32 matrix (spec), same guide
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X bf16 dense MFMA (spec, no sparsity)
 
+HIDDEN = {"gnn-z32-h128": 128}  # hidden_dim of the GNN workloads (default 64)
+
 WORKLOADS = {
     # name: (decoder, Z, iterations, default batch per GPU, SNR dB)
     "minsum-z32": ("minsum", 32, 10, 65536, 2.0),
@@ -60,6 +64,7 @@ WORKLOADS = {
     "bp-z32": ("bp", 32, 10, 65536, 2.0),
     "gnn-z4": ("gnn", 4, 5, 4096, 2.0),
     "gnn-z32": ("gnn", 32, 10, 32768, 2.0),
+    "gnn-z32-h128": ("gnn", 32, 10, 8192, 2.0),
     "gnn-z32-bf16": ("gnn-bf16", 32, 15, 32768, 2.0),
     "gnn-z4-bf16": ("gnn-bf16", 4, 5, 4096, 2.0),
     "gnn-z32-bf16-i10": ("gnn-bf16", 32, 10, 32768, 2.0),
@@ -232,7 +237,7 @@ def cpu_baseline(workload, z, iters, target_s):
         from ldpc_neural_decoder.models import create_message_gnn_decoder
         torch.manual_seed(7)
         dec, conv = create_message_gnn_decoder(torch.from_numpy(H), num_iterations=iters,
-                                               hidden_dim=64, base_graph=torch.from_numpy(base), Z=z)
+                                               hidden_dim=HIDDEN.get(workload, 64), base_graph=torch.from_numpy(base), Z=z)
         sd = {k: v.detach() for k, v in dec.state_dict().items()}
         types = conv.get_message_types(torch.from_numpy(base), z)
         ev, ec = conv.edge_var, conv.edge_chk
@@ -260,7 +265,7 @@ def cpu_baseline(workload, z, iters, target_s):
         run(b)
         dt = time.perf_counter() - t0
         return {"value": b / dt, "unit": "codewords/s", "cores": torch.get_num_threads(), "kind": "port",
-                "sample": f"{b} frames, BG2 Z={z}, MessageGNN {iters} layers H=64 fp32, {snr} dB, "
+                "sample": f"{b} frames, BG2 Z={z}, MessageGNN {iters} layers H={HIDDEN.get(workload, 64)} fp32, {snr} dB, "
                           f"{'forward + BCE + autograd backward' if train else 'forward'}, "
                           f"oracle.gnn_forward (torch CPU, segment means) on {cpu} with "
                           f"{torch.get_num_threads()} threads, {dt:.1f} s"}
@@ -438,9 +443,10 @@ def main():
     else:
         from ldpc_neural_decoder.models import create_message_gnn_decoder
         torch.manual_seed(7)
-        gdec, conv = create_message_gnn_decoder(H, num_iterations=iters, hidden_dim=64,
+        hid = HIDDEN.get(a.workload, 64)
+        gdec, conv = create_message_gnn_decoder(H, num_iterations=iters, hidden_dim=hid,
                                                 base_graph=base, Z=z)
-        ckpt = a.checkpoint or os.path.join(ROOT, "checkpoints", f"gnn_bg2_z{z}_i{iters}_h64.pt")
+        ckpt = a.checkpoint or os.path.join(ROOT, "checkpoints", f"gnn_bg2_z{z}_i{iters}_h{hid}.pt")
         if kind != "hybrid-gnn" and os.path.exists(ckpt):
             # a checkpoint written by the trainer (tools/train_gnn_checkpoint.py): tensors and plain data only
             ck = torch.load(ckpt, map_location="cpu", weights_only=True)
@@ -507,12 +513,17 @@ def main():
         # fp32 forward FLOPs per frame-layer as executed: the reference's MLPs cost 12 H^2 per message
         # (two sides x (W1 over [c; g]: 4 H^2 + W2: 2 H^2)); W1's group half is applied once per group
         # (gnn.hip, gnn_group_proj_kernel), so 8 H^2 per message + 2 H^2 per var / check group
-        fwd_flops = 8 * 64 * 64 * E + 2 * 64 * 64 * (g_n + g_m)
-        mlp_flops = 8 * 64 * 64 * E  # of which on the MLP kernel (bf16x6 splits)
-        nominal_flops = 12 * 64 * 64 * E
+        fwd_flops = 8 * hid * hid * E + 2 * hid * hid * (g_n + g_m)
+        mlp_flops = 8 * hid * hid * E  # of which on the MLP kernel (bf16x6 splits)
+        nominal_flops = 12 * hid * hid * E
         if kind == "hybrid-gnn":
             # check side only: 4 H^2 per message (W1 over c + W2) + 2 H^2 per check group (projection)
             per_launch_alg = (4 * 64 * 64 * E + 2 * 64 * 64 * g_m) * B * iters
+            bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
+        elif kind == "gnn" and hid != 64:
+            # the reference's useful FLOPs (12 H^2 E per frame-layer) against the fp32 MFMA peak
+            # (the row GEMMs execute them as bf16x6 splits on the bf16 MFMA: see notes)
+            per_launch_alg = nominal_flops * B * iters
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         elif kind in ("gnn-sweep", "gnn") and z == 32:
             # SURVEY 8(d) cfg4, HBM: per frame-layer 3 passes over the fp32 features (E x 64) + the

@@ -1300,8 +1300,19 @@ __global__ void gnn_memb_kernel(const float *__restrict__ emb0, int64_t layer_st
 
 int64_t layer_floats(int H, int T) { return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1; }
 
+// H = 32 k other than 64 (gnn_wide.hip) on the MFMA row GEMMs; LDPC_GNN_WIDE=0 keeps the VALU
+// kernels (A/B runs).  Read once: the workspace size depends on it.
+bool wide_on(const ldpc_gnn_plan *p, int H) {
+    static const bool env = [] {
+        const char *e = std::getenv("LDPC_GNN_WIDE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return env && gnn_wide_supported(H) && !p->weighted && p->n_gtiles > 0;
+}
+
 struct Ws {
     float *xa, *xb, *Mv, *Mc, *msg_out, *wt;
+    float *Pv, *Pc, *hbuf;  // wide path: projected group rows (B, G, H), MLP hidden rows (B, E, 2 H)
     float *S, *memb;  // row walk (H = 64, plan rw_*): per-check feature sums (B, Gc, H), mean type embeddings (L, Gc, H)
     int32_t *csr;
     int64_t bytes;
@@ -1312,8 +1323,9 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     const int64_t es = 4;  // bytes per stored feature (fp32 path)
     (void)precision;
-    const int64_t xb = layers > 1 ? al(B * p->E * H * es) : 0;
-    const int64_t xb2 = layers > 2 ? xb : 0;
+    const bool wide = wide_on(p, H);  // the last layer's rows are stored too (its head reads them)
+    const int64_t xb = layers > 1 || wide ? al(B * p->E * H * es) : 0;
+    const int64_t xb2 = layers > 2 || (wide && layers > 1) ? xb : 0;
     const int64_t mv = al(B * (int64_t)p->Gv * H * es), mc = al(B * (int64_t)p->Gc * H * es);
     const int64_t vs = al(B * p->E * 4), cs = al(gnn_csr_ints(p->E, N) * 4);
     char *c = static_cast<char *>(base);
@@ -1325,14 +1337,19 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     w.csr = reinterpret_cast<int32_t *>(c + xb + xb2 + mv + mc + vs);
     // H != 64 (gnn_mlp_tiled_kernel): every layer's transposed MLP weights, 6 H^2 floats each
     // (formed once per call, before the frame halves fork onto two streams)
-    const int64_t wtb = H != 64 && H <= kTiledMaxH ? al(6LL * H * H * 4 * layers) : 0;
+    const int64_t wtb = H != 64 && H <= kTiledMaxH && !wide ? al(6LL * H * H * 4 * layers) : 0;
     w.wt = wtb ? reinterpret_cast<float *>(c + xb + xb2 + mv + mc + vs + cs) : nullptr;
     const int64_t rwb = H == 64 && p->n_rw > 0 && layers > 1 ? mc : 0;
     const int64_t mbb = rwb ? al((int64_t)layers * p->Gc * H * es) : 0;
     char *r = c + xb + xb2 + mv + mc + vs + cs + wtb;
     w.S = rwb ? reinterpret_cast<float *>(r) : nullptr;
     w.memb = rwb ? reinterpret_cast<float *>(r + rwb) : nullptr;
-    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb;
+    const int64_t hb = wide ? al(B * p->E * 2 * H * es) : 0;
+    char *q = r + rwb + mbb;
+    w.Pv = wide ? reinterpret_cast<float *>(q) : nullptr;
+    w.Pc = wide ? reinterpret_cast<float *>(q + mv) : nullptr;
+    w.hbuf = wide ? reinterpret_cast<float *>(q + mv + mc) : nullptr;
+    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb + (wide ? mv + mc + hb : 0);
     return w;
 }
 
@@ -1870,6 +1887,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     L.Mv = w.Mv; L.Mc = w.Mc;
     L.vside = 1;
     const bool mfma = H == kMfmaH;
+    const bool wide = wide_on(p, H);
     if (!mfma && H > kMaxGenericH) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be <= " + std::to_string(kMaxGenericH));
     const size_t mfma_lds = (size_t)(kOffEmb + types * kEmbStride) * 4;
     if (mfma && mfma_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
@@ -1942,6 +1960,24 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         L.x_out = d_saved ? d_saved + (int64_t)l * B * p->E * H + xoff
                           : L.last ? nullptr : ((l % 2 == 0) ? w.xa : w.xb) + xoff;
         L.msg_out = w.msg_out + b0 * p->E;
+        if (wide) {
+            GnnWideLayer W{};
+            W.plan = p;
+            W.H = H; W.T = types; W.N = N; W.B = nb; W.E = p->E;
+            W.x_in = x_in;
+            W.llr = L.llr; W.msg_type = d_msg_type; W.msg_var = d_msg_var; W.w_in = L.w_in; W.b_in = L.b_in;
+            W.emb = L.emb; W.w1v = L.w1v; W.b1v = L.b1v; W.w2v = L.w2v; W.b2v = L.b2v;
+            W.w1c = L.w1c; W.b1c = L.b1c; W.w2c = L.w2c; W.b2c = L.b2c; W.wo = L.wo; W.bo = L.bo;
+            W.Mv = L.Mv; W.Mc = L.Mc;
+            W.Pv = w.Pv + b0 * p->Gv * H; W.Pc = w.Pc + b0 * p->Gc * H;
+            W.hbuf = w.hbuf + b0 * p->E * 2 * H;
+            W.y = L.x_out ? L.x_out : ((l % 2 == 0) ? w.xa : w.xb) + xoff;  // the last layer: a free buffer
+            W.residual = l > 0;
+            W.msg_out = L.last ? L.msg_out : nullptr;
+            if (int rc = gnn_wide_layer(W, st)) return rc;
+            x_in = W.y;
+            continue;
+        }
         const int64_t waves = nb * (int64_t)(p->Gv + p->Gc);
         L.d1 = H == 64 && gm_tiles() && d1_skip() && !p->weighted;
         if (proj) {

@@ -92,6 +92,25 @@ int gnn_project_groups(const ldpc_gnn_plan *p, int types, const float *d_weights
                        const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
                        float *d_pv, float *d_pc, float *d_gv, float *d_gc, hipStream_t s);
 
+// fp32 layer at hidden widths H = 32 k other than 64 (gnn_wide.hip): row GEMMs on the bf16 MFMA with
+// three-term splits.  Pointers are offset to the frame range [0, B); y = the layer's output rows
+// (x_out); msg_out set on the last layer (the output head is applied to y).
+struct GnnWideLayer {
+    const ldpc_gnn_plan *plan;
+    int H, T, N;
+    int64_t B, E;
+    const float *x_in;  // (B, E, H), null at layer 0
+    const float *llr;
+    const int32_t *msg_type, *msg_var;
+    const float *w_in, *b_in;
+    const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
+    float *Mv, *Mc, *Pv, *Pc, *hbuf, *y;
+    int residual;
+    float *msg_out;
+};
+bool gnn_wide_supported(int H);
+int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s);
+
 // The per-device side stream and the calling thread's fork/join events the forwards split their
 // frames over (thread-safe: see gnn.hip).
 int gnn_side_stream(hipStream_t *side, hipEvent_t *fork, hipEvent_t *join);

@@ -1,0 +1,426 @@
+// gnn_wide.hip -- MessageGNNLayer (message_gnn_decoder.py:51-129) for hidden widths H = 32 k other
+// than 64 (96 .. 256) on the bf16 MFMA, with every fp32 product as the three-term split of
+// gnn_mlp2s_kernel (fp32-accurate: v = v0 + v1 + v2 in bf16, six cross products, fp32 accumulator).
+//
+// The H = 64 path keeps a layer's four weight matrices in LDS and runs the whole MLP per 32-message
+// tile.  At H = 128 the split images of those matrices are 384 KB, so a layer here is a sequence of
+// row GEMMs, each over one slice of output units whose split weight images fit a CU's LDS:
+//   gnn_wide_gm_kernel   group means of c = x + emb[type] (the normalized clique adjacencies of
+//                        MGD:108/118 are segment means): Mv (B, Gv, H), Mc (B, Gc, H)
+//   gnn_wgemm_kernel     P_s = W1_s,right g_s + b1_s per group          (mode PROJ, both sides)
+//                        h_s = relu(W1_s,left c + P_s[group(m)])        (mode GEMM1, per side)
+//                        y = W2_v h_v + W2_c h_c + b2_v + b2_c (+ x)    (mode GEMM2, K = 2 H)
+//   gnn_wide_head_kernel msg_out = wo . y + bo on the last layer (MGD:142, :270)
+// h (B, E, 2 H) fp32 is the one extra round trip through HBM.  Each launch is persistent: a
+// workgroup holds one output slice's split images in LDS and its waves walk 32-row tiles; the
+// slices of one XCD walk the same tiles in step, so the input rows are read from HBM once per XCD
+// and hit L2 for the other slices (placement changes speed only, never results).
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
+#include "common.hpp"
+#include "gnn.hpp"
+
+namespace ldpc {
+namespace {
+
+typedef float f32x16w __attribute__((ext_vector_type(16)));
+
+enum WMode { kProj = 0, kGemm1 = 1, kGemm2 = 2 };
+
+struct WArgs {
+    int mode;
+    int K;             // reduction length (H, or 2 H for GEMM2)
+    int H;             // output row width
+    int NS;            // output units per workgroup slice (32 * NT)
+    int64_t R;         // rows
+    // input rows: in + r * in_stride (K floats); GEMM1 at layer 0: x = llr w_in + b_in
+    const float *in;
+    int64_t in_stride;
+    // weights: row u of the (H x ld) matrix W, columns col0 .. col0 + K (GEMM2: W2v | W2c)
+    const float *w_a, *w_b;  // GEMM2: W2v, W2c; else w_a = W1_s (H x 2H), w_b unused
+    int ld, col0;
+    // GEMM1: c = x + emb[type]; rows are (frame, message) pairs of E messages
+    const float *emb;      // (T, H)
+    const int32_t *msg_type, *msg_var;
+    const float *llr, *w_in, *b_in;
+    int N, T;
+    int64_t E;
+    // init: PROJ bias vector b (H); GEMM1 P_s rows (B, G, H) indexed by grp[m]; GEMM2 b2v + b2c
+    const float *init_a, *init_b;
+    const int32_t *grp;
+    int G;
+    const float *resid;    // GEMM2: x (B E, H) or null
+    float *out;
+    int64_t out_stride;    // floats per output row
+};
+
+constexpr int kWRowPad = 8;  // bf16 per image row past K: conflict-free ds_read_b128 (as gnn_bf16.hip's W1)
+__host__ __device__ inline size_t wgemm_img_bytes(int NS, int K) { return (size_t)3 * NS * (K + kWRowPad) * 2; }
+inline size_t wgemm_lds_bytes(const WArgs &a) {
+    size_t b = wgemm_img_bytes(a.NS, a.K);
+    if (a.mode == kGemm1) b += (size_t)(a.T + 2) * a.H * 4;  // emb rows, w_in, b_in (fp32)
+    b += (size_t)a.NS * 4;                                  // the slice's init vector (PROJ / GEMM2)
+    return (b + 15) / 16 * 16;
+}
+
+__device__ __forceinline__ void split3w(const float *v, bf16x8_t &a, bf16x8_t &b, bf16x8_t &c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const __bf16 h0 = (__bf16)v[i];
+        const float r1 = v[i] - (float)h0;
+        const __bf16 h1 = (__bf16)r1;
+        a[i] = h0;
+        b[i] = h1;
+        c[i] = (__bf16)(r1 - (float)h1);
+    }
+}
+
+// ReLU as one integer max on the bits (gnn.hip relu_i)
+__device__ __forceinline__ float relu_w(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
+
+// NT accumulator tiles of 32 output units per wave; 512 threads (8 waves) per workgroup, one or two
+// workgroups per CU by the LDS image
+constexpr int kWThreads = 512, kWWaves = kWThreads / 64;
+constexpr int kWAhead = 4;  // input k-steps in flight ahead of the one being multiplied
+template <int NT>
+__global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int nslices) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
+    constexpr int NS = 32 * NT;
+    // placement: XCD x = blockIdx % 8 hosts every slice; the blocks of (x, slice) share x's tile range
+    const int x = blockIdx.x % 8, ix = blockIdx.x / 8;
+    const int per_x = gridDim.x / 8;
+    const int slice = ix % nslices, rank = ix / nslices;
+    const int nrank = per_x / nslices;
+    if (rank >= nrank) return;
+    const int n0 = slice * NS;
+    const int K = A.K, rowb = K + kWRowPad;  // bf16 per image row
+    __bf16 *img = reinterpret_cast<__bf16 *>(smem);
+    const int imgstride = NS * rowb;
+    for (int i = tid; i < NS * K; i += kWThreads) {
+        const int u = i / K, k = i - u * K;
+        const float w = A.mode == kGemm2 ? (k < A.H ? A.w_a[(int64_t)(n0 + u) * A.H + k] : A.w_b[(int64_t)(n0 + u) * A.H + k - A.H])
+                                         : A.w_a[(int64_t)(n0 + u) * A.ld + A.col0 + k];
+        split_store(w, img + u * rowb + k, imgstride);
+    }
+    float *tabs = reinterpret_cast<float *>(smem + wgemm_img_bytes(NS, K));
+    float *initv = tabs;  // [NS]
+    float *embs = tabs + NS;  // GEMM1: emb [T][H], w_in [H], b_in [H]
+    if (A.mode != kGemm1)
+        for (int i = tid; i < NS; i += kWThreads)
+            initv[i] = A.mode == kGemm2 ? A.init_a[n0 + i] + A.init_b[n0 + i] : A.init_a[n0 + i];
+    if (A.mode == kGemm1) {
+        for (int i = tid; i < A.T * A.H; i += kWThreads) embs[i] = A.emb[i];
+        for (int i = tid; i < A.H; i += kWThreads) {
+            embs[A.T * A.H + i] = A.w_in[i];
+            embs[(A.T + 1) * A.H + i] = A.b_in[i];
+        }
+    }
+    __syncthreads();
+
+    // this XCD's contiguous tile range, walked by the (x, slice) blocks' waves interleaved
+    const int64_t ntiles = (A.R + 31) / 32;
+    const int64_t t0 = ntiles * x / 8, t1 = ntiles * (x + 1) / 8;
+    const int ksteps = K / 16;
+    // Per tile: the row context (row, frame, message, input pointer, type embedding, LLR).  Past the
+    // end a context points at a valid row (its loads are discarded): no branch around any load.
+    struct Ctx {
+        int64_t t, rr, fb, m;
+        bool ok, live;
+        const float *src, *eb;
+        float lv;
+    };
+    auto ctx_of = [&](int64_t t) {
+        Ctx c;
+        c.t = t;
+        c.live = t < t1;
+        const int64_t r = t * 32 + j;
+        c.ok = c.live && r < A.R;
+        c.rr = c.ok ? r : A.R - 1;
+        c.fb = 0;
+        c.m = 0;
+        if (A.mode == kGemm1) {
+            c.fb = c.rr / A.E;
+            c.m = c.rr - c.fb * A.E;
+        }
+        c.src = A.in ? A.in + c.rr * A.in_stride + 8 * h : nullptr;
+        c.eb = A.mode == kGemm1 ? embs + A.msg_type[c.m] * A.H + 8 * h : nullptr;
+        c.lv = (A.mode == kGemm1 && !A.in) ? A.llr[c.fb * A.N + A.msg_var[c.m]] : 0.0f;
+        return c;
+    };
+    // input chunk of k-step s: units 16 s + 8 h .. + 7 of the context's row (before the embedding)
+    auto chunk = [&](const Ctx &c, int s, float *v) {
+        if (c.src) {
+            const float4 a = *reinterpret_cast<const float4 *>(c.src + 16 * s);
+            const float4 b = *reinterpret_cast<const float4 *>(c.src + 16 * s + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {  // layer 0: Linear(1, H) of the message's LLR
+            const float *wi = embs + A.T * A.H + 16 * s + 8 * h, *bi = wi + A.H;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = c.lv * wi[i] + bi[i];
+        }
+    };
+    const int64_t stride = (int64_t)nrank * kWWaves;
+    Ctx cur = ctx_of(t0 + (int64_t)rank * kWWaves + wave);
+    if (!cur.live) return;
+    // a ring of kWAhead input chunks, continuous over tiles: while chunk s of this tile is multiplied,
+    // chunk s + kWAhead -- of this tile, or of the next one near the end -- is in flight
+    float ring[kWAhead][8];
+#pragma unroll
+    for (int a = 0; a < kWAhead; ++a) chunk(cur, a, ring[a]);  // K >= 96: ksteps >= kWAhead
+    const __bf16 *wl = img + j * rowb + 8 * h;
+    while (cur.live) {
+        const Ctx nxt = ctx_of(cur.t + stride);
+        // accumulators start from the additive term (GEMM1: the projected group row; GEMM2: b2 + x;
+        // projection: b1), loaded with the tile's first chunks instead of after its last MFMA
+        f32x16w acc[NT];
+        {
+            const float *ip = A.mode == kGemm1 ? A.init_a + (cur.fb * A.G + A.grp[cur.m]) * A.H + n0 + 4 * h : nullptr;
+            const float *xp = A.resid ? A.resid + cur.rr * A.H + n0 + 4 * h : nullptr;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int u = 32 * tt + 8 * q;
+                    float4 iv = ip ? *reinterpret_cast<const float4 *>(ip + u) : *reinterpret_cast<const float4 *>(initv + u + 4 * h);
+                    if (xp) {
+                        const float4 xv = *reinterpret_cast<const float4 *>(xp + u);
+                        iv = make_float4(xv.x + iv.x, xv.y + iv.y, xv.z + iv.z, xv.w + iv.w);
+                    }
+                    acc[tt][4 * q] = iv.x; acc[tt][4 * q + 1] = iv.y; acc[tt][4 * q + 2] = iv.z; acc[tt][4 * q + 3] = iv.w;
+                }
+        }
+        for (int s0 = 0; s0 < ksteps; s0 += kWAhead) {
+#pragma unroll
+            for (int a = 0; a < kWAhead; ++a) {
+                const int s = s0 + a;
+                if (s < ksteps) {
+                    float v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = ring[a][i] + (cur.eb ? cur.eb[16 * s + i] : 0.0f);
+                    if (s + kWAhead < ksteps)
+                        chunk(cur, s + kWAhead, ring[a]);
+                    else
+                        chunk(nxt, s + kWAhead - ksteps, ring[a]);
+                    bf16x8_t b0, b1, b2;
+                    split3w(v, b0, b1, b2);
+#pragma unroll
+                    for (int q = 0; q < NT; ++q) acc[q] = mfma6(wl + 32 * q * rowb + 16 * s, b0, b1, b2, acc[q], imgstride);
+                }
+            }
+        }
+        if (cur.ok) {
+            // register 4 q + i of tile tt holds unit n0 + 32 tt + 8 q + 4 h + i of the row
+            float *op = A.out + cur.rr * A.out_stride + n0 + 4 * h;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float4 o = make_float4(acc[tt][4 * q], acc[tt][4 * q + 1], acc[tt][4 * q + 2], acc[tt][4 * q + 3]);
+                    if (A.mode == kGemm1) o = make_float4(relu_w(o.x), relu_w(o.y), relu_w(o.z), relu_w(o.w));
+                    *reinterpret_cast<float4 *>(op + 32 * tt + 8 * q) = o;
+                }
+        }
+        cur = nxt;
+    }
+}
+
+// Group means of c = x + emb[type] (layer 0: x = llr w_in + b_in) over the plan's group tiles
+// (gnn.hpp gt_*: 8 groups of one degree per tile, var side then check side): H / 4 lanes per group
+// (one float4 each), 64 / (H / 4) groups per wave, members in ascending order, four in flight.
+struct WGm {
+    const float *x;        // (B, E, H) or null (layer 0)
+    const float *llr, *w_in, *b_in, *emb;
+    const int32_t *msg_type, *msg_var;
+    const int2 *meta;
+    const int32_t *grp, *mem;
+    int n_tiles;
+    const float *inv_v, *inv_c;
+    float *Mv, *Mc;
+    int Gv, Gc, H, N, gpw;  // gpw: groups per wave
+    int64_t E, B;
+};
+
+__global__ __launch_bounds__(256) void gnn_wide_gm_kernel(WGm A) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, lg = A.H / 4;
+    const int wpt = 8 / A.gpw;  // waves per tile
+    const int64_t tile_w = w / wpt;
+    if (tile_w >= A.B * A.n_tiles) return;
+    const int64_t b = tile_w / A.n_tiles;
+    const int t = (int)(tile_w - b * A.n_tiles);
+    const int q = (int)(w - tile_w * wpt) * A.gpw + lane / lg, u = 4 * (lane % lg);
+    if (lane / lg >= A.gpw) return;
+    const int2 md = A.meta[t];
+    const int g = A.grp[8 * t + q];
+    if (g < 0) return;
+    const int32_t *mem = A.mem + md.y + q;
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    auto feat = [&](int mm) {
+        if (A.x) return *reinterpret_cast<const float4 *>(A.x + (b * A.E + mm) * A.H + u);
+        const float l = A.llr[b * A.N + A.msg_var[mm]];
+        const float4 wi = *reinterpret_cast<const float4 *>(A.w_in + u), bi = *reinterpret_cast<const float4 *>(A.b_in + u);
+        return make_float4(l * wi.x + bi.x, l * wi.y + bi.y, l * wi.z + bi.z, l * wi.w + bi.w);
+    };
+    auto add = [&](float4 v, int mm) {
+        const float4 e = *reinterpret_cast<const float4 *>(A.emb + (int64_t)A.msg_type[mm] * A.H + u);
+        s.x += v.x + e.x; s.y += v.y + e.y; s.z += v.z + e.z; s.w += v.w + e.w;
+    };
+    int i = 0;
+    for (; i + 4 <= md.x; i += 4) {  // four members' rows in flight, summed in ascending order
+        const int m0 = mem[8 * i], m1 = mem[8 * i + 8], m2 = mem[8 * i + 16], m3 = mem[8 * i + 24];
+        const float4 v0 = feat(m0), v1 = feat(m1), v2 = feat(m2), v3 = feat(m3);
+        add(v0, m0);
+        add(v1, m1);
+        add(v2, m2);
+        add(v3, m3);
+    }
+    for (; i < md.x; ++i) add(feat(mem[8 * i]), mem[8 * i]);
+    const bool isv = g < A.Gv;
+    const int gg = isv ? g : g - A.Gv;
+    const float inv = isv ? A.inv_v[gg] : A.inv_c[gg];
+    float *dst = isv ? A.Mv + (b * A.Gv + gg) * A.H : A.Mc + (b * A.Gc + gg) * A.H;
+    *reinterpret_cast<float4 *>(dst + u) = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+}
+
+// msg_out[r] = wo . y[r] + bo (16 lanes per row)
+__global__ __launch_bounds__(256) void gnn_wide_head_kernel(const float *__restrict__ y, int H, int64_t R,
+                                                            const float *__restrict__ wo, const float *__restrict__ bo,
+                                                            float *__restrict__ msg_out) {
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int q = threadIdx.x & 15;
+    if (r >= R) return;
+    const float *yr = y + r * H;
+    float part = 0.0f;
+    for (int u = q; u < H; u += 16) part += yr[u] * wo[u];
+    for (int off = 8; off > 0; off >>= 1) part += __shfl_xor(part, off, 16);
+    if (q == 0) msg_out[r] = part + bo[0];
+}
+
+int g_wcus = 0;
+
+int launch_wgemm(WArgs a, hipStream_t s) {
+    if (!g_wcus) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_wcus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (a.R <= 0) return LDPC_OK;
+    // the widest output slice (4, 2 or 1 tiles of 32 units) whose split images fit the LDS
+    const size_t extra = (a.mode == kGemm1 ? (size_t)(a.T + 2) * a.H * 4 : 0) + 4 * 128 + 16;
+    a.NS = 32;
+    for (int nt : {4, 2}) {
+        if (a.H % (32 * nt) == 0 && wgemm_img_bytes(32 * nt, a.K) + extra <= 160 * 1024) {
+            a.NS = 32 * nt;
+            break;
+        }
+    }
+    const size_t lds = wgemm_lds_bytes(a);
+    if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "hidden_dim too wide for the MFMA row GEMM's LDS image");
+    const int nslices = a.H / a.NS;
+    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
+    // blocks per XCD: a multiple of the slice count, about per_cu workgroups per CU
+    const int per_x = std::max(nslices, (g_wcus / 8) * per_cu / nslices * nslices);
+    const void *fn = a.NS == 128 ? reinterpret_cast<const void *>(gnn_wgemm_kernel<4>)
+                     : a.NS == 64 ? reinterpret_cast<const void *>(gnn_wgemm_kernel<2>)
+                                  : reinterpret_cast<const void *>(gnn_wgemm_kernel<1>);
+    LDPC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (a.NS == 128)
+        hipLaunchKernelGGL(gnn_wgemm_kernel<4>, dim3(8 * per_x), dim3(kWThreads), lds, s, a, nslices);
+    else if (a.NS == 64)
+        hipLaunchKernelGGL(gnn_wgemm_kernel<2>, dim3(8 * per_x), dim3(kWThreads), lds, s, a, nslices);
+    else
+        hipLaunchKernelGGL(gnn_wgemm_kernel<1>, dim3(8 * per_x), dim3(kWThreads), lds, s, a, nslices);
+    LDPC_CHECK_LAUNCH("gnn_wgemm_kernel");
+    return LDPC_OK;
+}
+
+}  // namespace
+
+bool gnn_wide_supported(int H) { return H != 64 && H % 32 == 0 && H >= 96 && H <= 256; }
+
+int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
+    const int H = L.H;
+    const int64_t BE = L.B * L.E;
+    // group means (every group: the H = 64 path's degree-1 shortcut is not taken here)
+    {
+        WGm g{};
+        g.x = L.x_in;
+        g.llr = L.llr; g.w_in = L.w_in; g.b_in = L.b_in; g.emb = L.emb;
+        g.msg_type = L.msg_type; g.msg_var = L.msg_var;
+        g.meta = L.plan->gt_meta; g.grp = L.plan->gt_grp; g.mem = L.plan->gt_mem; g.n_tiles = L.plan->n_gtiles;
+        g.inv_v = L.plan->inv_v; g.inv_c = L.plan->inv_c;
+        g.Mv = L.Mv; g.Mc = L.Mc;
+        g.Gv = L.plan->Gv; g.Gc = L.plan->Gc; g.H = H; g.N = L.N;
+        g.gpw = std::max(1, 64 / (H / 4));
+        g.E = L.E; g.B = L.B;
+        const int64_t waves = L.B * (int64_t)g.n_tiles * (8 / g.gpw);
+        hipLaunchKernelGGL(gnn_wide_gm_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, g);
+        LDPC_CHECK_LAUNCH("gnn_wide_gm_kernel");
+    }
+    WArgs base{};
+    base.H = H;
+    base.emb = L.emb; base.msg_type = L.msg_type; base.msg_var = L.msg_var;
+    base.llr = L.llr; base.w_in = L.w_in; base.b_in = L.b_in; base.N = L.N; base.T = L.T; base.E = L.E;
+    // projections P_s = W1_s,right g + b1_s
+    for (int side = 0; side < 2; ++side) {
+        WArgs a = base;
+        a.mode = kProj;
+        a.K = H;
+        a.R = L.B * (side ? L.plan->Gc : L.plan->Gv);
+        a.in = side ? L.Mc : L.Mv;
+        a.in_stride = H;
+        a.w_a = side ? L.w1c : L.w1v;
+        a.ld = 2 * H;
+        a.col0 = H;
+        a.init_a = side ? L.b1c : L.b1v;
+        a.out = side ? L.Pc : L.Pv;
+        a.out_stride = H;
+        if (int rc = launch_wgemm(a, s)) return rc;
+    }
+    // h_s = relu(W1_s,left c + P_s[group]) into h (B E, 2 H)
+    for (int side = 0; side < 2; ++side) {
+        WArgs a = base;
+        a.mode = kGemm1;
+        a.K = H;
+        a.R = BE;
+        a.in = L.x_in;
+        a.in_stride = H;
+        a.w_a = side ? L.w1c : L.w1v;
+        a.ld = 2 * H;
+        a.col0 = 0;
+        a.init_a = side ? L.Pc : L.Pv;
+        a.grp = side ? L.plan->cgroup : L.plan->vgroup;
+        a.G = side ? L.plan->Gc : L.plan->Gv;
+        a.out = L.hbuf + side * H;
+        a.out_stride = 2 * H;
+        if (int rc = launch_wgemm(a, s)) return rc;
+    }
+    // y = W2_v h_v + W2_c h_c + (b2_v + b2_c) (+ x): the reference's MLP_v + MLP_c (+ residual)
+    {
+        WArgs a = base;
+        a.mode = kGemm2;
+        a.K = 2 * H;
+        a.R = BE;
+        a.in = L.hbuf;
+        a.in_stride = 2 * H;
+        a.w_a = L.w2v;
+        a.w_b = L.w2c;
+        a.init_a = L.b2v;
+        a.init_b = L.b2c;
+        a.resid = L.residual ? L.x_in : nullptr;
+        a.out = L.y;
+        a.out_stride = H;
+        if (int rc = launch_wgemm(a, s)) return rc;
+    }
+    if (L.msg_out) {
+        hipLaunchKernelGGL(gnn_wide_head_kernel, dim3((unsigned)((BE * 16 + 255) / 256)), dim3(256), 0, s, L.y, H, BE,
+                           L.wo, L.bo, L.msg_out);
+        LDPC_CHECK_LAUNCH("gnn_wide_head_kernel");
+    }
+    return LDPC_OK;
+}
+
+}  // namespace ldpc

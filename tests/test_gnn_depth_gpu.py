@@ -27,11 +27,11 @@ TOL = 2e-5
 CFG_BATCH = 32768
 
 
-def _model(layers, cuda, seed=0, precision="fp32"):
+def _model(layers, cuda, seed=0, precision="fp32", hidden=64):
     torch.manual_seed(seed)
     base = load_base_matrix(code_path(32))
     H = expand_base_matrix(base, 32)
-    dec, conv = create_message_gnn_decoder(H, num_iterations=layers, hidden_dim=64, base_graph=base, Z=32)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=layers, hidden_dim=hidden, base_graph=base, Z=32)
     with torch.no_grad():
         for p in dec.parameters():
             p.mul_(0.5)
@@ -149,3 +149,19 @@ def test_split_mlp_is_fp32_accurate(cuda, oracle_mod, monkeypatch):
         err[split] = float(np.abs(_native(dec, conv, types, llr, cuda).cpu().numpy() - exact).max())
     ref_err = float(np.abs(f32 - exact).max())
     assert err["1"] <= 2 * max(err["0"], ref_err) + 1e-7, (err, ref_err)
+
+
+@pytest.mark.parametrize("hidden,layers", [(128, 10), (96, 6), (192, 4), (256, 3)])
+def test_wide_hidden_mfma_vs_oracle(cuda, oracle_mod, hidden, layers):
+    """hidden_dim = 32 k other than 64 (message_gnn_decoder.py:22, :162 take any width) on the MFMA
+    row GEMMs of gnn_wide.hip (bf16x6 splits: fp32 products): BG2 Z=32 against the oracle at the
+    H = 64 bar (|dprobs| <= 2e-5), H = 128 at cfg4's 10 layers; a sub-batch decodes bit-identically
+    to its rows of the full batch (a frame's output depends on that frame alone)."""
+    base, H, dec, conv, types = _model(layers, cuda, seed=hidden, hidden=hidden)
+    llr = awgn_llr(6, H.shape[1], 1.0, seed=hidden, device=cuda)
+    got = _native(dec, conv, types, llr, cuda).cpu().numpy()
+    ref = _oracle(oracle_mod, dec, conv, H, types, llr)
+    err = float(np.abs(got - ref).max())
+    assert err <= TOL, err
+    sub = _native(dec, conv, types, llr[2:5].contiguous(), cuda).cpu().numpy()
+    assert np.array_equal(sub, got[2:5])
