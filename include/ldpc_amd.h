@@ -197,7 +197,7 @@ int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types, int layer
                         const float *d_llr, int N, int64_t B, int precision, int flags, float *d_probs,
                         int32_t *d_iters, void *d_work, int64_t work_bytes, void *stream);
 
-/* ---- training (fp32, hidden_dim <= 64) -------------------------------------------------------
+/* ---- training (fp32, hidden_dim <= 256) ------------------------------------------------------
  * Replaces torch autograd through MessageGNNDecoder.forward + F.binary_cross_entropy
  * (message_gnn_decoder.py:190-317, :314), as driven by trainer.py:70-102 (zero_grad, forward,
  * loss.backward(), SGD step).
@@ -235,6 +235,24 @@ int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int types, int laye
                          int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
                          const float *d_layer_probs, const float *d_grad_layer_probs, float *d_grad_weights,
                          void *d_work, int64_t work_bytes, void *stream);
+/* Saved projections (round 5): the forward keeps every layer's projected group rows W1_s,right g_s +
+ * b1_s and group means g_s (the fp32 path's gnn_group_proj_kernel outputs) in d_proj, so that the
+ * backward does not recompute them.  hidden_dim 64 with a group plan; elsewhere the area is 0 floats
+ * and the _ex functions behave as the ones above.
+ * ldpc_gnn_train_proj_floats: float32 elements of d_proj = L * B * (Gv + Gc) * 2 * H, laid out per
+ *   layer as [Pv (B, Gv, H) | Pc (B, Gc, H) | gv (B, Gv, H) | gc (B, Gc, H)].
+ * ldpc_gnn_forward_train_ex / ldpc_gnn_backward_ds_ex: ldpc_gnn_forward_train / ldpc_gnn_backward_ds
+ *   with d_proj (null = recompute in the backward).  The backward only reads d_proj. */
+int64_t ldpc_gnn_train_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int layers);
+int ldpc_gnn_forward_train_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                              const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                              const float *d_llr, int N, int64_t B, float *d_probs, float *d_saved, float *d_proj,
+                              void *d_work, int64_t work_bytes, void *stream);
+int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
+                            const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N,
+                            int64_t B, const float *d_probs, const float *d_grad_probs, const float *d_saved,
+                            const float *d_proj, const float *d_layer_probs, const float *d_grad_layer_probs,
+                            float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream);
 
 /* ---- index-gather neural-BP layers (models/layers.py) ------------------
  * d_idx is the reference's (n_out, K) index tensor transposed to (K, n_out) int32, -1 = padding

@@ -537,6 +537,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
                     const float4 e = *reinterpret_cast<const float4 *>(P.memb + (int64_t)g * 64 + c4);
                     const float inv = P.inv_c[g];
                     mean = make_float4(sv.x * inv + e.x, sv.y * inv + e.y, sv.z * inv + e.z, sv.w * inv + e.w);
+                    if (P.gsave_c) *reinterpret_cast<float4 *>(P.gsave_c + ((int64_t)b * P.Gc + g) * 64 + c4) = mean;
                 }
                 *reinterpret_cast<float4 *>(gm + slot * kPS + c4) = mean;
             }
@@ -1857,9 +1858,15 @@ extern "C" int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, i
     return carve(p, hidden, N, B, layers, precision, nullptr).bytes;
 }
 
+int64_t ldpc::gnn_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int layers) {
+    if (hidden != kMfmaH || p->weighted || p->n_ptiles <= 0) return 0;
+    return (int64_t)layers * B * (p->Gv + p->Gc) * 2 * hidden;
+}
+
 int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
                            const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
-                           float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s) {
+                           float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s,
+                           float *d_proj) {
     const int H = hidden;
     Ws w = carve(p, H, N, B, layers, 0, d_work);
     if (!d_work || work_bytes < w.bytes)
@@ -1995,7 +2002,18 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
                 L.ntile_pf = p->n_mtiles;
                 L.ntile_v1 = p->n_mtiles_v1;
             }
-            const bool skip_v1 = rw ? rwd1 : d1t;
+            // training with saved projections (d_proj): this layer's projected rows and group means go
+            // to d_proj for the backward, every var group's included (the backward's GEMM1 reads them)
+            bool skip_v1 = rw ? rwd1 : d1t;
+            if (d_proj) {
+                const int64_t G = p->Gv + p->Gc;
+                float *base = d_proj + (int64_t)l * B * G * 2 * H;
+                L.Mv = base + b0 * p->Gv * H;
+                L.Mc = base + B * p->Gv * H + b0 * p->Gc * H;
+                L.gsave_v = base + B * G * H + b0 * p->Gv * H;
+                L.gsave_c = base + B * G * H + B * p->Gv * H + b0 * p->Gc * H;
+                skip_v1 = false;
+            }
             const ProjTiles T{p->pt_meta, p->pt_grp, p->pt_deg, p->pt_mem, p->n_ptiles, skip_v1 ? p->n_ptiles_v1 : 0};
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;

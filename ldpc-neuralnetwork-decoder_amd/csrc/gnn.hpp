@@ -81,9 +81,14 @@ __device__ __forceinline__ const int32_t *csr_mem(const int32_t *ints, int N) { 
 
 // fp32 forward (precision 0).  d_saved (L, B, E, H) or null: when set, layer l writes its output
 // features to d_saved[l] (the last layer included) for the backward pass (gnn_train.hip).
+// d_proj (training, H = 64 group plans; gnn_proj_floats floats, null = none): every layer's projected
+// group rows and group means, [l][Pv (B, Gv, H) | Pc (B, Gc, H) | gv (B, Gv, H) | gc (B, Gc, H)], kept
+// for the backward instead of recomputed there.
 int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
                      const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
-                     float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s);
+                     float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s,
+                     float *d_proj = nullptr);
+int64_t gnn_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int layers);
 
 // Layer `layer`'s projected group rows W1_s,right g + b1_s (d_pv / d_pc, (B, G, 64)) and, when
 // d_gv is set, the group means g themselves (d_gv / d_gc) of c = x + emb (x = d_x, or the LLR

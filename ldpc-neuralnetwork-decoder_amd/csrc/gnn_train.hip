@@ -1580,10 +1580,23 @@ extern "C" int64_t ldpc_gnn_train_workspace_size(const ldpc_gnn_plan *p, int hid
     return fwd > bwd ? fwd : bwd;
 }
 
+extern "C" int64_t ldpc_gnn_train_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int layers) {
+    if (!p || hidden <= 0 || B < 0 || layers <= 0) return fail(LDPC_EINVAL, "bad arguments");
+    return gnn_proj_floats(p, hidden, B, layers);
+}
+
 extern "C" int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                                       const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
                                       const float *d_llr, int N, int64_t B, float *d_probs, float *d_saved,
                                       void *d_work, int64_t work_bytes, void *stream) {
+    return ldpc_gnn_forward_train_ex(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
+                                     d_saved, nullptr, d_work, work_bytes, stream);
+}
+
+extern "C" int ldpc_gnn_forward_train_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                                         const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                                         const float *d_llr, int N, int64_t B, float *d_probs, float *d_saved,
+                                         float *d_proj, void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     if (hidden <= 0 || hidden > kMaxTrainH || types <= 0 || layers <= 0 || N <= 0 || B < 0)
@@ -1591,8 +1604,9 @@ extern "C" int ldpc_gnn_forward_train(const ldpc_gnn_plan *p, int hidden, int ty
     if (B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_saved)
         return fail(LDPC_EINVAL, "NULL tensor");
+    if (d_proj && gnn_proj_floats(p, hidden, B, layers) == 0) d_proj = nullptr;  // a path without the area
     return gnn_fp32_forward(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs, d_saved,
-                            d_work, work_bytes, static_cast<hipStream_t>(stream));
+                            d_work, work_bytes, static_cast<hipStream_t>(stream), d_proj);
 }
 
 extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int types, int layers,
@@ -1601,6 +1615,17 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
                                     const float *d_grad_probs, const float *d_saved, const float *d_layer_probs,
                                     const float *d_grad_layer_probs, float *d_grad_weights, void *d_work,
                                     int64_t work_bytes, void *stream) {
+    return ldpc_gnn_backward_ds_ex(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
+                                   d_grad_probs, d_saved, nullptr, d_layer_probs, d_grad_layer_probs, d_grad_weights,
+                                   d_work, work_bytes, stream);
+}
+
+extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers,
+                                       const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
+                                       const float *d_llr, int N, int64_t B, const float *d_probs,
+                                       const float *d_grad_probs, const float *d_saved, const float *d_proj,
+                                       const float *d_layer_probs, const float *d_grad_layer_probs,
+                                       float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
     if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     const int H = hidden, T = types, L = layers;
@@ -1641,6 +1666,8 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     // projected groups (see train_mlp_bwd_mfma_kernel): H = 64 on MFMA with the plan's projection tiles
     const bool pj = H == 64 && bwd_mfma() && bwd_proj() && p->n_ptiles > 0;
+    // the forward's saved projections (ldpc_gnn_forward_train_ex): no recompute here
+    const bool sp = pj && d_proj != nullptr;
     if (pj) {
         LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<512, true>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
@@ -1672,7 +1699,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         v.H = H; v.T = T; v.N = N; v.mode = 2; v.E = E; v.R = R;
         if (int rc = launch_vec(v, w.hv, w.hc, s)) return rc;
     }
-    const bool ovl = pj && L > 1 && bwd_overlap();
+    const bool ovl = pj && L > 1 && bwd_overlap() && !sp;
     hipStream_t s2 = nullptr;
     hipEvent_t ev_ready[2] = {}, ev_free[2] = {};
     int rc0 = 0;
@@ -1719,8 +1746,18 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         // with the side stream, odd layers use the second set
         const bool odd = ovl && (l & 1);
         float *Mv = odd ? w.Mv1 : w.Mv, *Mc = odd ? w.Mc1 : w.Mc;
-        float *Gsv = odd ? w.Gs1v : w.da, *Gsc = odd ? w.Gs1c : w.db;
-        if (ovl) {
+        const float *Gsv = odd ? w.Gs1v : w.da, *Gsc = odd ? w.Gs1c : w.db;
+        // projected rows the MLP backward reads (Pv / Pc) and the buffers that then receive the
+        // group sums of dh (Mv / Mc): one set when recomputed here, apart with saved projections
+        const float *Pv = Mv, *Pc = Mc;
+        if (sp) {
+            const int64_t G = p->Gv + p->Gc;
+            const float *base = d_proj + (int64_t)l * B * G * 2 * H;
+            Pv = base;
+            Pc = base + B * p->Gv * H;
+            Gsv = base + B * G * H;
+            Gsc = base + B * G * H + B * p->Gv * H;
+        } else if (ovl) {
             // side stream: layer l's set was filled one iteration earlier (or here, for the last
             // layer); layer l - 1's goes into the other set once layer l + 1 has released it
             if (l == L - 1 && (rc0 = side_project(l))) return rc0;
@@ -1731,7 +1768,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
             LDPC_HIP(hipStreamWaitEvent(s, ev_ready[l & 1], 0));
         } else if (pj) {  // forward recompute: projected rows (Mv / Mc) and the group means (Gsv / Gsc)
             if (int rc = gnn_project_groups(p, T, d_weights, l, x, d_msg_type, d_msg_var, d_llr, N, B, Mv, Mc,
-                                            Gsv, Gsc, s))
+                                            w.da, w.db, s))  // = Gsv / Gsc here
                 return rc;
         } else {  // group means of c (forward recompute)
             GmT g{};
@@ -1746,7 +1783,7 @@ extern "C" int ldpc_gnn_backward_ds(const ldpc_gnn_plan *p, int hidden, int type
         // MLP backward
         MlpT m{};
         m.x = x; m.llr = d_llr; m.w_in = d_weights; m.b_in = d_weights + H;
-        m.Mv = Mv; m.Mc = Mc; m.dX = w.dX;
+        m.Mv = Pv; m.Mc = Pc; m.dX = w.dX;
         m.msg_type = d_msg_type; m.msg_var = d_msg_var; m.vgroup = p->vgroup; m.cgroup = p->cgroup;
         m.emb = W[0]; m.w1v = W[1]; m.b1v = W[2]; m.w2v = W[3]; m.w1c = W[5]; m.b1c = W[6]; m.w2c = W[7];
         m.cbuf = pj ? nullptr : w.cbuf;  // PJ: train_dw1_kernel forms c itself

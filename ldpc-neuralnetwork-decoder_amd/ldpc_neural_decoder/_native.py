@@ -76,6 +76,11 @@ SIGNATURES = {
                                             ctypes.c_int, _I64, _P, _P, _P, _I64, _P]),
     "ldpc_gnn_backward_ds": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
                                             ctypes.c_int, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "ldpc_gnn_train_proj_floats": (_I64, [_P, ctypes.c_int, _I64, ctypes.c_int]),
+    "ldpc_gnn_forward_train_ex": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
+                                                 ctypes.c_int, _I64, _P, _P, _P, _P, _I64, _P]),
+    "ldpc_gnn_backward_ds_ex": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P,
+                                               ctypes.c_int, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
 }
 
 _lib = None

@@ -354,6 +354,12 @@ class MessageGNNDecoder(nn.Module):
         return (soft_bits > 0.5).float()
 
 
+def _saved_projections():
+    """LDPC_GNN_SAVED_PROJ=0 makes the backward recompute the projections (A/B runs, tests)."""
+    import os
+    return os.environ.get("LDPC_GNN_SAVED_PROJ", "1") != "0"
+
+
 class _NativeGnnTrain(torch.autograd.Function):
     """Autograd node of the native fp32 forward (message_gnn_decoder.py:190-307): forward saves
     each layer's features, backward is ldpc_gnn_backward (csrc/gnn_train.hip).  Replaces torch's
@@ -372,7 +378,10 @@ class _NativeGnnTrain(torch.autograd.Function):
         E = dec.num_messages
         blob = torch.cat([p.detach().reshape(-1).to(dev, torch.float32) for p in params]).contiguous()
         wsb = N.check(N.lib().ldpc_gnn_train_workspace_size(plan.handle, H, Nv, max(B, 1), L))
-        need = L * B * E * H * 4 + wsb
+        # the forward's projected group rows and group means, kept for the backward (0 where the
+        # path has none): no recompute there
+        npj = N.check(N.lib().ldpc_gnn_train_proj_floats(plan.handle, H, B, L)) if _saved_projections() else 0
+        need = L * B * E * H * 4 + npj * 4 + wsb
         free = torch.cuda.mem_get_info(dev)[0]
         free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)  # torch's cache
         if need > free:
@@ -383,23 +392,24 @@ class _NativeGnnTrain(torch.autograd.Function):
                 f"for inference, which is chunked")
         probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
         saved = torch.empty((L, B, E, H), dtype=torch.float32, device=dev)
+        proj = torch.empty(npj, dtype=torch.float32, device=dev)
         if B:
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-            N.check(N.lib().ldpc_gnn_forward_train(
+            N.check(N.lib().ldpc_gnn_forward_train_ex(
                 plan.handle, H, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr), Nv, B,
-                N.ptr(probs), N.ptr(saved), N.ptr(ws), wsb, N.stream_ptr(dev)))
+                N.ptr(probs), N.ptr(saved), N.ptr(proj) if npj else None, N.ptr(ws), wsb, N.stream_ptr(dev)))
         layer_probs = torch.empty((max(L - 1, 0) if all_layers else 0, B, Nv), dtype=torch.float32, device=dev)
         if all_layers and B and L > 1:
             N.check(N.lib().ldpc_gnn_layer_probs(
                 plan.handle, H, T, L, N.ptr(blob), N.ptr(io_map), N.ptr(llr), Nv, B, N.ptr(saved),
                 N.ptr(layer_probs), N.ptr(ws), wsb, N.stream_ptr(dev)))
-        ctx.save_for_backward(llr, io_map, types, blob, probs, saved, layer_probs)
+        ctx.save_for_backward(llr, io_map, types, blob, probs, saved, layer_probs, proj)
         ctx.meta = (plan, H, T, L, [p.shape for p in params])
         return probs, layer_probs
 
     @staticmethod
     def backward(ctx, grad_probs, grad_layer_probs):
-        llr, io_map, types, blob, probs, saved, layer_probs = ctx.saved_tensors
+        llr, io_map, types, blob, probs, saved, layer_probs, proj = ctx.saved_tensors
         plan, H, T, L, shapes = ctx.meta
         dev = llr.device
         B, Nv = llr.shape
@@ -411,9 +421,10 @@ class _NativeGnnTrain(torch.autograd.Function):
         gl = None
         if grad_layer_probs is not None and layer_probs.numel():
             gl = grad_layer_probs.to(dev, torch.float32).contiguous()
-        N.check(N.lib().ldpc_gnn_backward_ds(
+        N.check(N.lib().ldpc_gnn_backward_ds_ex(
             plan.handle, H, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr), Nv, B,
-            N.ptr(probs), N.ptr(g), N.ptr(saved), N.ptr(layer_probs) if gl is not None else None,
+            N.ptr(probs), N.ptr(g), N.ptr(saved), N.ptr(proj) if proj.numel() else None,
+            N.ptr(layer_probs) if gl is not None else None,
             N.ptr(gl) if gl is not None else None, N.ptr(grad), N.ptr(ws), wsb, N.stream_ptr(dev)))
         grads, off = [], 0
         for s in shapes:

@@ -176,3 +176,8 @@ def test_fp32_group_mean_variants_bit_identical(cuda, tmp_path):
     d = (p - child("nod1.pt", LDPC_GNN_D1="0")).abs().max().item()
     print(f"projected path, degree-1 tiles vs none: max |dp| {d:.2e}")
     assert d <= 1e-5
+    # round 5: the row walk (check-group sums from the producing MLP, the default) against the tile
+    # walk with gathered check means (LDPC_GNN_ROWWALK=0): summation order apart, |dp| <= 1e-5
+    d = (p - child("norw.pt", LDPC_GNN_ROWWALK="0")).abs().max().item()
+    print(f"row walk vs tile walk: max |dp| {d:.2e}")
+    assert d <= 1e-5
