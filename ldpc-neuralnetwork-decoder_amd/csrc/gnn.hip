@@ -62,13 +62,6 @@ constexpr int kMaxGenericH = 1024;
 #ifndef LDPC_PROJ_NT
 #define LDPC_PROJ_NT 768
 #endif
-int mlp_threads() {
-    static int t = [] {
-        const char *e = std::getenv("LDPC_GNN_MLP_THREADS");
-        return (e && std::atoi(e) == 256) ? 256 : 512;
-    }();
-    return t;
-}
 // LDPC_GNN_D1=0 keeps the Mv rows of degree-1 var groups (A/B runs)
 bool d1_skip() {
     static bool t = [] {
@@ -1465,16 +1458,6 @@ bool proj_path() {
     return t;
 }
 
-// LDPC_GNN_PROJ_WGS=n caps the projection kernel's workgroups per CU (speed only; 0 = as many as
-// the LDS allows, at most 3): fewer waves in flight keep fewer frames' feature rows competing for an
-// XCD's L2 between a row's check-side and var-side reads
-int proj_wgs_cap() {
-    static int t = [] {
-        const char *e = std::getenv("LDPC_GNN_PROJ_WGS");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    return t;
-}
 
 // LDPC_GNN_STREAMS=1 runs the fp32 forward as one frame range on the caller's stream (A/B runs);
 // default 2: two frame halves on two streams, so one half's HBM-bound group-mean launch runs in
@@ -1898,9 +1881,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     if (!mfma && H > kMaxGenericH) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be <= " + std::to_string(kMaxGenericH));
     const size_t mfma_lds = (size_t)(kOffEmb + types * kEmbStride) * 4;
     if (mfma && mfma_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
-    const int mt = mlp_threads();
-    const void *mfma_fn = mt == 512 ? reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<512>)
-                                    : reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<256>);
+    const int mt = 512;  // MLP workgroups of 8 waves (the default of every measured round)
+    const void *mfma_fn = reinterpret_cast<const void *>(gnn_mlp_mfma_kernel<512>);
     if (mfma) LDPC_HIP(hipFuncSetAttribute(mfma_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mfma_lds));
     // projected-group path (H = 64, group plans; LDPC_GNN_PROJ=0 selects the per-message [c; g]
     // kernels for A/B runs)
@@ -1923,7 +1905,6 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         if (mlp2_lds > 160 * 1024 || proj_lds > 160 * 1024)
             return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
         proj_per_cu = std::max<int>(1, std::min<int>(3, (int)((160 * 1024) / proj_lds)));
-        if (proj_wgs_cap()) proj_per_cu = std::min(proj_per_cu, proj_wgs_cap());
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
@@ -2056,10 +2037,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             const int64_t tiles = (nb * p->E + 31) / 32;
             const int64_t want = (tiles + mt / 64 - 1) / (mt / 64);
             const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus);
-            if (mt == 512)
-                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<512>, dim3(grid), dim3(512), mfma_lds, st, L);
-            else
-                hipLaunchKernelGGL(gnn_mlp_mfma_kernel<256>, dim3(grid), dim3(256), mfma_lds, st, L);
+            hipLaunchKernelGGL(gnn_mlp_mfma_kernel<512>, dim3(grid), dim3(512), mfma_lds, st, L);
             LDPC_CHECK_LAUNCH("gnn_mlp_mfma_kernel");
         } else {
             if (w.wt) {  // tiled: kTiledNM messages per wave over the layer's transposed weights

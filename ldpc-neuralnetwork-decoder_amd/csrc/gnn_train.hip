@@ -1287,13 +1287,9 @@ __global__ __launch_bounds__(256, 2) void train_dw2_kernel(Dw2T P) {
     }
 }
 
-// workgroups per CU of the weight-gradient reductions (LDPC_GNN_OUTER_WGS, default 2: 40.1 vs 41.0
-// ms per step at 4 and 43.6 at 8, profiles/r04); read per call
-int outer_wgs() {
-    const char *e = std::getenv("LDPC_GNN_OUTER_WGS");
-    const int v = e ? std::atoi(e) : 2;
-    return v >= 1 && v <= 16 ? v : 2;
-}
+// workgroups per CU of the weight-gradient reductions: 2 (40.1 vs 41.0 ms per step at 4 and 43.6
+// at 8, profiles/r04)
+constexpr int kOuterWgs = 2;
 
 int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
     if (o.H > 64 || o.J > 128) {  // tiles of 64 gradient rows x 128 Z columns, one launch each
@@ -1675,7 +1671,7 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     }
     auto blocks = [](int64_t work, int per) { return dim3((unsigned)((work + per - 1) / per)); };
-    const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * outer_wgs());
+    const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * kOuterWgs);
 
     // head: dz, dX_L, dwo, dbo
     const float *WL[11];

@@ -157,9 +157,7 @@ int build(ldpc_graph *g) {
     g->nslots = nslots;
 
     // schedules (cost in VALU-ish units per lane vector), LPT over W waves
-    int W = 4;
-    if (const char *env = std::getenv("LDPC_FLOOD_WAVES")) W = std::atoi(env);
-    W = std::max(1, std::min(kMaxWaves, W));
+    const int W = std::min(kMaxWaves, 4);
     std::vector<std::vector<int>> row_blocks(Mb), col_blocks(Nb);
     for (size_t i = 0; i < blocks.size(); ++i) {
         row_blocks[blocks[i].r].push_back((int)i);  // c ascending (row-major order)

@@ -563,10 +563,6 @@ extern "C" int ldpc_check_groups_minsum(const float *d_in, int64_t B, int n, con
     if (B < 0 || n <= 0 || G < 0 || K <= 0) return fail(LDPC_EINVAL, "bad check-group dimensions");
     if (!B || !G) return LDPC_OK;
     if (!d_in || !d_gptr || !d_gmem || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
-    static const int fpw_env = [] {  // LDPC_CHECK_FPW=1|2|4|8: frames per workgroup (speed only)
-        const char *e = std::getenv("LDPC_CHECK_FPW");
-        return e ? std::atoi(e) : 0;
-    }();
     // one frame per workgroup by default: 4 workgroups per CU overlap staging with compute
     // (+1.8 % on lay-z32 over 2 frames; 4 frames, one workgroup per CU, -19 %)
     static const int idx_f = [] {  // LDPC_CHECK_IDX_F=0: the per-frame kernel (A/B); 1 / 2 / 4 frames per workgroup
@@ -586,27 +582,14 @@ extern "C" int ldpc_check_groups_minsum(const float *d_in, int64_t B, int n, con
             return LDPC_OK;
         }
     }
-    int fpw = gather_fpw(n) ? 1 : 0;
-    if (fpw && (fpw_env == 1 || fpw_env == 2 || fpw_env == 4 || fpw_env == 8) &&
-        (size_t)fpw_env * n * 4 <= 160 * 1024)
-        fpw = fpw_env;
-    if (!fpw) return fail(LDPC_EUNSUPPORTED, "check-group rows do not fit LDS");
-    const dim3 grid((unsigned)((B + fpw - 1) / fpw));
-    const size_t lds = (size_t)fpw * n * 4;
+    // one frame per workgroup (2, 4 and 8 frames per workgroup measured slower, profiles/r04)
+    if (!gather_fpw(n)) return fail(LDPC_EUNSUPPORTED, "check-group rows do not fit LDS");
+    const size_t lds = (size_t)n * 4;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (lds > 64 * 1024) {
-        const void *fn = fpw == 8   ? reinterpret_cast<const void *>(check_group_kernel<8>)
-                         : fpw == 4 ? reinterpret_cast<const void *>(check_group_kernel<4>)
-                         : fpw == 2 ? reinterpret_cast<const void *>(check_group_kernel<2>)
-                                    : reinterpret_cast<const void *>(check_group_kernel<1>);
-        LDPC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    }
-    switch (fpw) {
-        case 8: hipLaunchKernelGGL(check_group_kernel<8>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
-        case 4: hipLaunchKernelGGL(check_group_kernel<4>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
-        case 2: hipLaunchKernelGGL(check_group_kernel<2>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
-        default: hipLaunchKernelGGL(check_group_kernel<1>, grid, dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out); break;
-    }
+    if (lds > 64 * 1024)
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(check_group_kernel<1>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(check_group_kernel<1>, dim3((unsigned)B), dim3(512), lds, s, d_in, B, n, d_gptr, d_gmem, G, K, d_out);
     LDPC_CHECK_LAUNCH("check_group_kernel");
     return LDPC_OK;
 }
