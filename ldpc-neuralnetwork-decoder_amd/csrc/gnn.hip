@@ -121,7 +121,6 @@ struct GnnLayer {
     // each check's sum of its output rows to S_out (B, Gc, 64) for the next layer, whose projection
     // forms the check-side means as S_in * inv_c + memb (this layer's mean type embedding per check)
     const int4 *rw_meta = nullptr;
-    const int32_t *rw_cg = nullptr;
     int rw_n = 0;
     float *S_out = nullptr;
     const float *S_in = nullptr, *memb = nullptr;
@@ -853,7 +852,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_d1 + o * kS6Row + p, kS6Img);
         }
     if (tid < 64) {
-        lds[kS6OffB + tid] = P.vside ? P.b2v[tid] : 0.0f;
+        lds[kS6OffB + tid] = (P.vside ? P.b2v[tid] : 0.0f) + P.b2c[tid];  // both output biases
         lds[kS6OffB + 64 + tid] = P.b2c[tid];
         lds[kS6OffB + 128 + tid] = P.last ? P.wo[tid] : 0.0f;
     }
@@ -862,17 +861,14 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     for (int i = tid; i < P.T * 64; i += NT) lds[kS6OffEmb + (i >> 6) * kPS + (i & 63)] = P.emb[i];
     __syncthreads();
 
-    const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = tid >> 6;
+    const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the walk's indices in SGPRs
     const float bo = P.last ? P.bo[0] : 0.0f;
     const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
     float S[32];  // row walk: this lane's check's running sum of output rows (its half's 32 units)
 
-    // One 32-message tile: slot j is message m of frame b (row rr of x); ok = a real message (a padding
-    // slot computes on a valid row and writes nothing); d1t = a degree-1 var tile; pc = the slot's
-    // projected check row (+ 4 half).
-    auto tile = [&](int64_t b, int64_t m, int64_t rr, bool ok, bool d1t, const float *pc) {
-        // x[s][i] = feature pi16(16 s + 8 h + i) before the type embedding (float4 pairs)
-        float x[4][8];
+    // A tile's features before the type embedding: x[s][i] = feature pi16(16 s + 8 h + i) of row rr
+    // (float4 pairs), or layer 0's input embedding of the message's LLR.
+    auto load_x = [&](float (&x)[4][8], int64_t b, int64_t m, int64_t rr) {
         if (P.x_in) {
             const float *xr = P.x_in + rr * 64 + 4 * half;
             const float hv = HYB && P.hv2c ? P.hv2c[rr] : 0.0f;
@@ -898,24 +894,39 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                     x[s][i] = l * P.w_in[u] + P.b_in[u];
                 }
         }
-        const float *e = lds + kS6OffEmb + P.msg_type[m] * kPS;
-        // a degree-1 tile's var side starts from b1v (its group half is in the combined W1v image)
-        const float *pv = d1t ? P.b1v + 4 * half : P.Mv + (b * P.Gv + P.vgroup[m]) * 64 + 4 * half;
+    };
+    // a projected group row, as the lane's accumulator registers: r[t][4 q + i] = unit 32 t + 8 q + 4 h + i
+    auto load_acc = [](f32x16 (&r)[2], const float *p) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 a = *reinterpret_cast<const float4 *>(p + 8 * q);
+            const float4 c = *reinterpret_cast<const float4 *>(p + 32 + 8 * q);
+            r[0][4 * q] = a.x; r[0][4 * q + 1] = a.y; r[0][4 * q + 2] = a.z; r[0][4 * q + 3] = a.w;
+            r[1][4 * q] = c.x; r[1][4 * q + 1] = c.y; r[1][4 * q + 2] = c.z; r[1][4 * q + 3] = c.w;
+        }
+    };
+
+    // One 32-message tile: slot j is message m of frame b (row rr of x); ok = a real message (a padding
+    // slot computes on a valid row and writes nothing); d1t = a degree-1 var tile; pc = the slot's
+    // projected check row (+ 4 half); x = the tile's features (load_x), typ = its message type, pv = its
+    // var side's starting accumulators (the projected group row W1v_right g + b1v, or b1v on a degree-1
+    // tile).  Row walk (RW): the tile also loads the NEXT tile's x (row xn, once GEMM1 has read
+    // this tile's) and var-side row (frame bn, var group vgn, degree-1 d1n; once GEMM2 has consumed
+    // this tile's var side) into x and pv, so their latency hides under this tile's MFMAs.
+    auto tile = [&](int64_t b, int64_t m, int64_t rr, bool ok, const float *pc, float (&x)[4][8], int typ,
+                    f32x16 (&pv)[2], bool d1t, const float *xn, int64_t bn, int vgn, bool d1n) {
+        const float *e = lds + kS6OffEmb + typ * kPS;
+        // the per-walk constants are re-read from LDS at every tile (an opaque offset: hoisted out of the
+        // walk they would hold 64 VGPRs)
+        int boff = kS6OffB;
+        asm volatile("" : "+s"(boff));
+        const float *b2 = lds + boff, *wo = lds + boff + 128;
         // GEMM1 of both sides per k-step over one split of c (c = x + emb[type] is the same for
         // both), each side's accumulators from its projected group row W1_right g + b1
         f32x16 hs[2][2];
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            if (side == 0 && !P.vside) continue;
-            const float *pr = side == 0 ? pv : pc;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 a = *reinterpret_cast<const float4 *>(pr + 8 * q);
-                const float4 c = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q);
-                hs[side][0][4 * q] = a.x; hs[side][0][4 * q + 1] = a.y; hs[side][0][4 * q + 2] = a.z; hs[side][0][4 * q + 3] = a.w;
-                hs[side][1][4 * q] = c.x; hs[side][1][4 * q + 1] = c.y; hs[side][1][4 * q + 2] = c.z; hs[side][1][4 * q + 3] = c.w;
-            }
-        }
+        hs[0][0] = pv[0];
+        hs[0][1] = pv[1];
+        load_acc(hs[1], pc);
         const __bf16 *W1v = (d1t ? img_d1 : img) + abase, *W1c = img + 3 * kS6Img + abase;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -932,7 +943,27 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             hs[1][1] = mfma6(W1c + 32 * kS6Row + 16 * s, c0, c1, c2, hs[1][1], kS6Img);
             __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
         }
-        f32x16 y0 = {}, y1 = {};
+        // GEMM2's accumulators start from the residual and the output biases: register 4 q + i of
+        // tile ot is unit 32 ot + 8 q + 4 half + i = x[2 ot + (q >> 1)][4 (q & 1) + i]
+        f32x16 y0, y1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int o = 8 * q + 4 * half + i;
+                y0[4 * q + i] = (P.residual ? x[q >> 1][4 * (q & 1) + i] : 0.0f) + b2[o];
+                y1[4 * q + i] = (P.residual ? x[2 + (q >> 1)][4 * (q & 1) + i] : 0.0f) + b2[32 + o];
+            }
+        if constexpr (RW) {  // x is consumed: the next tile's (layer 0 computes its x at the tile)
+            if (P.x_in)
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const float4 v = *reinterpret_cast<const float4 *>(xn + 32 * (s >> 1) + 16 * (s & 1) + 8 * q);
+                        x[s][4 * q] = v.x; x[s][4 * q + 1] = v.y; x[s][4 * q + 2] = v.z; x[s][4 * q + 3] = v.w;
+                    }
+        }
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             if (side == 0 && !P.vside) continue;
@@ -949,31 +980,21 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 y1 = mfma6(W2 + 32 * kS6Row + 16 * s, r0, r1, r2, y1, kS6Img);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            if constexpr (RW) {  // the var side is consumed: the next tile's var-side row
+                if (side == 0) load_acc(pv, (d1n || !P.vside ? P.b1v : P.Mv + (bn * P.Gv + vgn) * 64) + 4 * half);
+            }
         }
-        const float *b2v = lds + kS6OffB, *b2c = lds + kS6OffB + 64, *wo = lds + kS6OffB + 128;
         float part = 0.0f;
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int o0 = 32 * ot + 8 * q + 4 * half;
-                float4 v;
-                float *vv = reinterpret_cast<float *>(&v);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float acc = ot == 0 ? y0[4 * q + i] : y1[4 * q + i];
-                    vv[i] = (acc + b2v[o0 + i]) + b2c[o0 + i];
-                }
-                // residual: register 4 q + i of tile ot is x[2 ot + (q >> 1)][4 (q & 1) + i]
-                if (P.residual) {
-                    v.x += x[2 * ot + (q >> 1)][4 * (q & 1)];
-                    v.y += x[2 * ot + (q >> 1)][4 * (q & 1) + 1];
-                    v.z += x[2 * ot + (q >> 1)][4 * (q & 1) + 2];
-                    v.w += x[2 * ot + (q >> 1)][4 * (q & 1) + 3];
-                }
+                const f32x16 &y = ot == 0 ? y0 : y1;
+                const float4 v = make_float4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]);
                 if (P.last) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) part += vv[i] * wo[o0 + i];
+                    part += v.x * wo[o0]; part += v.y * wo[o0 + 1];
+                    part += v.z * wo[o0 + 2]; part += v.w * wo[o0 + 3];
                 }
                 if (ok && P.x_out) *reinterpret_cast<float4 *>(P.x_out + rr * 64 + o0) = v;
                 if constexpr (RW) {  // the check's sum of next-layer features (row walk)
@@ -987,6 +1008,10 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             if (ok && half == 0) P.msg_out[b * P.E + m] = part + bo;
         }
     };
+    // a tile's var-side starting row: b1v on a degree-1 tile, else its projected group row
+    auto pv_row = [&](int64_t b, int64_t m, bool d1t) -> const float * {
+        return (d1t || !P.vside ? P.b1v : P.Mv + (b * P.Gv + P.vgroup[m]) * 64) + 4 * half;
+    };
     if constexpr (RW) {
         // Row walk (plan rw_*): a unit is one frame's check tile group -- up to 32 consecutive checks of
         // one degree d whose messages are contiguous runs (the reference's check-major order,
@@ -994,30 +1019,78 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         // (lane j = check j).  Every tile of the unit reads the same 32 projected check rows, and the
         // lane sums its check's output rows in registers: the next layer's check-group sums leave the
         // kernel as one row per check (S_out) instead of being gathered from the feature rows again.
+        // Units per launch < 2^31 (B * rw_n <= B * E, bounded by the caller's chunking).
         const int64_t nunits = P.B * P.rw_n;
         const TileWalk tw = xcd_tiles(nunits, NT / 64, wave);
-        for (int64_t u = tw.first; u < tw.end; u += tw.stride) {
-            const int64_t b = u / P.rw_n;
-            const int c = (int)(u - b * P.rw_n);
-            const int4 md = P.rw_meta[c];  // {first message, checks, degree, degree-1 tile mask}
-            const bool okc = j < md.y;
-            const int cg = P.rw_cg[32 * c + (okc ? j : 0)];
-            const float *pc = P.Mc + (b * P.Gc + cg) * 64 + 4 * half;
-            const int64_t mj = md.x + (int64_t)(okc ? j : 0) * md.z;
+        if (tw.first >= tw.end) return;
+        const uint32_t rwn = (uint32_t)P.rw_n;
+        // unit meta through the scalar cache (uniform addresses; a vector load here would make the
+        // walk wait on the vector counter, i.e. on the prefetches issued before it)
+        typedef const __attribute__((address_space(4))) int *MetaP;
+        const MetaP mp = (MetaP)P.rw_meta;
+        auto meta = [&](int k) { return make_int4(mp[4 * k], mp[4 * k + 1], mp[4 * k + 2], mp[4 * k + 3]); };
+        // the walk's position: unit u = frame b, meta md = {first message, checks, degree, degree-1
+        // tile mask}, first check group cg0 (lane j: check group cg0 + j), tile i; the lane's message m
+        // (okc: the lane holds a real check; a padding lane repeats lane 0's message, writes nothing)
+        int64_t u = tw.first;
+        int64_t b = (uint32_t)u / rwn;
+        int cu = (int)(u - b * rwn), i = 0;
+        int4 md = meta(2 * cu);
+        int cg0 = mp[8 * cu + 4];
+        bool okc = j < md.y;
+        int m = md.x + (okc ? j : 0) * md.z;
+        bool d1 = P.ntile_v1 && (md.w & 1);
+        float x[4][8];
+        f32x16 pv[2];
+        int typ = P.msg_type[m];
+        if (P.x_in) load_x(x, b, m, b * P.E + m);
+        if (P.vside) load_acc(pv, pv_row(b, m, d1));
 #pragma unroll
-            for (int i = 0; i < 32; ++i) S[i] = 0.0f;
-            for (int i = 0; i < md.z; ++i) tile(b, mj + i, b * P.E + mj + i, okc, P.ntile_v1 && ((md.w >> i) & 1), pc);
-            if (okc && P.S_out) {
-                float *dst = P.S_out + (b * P.Gc + cg) * 64;
-#pragma unroll
-                for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 v = make_float4(S[16 * ot + 4 * q], S[16 * ot + 4 * q + 1], S[16 * ot + 4 * q + 2],
-                                                     S[16 * ot + 4 * q + 3]);
-                        *reinterpret_cast<float4 *>(dst + 32 * ot + 8 * q + 4 * half) = v;
-                    }
+        for (int k = 0; k < 32; ++k) S[k] = 0.0f;
+        for (;;) {
+            // the next tile: (u, i + 1), else the first tile of the wave's next unit; past the wave's
+            // last tile the current one again (loads of valid rows, discarded)
+            const bool inunit = i + 1 < md.z;
+            bool more = true;
+            int64_t uq = u, bq = b;
+            int iq = i + 1, mq = m + 1, cg0q = cg0;
+            int4 mdq = md;
+            bool okq = okc;
+            if (!inunit) {  // uniform
+                const int64_t un = u + tw.stride;
+                more = un < tw.end;
+                uq = more ? un : u;
+                bq = (uint32_t)uq / rwn;
+                const int cq = (int)(uq - bq * rwn);
+                mdq = meta(2 * cq);
+                cg0q = mp[8 * cq + 4];
+                okq = j < mdq.y;
+                iq = more ? 0 : i;
+                mq = mdq.x + (okq ? j : 0) * mdq.z + iq;
             }
+            const bool d1q = P.ntile_v1 && ((mdq.w >> iq) & 1);
+            const int typq = P.msg_type[mq], vgq = P.vgroup[mq];
+            const int cg = cg0 + (okc ? j : 0);
+            if (!P.x_in) load_x(x, b, m, b * P.E + m);  // layer 0: x from the LLR at the tile
+            tile(b, m, b * P.E + m, okc, P.Mc + (b * P.Gc + cg) * 64 + 4 * half, x, typ, pv, d1,
+                 P.x_in + (bq * P.E + mq) * 64 + 4 * half, bq, vgq, d1q);
+            if (!inunit) {  // the unit's last tile: its checks' sums
+                if (okc && P.S_out) {
+                    float *dst = P.S_out + (b * P.Gc + cg) * 64;
+#pragma unroll
+                    for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float4 v = make_float4(S[16 * ot + 4 * q], S[16 * ot + 4 * q + 1],
+                                                         S[16 * ot + 4 * q + 2], S[16 * ot + 4 * q + 3]);
+                            *reinterpret_cast<float4 *>(dst + 32 * ot + 8 * q + 4 * half) = v;
+                        }
+                }
+#pragma unroll
+                for (int k = 0; k < 32; ++k) S[k] = 0.0f;
+            }
+            if (!more) break;
+            u = uq; i = iq; b = bq; md = mdq; cg0 = cg0q; okc = okq; m = mq; d1 = d1q; typ = typq;
         }
         return;
     }
@@ -1055,7 +1128,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             pm += rsm;
             if (pm >= P.E) { pm -= P.E; ++pb; }
         }
-        tile(b, m, rr, ok, d1t, P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half);
+        float x[4][8];
+        f32x16 pv[2];
+        load_x(x, b, m, rr);
+        if (P.vside) load_acc(pv, pv_row(b, m, d1t));
+        tile(b, m, rr, ok, P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half, x, P.msg_type[m], pv, d1t, nullptr, 0, 0, false);
     }
 }
 
@@ -1601,7 +1678,7 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     ct_m0.push_back((int32_t)E);
     // fp32 row walk: check tile groups (gnn.hpp rw_*), used when they fill >= 90 % of their tiles
     std::vector<int32_t> rw_meta, rw_cg;
-    bool rw_d1 = true;
+    bool rw_d1 = true, rw_contig = true;  // rw_contig: lane k of a unit holds check group first + k
     if (aligned) {
         auto vdeg1 = [&](int64_t m) { return vptr[h_vgroup[m] + 1] - vptr[h_vgroup[m]] == 1; };
         int64_t m = 0, slots = 0, d1_msgs = 0, d1_in_tiles = 0;
@@ -1625,13 +1702,15 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
                     d1_in_tiles += n;
                 }
             }
-            rw_meta.insert(rw_meta.end(), {(int32_t)m0, n, d, mask});
+            for (int k = 1; k < n; ++k) rw_contig = rw_contig && rw_cg[rw_cg.size() - 32 + k] == rw_cg[rw_cg.size() - 32] + k;
+            rw_meta.insert(rw_meta.end(), {(int32_t)m0, n, d, mask, rw_cg[rw_cg.size() - 32], 0, 0, 0});
             slots += 32LL * d;
         }
         rw_d1 = d1_in_tiles == d1_msgs;
         if (!rw_d1)
-            for (size_t c = 0; c < rw_meta.size(); c += 4) rw_meta[c + 3] = 0;
-        if ((double)E < 0.9 * (double)slots) rw_meta.clear(), rw_cg.clear();
+            for (size_t c = 0; c < rw_meta.size(); c += 8) rw_meta[c + 3] = 0;
+        if ((double)E < 0.9 * (double)slots || !rw_contig) rw_meta.clear();
+        rw_cg.clear();
     }
     // fp32 path: projection tiles of 32 groups of one side (gnn.hpp), each side sorted by degree
     std::vector<int32_t> pt;  // meta [4 n] | grp [32 n] | deg [32 n] | mem
@@ -1701,7 +1780,7 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
     hipError_t e4 = hipMalloc(&p->d_gt, gt_words * 4);
     hipError_t e5 = hipMalloc(&p->d_pt, pt.size() * 4);
     hipError_t e6 = hipMalloc(&p->d_ct, ct_m0.size() * 4);
-    hipError_t e7 = rw_meta.empty() ? hipSuccess : hipMalloc(&p->d_rw, (rw_meta.size() + rw_cg.size()) * 4);
+    hipError_t e7 = rw_meta.empty() ? hipSuccess : hipMalloc(&p->d_rw, rw_meta.size() * 4);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess ||
         e6 != hipSuccess || e7 != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
@@ -1715,16 +1794,13 @@ extern "C" int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_v
                   hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_pt, pt.data(), pt.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_ct, ct_m0.data(), ct_m0.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        (p->d_rw && (hipMemcpy(p->d_rw, rw_meta.data(), rw_meta.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-                     hipMemcpy(p->d_rw + rw_meta.size(), rw_cg.data(), rw_cg.size() * 4, hipMemcpyHostToDevice) !=
-                         hipSuccess))) {
+        (p->d_rw && hipMemcpy(p->d_rw, rw_meta.data(), rw_meta.size() * 4, hipMemcpyHostToDevice) != hipSuccess)) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan upload failed");
     }
-    p->n_rw = (int)(rw_meta.size() / 4);
+    p->n_rw = (int)(rw_meta.size() / 8);
     p->rw_d1 = p->n_rw > 0 && rw_d1;
     p->rw_meta = reinterpret_cast<const int4 *>(p->d_rw);
-    p->rw_cg = p->d_rw ? p->d_rw + rw_meta.size() : nullptr;
     p->n_ptiles = (int)(pt_meta.size() / 4);
     p->n_ptiles_v = n_ptiles_v;
     p->n_ptiles_v1 = n_ptiles_v1;
@@ -1972,7 +2048,6 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             L.d1 = 0;
             if (rw) {
                 L.rw_meta = p->rw_meta;
-                L.rw_cg = p->rw_cg;
                 L.rw_n = p->n_rw;
                 L.ntile_v1 = rwd1;
                 L.S_in = l > 0 ? w.S + b0 * p->Gc * H : nullptr;

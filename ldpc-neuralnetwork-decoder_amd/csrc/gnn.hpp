@@ -53,16 +53,16 @@ struct ldpc_gnn_plan {
     int32_t *d_ct = nullptr;
     const int32_t *ct_m0 = nullptr;  // [n_ctiles + 1]
     // fp32 row walk (gnn.hip gnn_mlp2s_kernel RW): check tile groups -- up to 32 consecutive check
-    // groups of one degree d, each a contiguous message run -- rw_meta[c] = {first message, checks,
+    // groups of one degree d, each a contiguous message run -- rw_meta[2 c] = {first message, checks,
     // d, degree-1 tile mask (bit i: message i of every check belongs to a degree-1 var group)},
-    // rw_cg[32 c + k] = check group of lane k (-1 = padding).  n_rw = 0: no such walk (the checks are
-    // not contiguous runs, or the groups fill their tiles too sparsely).  rw_d1: the masks are in use
+    // rw_meta[2 c + 1].x = the first check group (lane k holds group first + k).  n_rw = 0: no such walk
+    // (the checks are not contiguous runs of consecutive groups, or the groups fill their tiles too
+    // sparsely).  rw_d1: the masks are in use
     // (every degree-1 var group's message lies in a masked tile, so its projected row is never read).
     int n_rw = 0;
     bool rw_d1 = false;
     int32_t *d_rw = nullptr;
     const int4 *rw_meta = nullptr;
-    const int32_t *rw_cg = nullptr;
 };
 
 namespace ldpc {
