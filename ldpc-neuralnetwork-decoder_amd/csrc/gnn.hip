@@ -863,7 +863,9 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the walk's indices in SGPRs
     const float bo = P.last ? P.bo[0] : 0.0f;
-    const int abase = j * kS6Row + 8 * half;  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
+    const int abase = j * kS6Row + 8 * half;
+  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
+    const bool vs = HYB ? P.vside != 0 : true;  // the var side (only the hybrid kernel runs without it)
     float S[32];  // row walk: this lane's check's running sum of output rows (its half's 32 units)
 
     // A tile's features before the type embedding: x[s][i] = feature pi16(16 s + 8 h + i) of row rr
@@ -922,11 +924,15 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         asm volatile("" : "+s"(boff));
         const float *b2 = lds + boff, *wo = lds + boff + 128;
         // GEMM1 of both sides per k-step over one split of c (c = x + emb[type] is the same for
-        // both), each side's accumulators from its projected group row W1_right g + b1
+        // both); the var side's accumulators start from its projected group row W1_right g + b1
         f32x16 hs[2][2];
         hs[0][0] = pv[0];
         hs[0][1] = pv[1];
-        load_acc(hs[1], pc);
+        // the check side's projected row is added after GEMM1 (its load lands under the MFMAs)
+        f32x16 pcr[2];
+        load_acc(pcr, pc);
+        hs[1][0] = f32x16{};
+        hs[1][1] = f32x16{};
         const __bf16 *W1v = (d1t ? img_d1 : img) + abase, *W1c = img + 3 * kS6Img + abase;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -935,7 +941,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             for (int i = 0; i < 8; ++i) c[i] = x[s][i] + e[pi16(16 * s + 8 * half + i)];
             bf16x8_t c0, c1, c2;
             split3(c, c0, c1, c2);
-            if (P.vside) {
+            if (vs) {
                 hs[0][0] = mfma6(W1v + 16 * s, c0, c1, c2, hs[0][0], kS6Img);
                 hs[0][1] = mfma6(W1v + 32 * kS6Row + 16 * s, c0, c1, c2, hs[0][1], kS6Img);
             }
@@ -943,6 +949,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             hs[1][1] = mfma6(W1c + 32 * kS6Row + 16 * s, c0, c1, c2, hs[1][1], kS6Img);
             __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
         }
+        hs[1][0] += pcr[0];
+        hs[1][1] += pcr[1];
         // GEMM2's accumulators start from the residual and the output biases: register 4 q + i of
         // tile ot is unit 32 ot + 8 q + 4 half + i = x[2 ot + (q >> 1)][4 (q & 1) + i]
         f32x16 y0, y1;
@@ -966,7 +974,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         }
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-            if (side == 0 && !P.vside) continue;
+            if (side == 0 && !vs) continue;
             const f32x16 &h0 = hs[side][0], &h1 = hs[side][1];
             const __bf16 *W2 = img + kS6OffW2 + 3 * side * kS6Img + abase;
 #pragma unroll
@@ -981,7 +989,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (RW) {  // the var side is consumed: the next tile's var-side row
-                if (side == 0) load_acc(pv, (d1n || !P.vside ? P.b1v : P.Mv + (bn * P.Gv + vgn) * 64) + 4 * half);
+                if (side == 0) load_acc(pv, (d1n ? P.b1v : P.Mv + (bn * P.Gv + vgn) * 64) + 4 * half);
             }
         }
         float part = 0.0f;
@@ -1010,7 +1018,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     };
     // a tile's var-side starting row: b1v on a degree-1 tile, else its projected group row
     auto pv_row = [&](int64_t b, int64_t m, bool d1t) -> const float * {
-        return (d1t || !P.vside ? P.b1v : P.Mv + (b * P.Gv + P.vgroup[m]) * 64) + 4 * half;
+        return (d1t || !vs ? P.b1v : P.Mv + (b * P.Gv + P.vgroup[m]) * 64) + 4 * half;
     };
     if constexpr (RW) {
         // Row walk (plan rw_*): a unit is one frame's check tile group -- up to 32 consecutive checks of
@@ -1044,7 +1052,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         f32x16 pv[2];
         int typ = P.msg_type[m];
         if (P.x_in) load_x(x, b, m, b * P.E + m);
-        if (P.vside) load_acc(pv, pv_row(b, m, d1));
+        if (vs) load_acc(pv, pv_row(b, m, d1));
 #pragma unroll
         for (int k = 0; k < 32; ++k) S[k] = 0.0f;
         for (;;) {
@@ -1131,7 +1139,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         float x[4][8];
         f32x16 pv[2];
         load_x(x, b, m, rr);
-        if (P.vside) load_acc(pv, pv_row(b, m, d1t));
+        if (vs) load_acc(pv, pv_row(b, m, d1t));
         tile(b, m, rr, ok, P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half, x, P.msg_type[m], pv, d1t, nullptr, 0, 0, false);
     }
 }
