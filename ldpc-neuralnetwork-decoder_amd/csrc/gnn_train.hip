@@ -698,6 +698,186 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
     }
 }
 
+// ---- H = 64, projected groups, every fp32 product as bf16x6 splits on v_mfma_f32_32x32x16_bf16
+// (gnn_mlp2s_kernel's scheme: the results are fp32 GEMMs up to summation order, at 6 x 32 instead
+// of 8 x 64 MFMA cycles per K = 16).  Same outputs as train_mlp_bwd_mfma_kernel<.., true>; hidden
+// units / input features on the MFMA rows, the tile's 32 messages on the columns, per side:
+//   GEMM2'  d  = W2^T dX     A[u][o] = W2[o][u]            B: dX, natural K order
+//   GEMM1   u  = W1_left c   A[u][p] = W1[u][pi16(p)]      B: c in pi16 K order (x loaded as the
+//                             + P (the projected row)       forward loads it)
+//   GEMM3'  dz = W1_left^T dh A[k][p] = W1[pi16(p)][k]      B: dh's accumulator registers as they
+//                             (both sides into one tile)    stand (k-step t = registers 8 (t&1) ..
+//                                                           of tile t >> 1)
+// Six A images (2 sides x 3 matrices) x 3 bf16 splits in 147 KB of LDS: 64-element rows with the
+// 16-byte chunks XOR-swizzled by (row >> 1) & 7, so a ds_read_b128 of 16 rows hits 16 bank groups.
+constexpr int kB6Img = 64 * 64;  // bf16 per split image
+__device__ __forceinline__ int b6_at(int row, int k) { return row * 64 + (((k >> 3) ^ ((row >> 1) & 7)) << 3) + (k & 7); }
+inline size_t mlp_bwd_s6_lds() { return (size_t)18 * kB6Img * 2; }
+// acc += A B over k-step chunk pair (lane half h reads chunk 2 s + h of row r): A from the three
+// split images at img + off (off = b6_at(r, 16 s + 8 h)), B the three splits of the lane's operand
+__device__ __forceinline__ f32x16 mfma6o(const __bf16 *img, int off, const bf16x8_t &b0, const bf16x8_t &b1,
+                                         const bf16x8_t &b2, f32x16 acc) {
+    return mfma6(img + off, b0, b1, b2, acc, kB6Img);
+}
+
+__global__ __launch_bounds__(512, 1) void train_mlp_bwd_s6_kernel(MlpT A) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    __bf16 *img = reinterpret_cast<__bf16 *>(sm);  // image m (G2T_v, G1_v, G3_v, G2T_c, G1_c, G3_c), split q: 3 m + q
+    constexpr int H = 64;
+    for (int i = threadIdx.x; i < H * H; i += 512) {
+        const int r = i >> 6, p = i & 63, up = pi16(p);
+        const float w[6] = {A.w2v[p * H + r], A.w1v[r * 2 * H + up], A.w1v[up * 2 * H + r],
+                            A.w2c[p * H + r], A.w1c[r * 2 * H + up], A.w1c[up * 2 * H + r]};
+#pragma unroll
+        for (int q = 0; q < 6; ++q) split_store(w[q], img + 3 * q * kB6Img + b6_at(r, p), kB6Img);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 31, half = lane >> 5,
+              wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // A fragment offsets    // A fragment offsets of row j per k-step (row j + 32: + 32 * 64, the same swizzle)
+    int aoff[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) aoff[s] = b6_at(j, 16 * s + 8 * half);
+    const __bf16 *G2[2] = {img, img + 9 * kB6Img}, *G1[2] = {img + 3 * kB6Img, img + 12 * kB6Img},
+                 *G3[2] = {img + 6 * kB6Img, img + 15 * kB6Img};
+    const int64_t ntiles = (A.R + 31) / 32;
+    const TileWalk tw = xcd_tiles(ntiles, 8, wave);
+    // this tile's dX (k-step s: o = 16 s + 8 h + i) and x (feature pi16(16 s + 8 h + i)) rows; the
+    // next tile's load under this tile's GEMM3' (layer 0 forms its x from the LLR at the tile)
+    float dxr[4][8], xr[4][8];
+    auto load_rows = [&](int64_t rq) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float4 v = *reinterpret_cast<const float4 *>(A.dX + rq * H + 16 * s + 8 * half + 4 * q);
+                dxr[s][4 * q] = v.x; dxr[s][4 * q + 1] = v.y; dxr[s][4 * q + 2] = v.z; dxr[s][4 * q + 3] = v.w;
+                if (A.x) {
+                    const float4 w = *reinterpret_cast<const float4 *>(A.x + rq * H + 32 * (s >> 1) + 16 * (s & 1) + 8 * q + 4 * half);
+                    xr[s][4 * q] = w.x; xr[s][4 * q + 1] = w.y; xr[s][4 * q + 2] = w.z; xr[s][4 * q + 3] = w.w;
+                }
+            }
+    };
+    if (tw.first < tw.end) load_rows(std::min<int64_t>(tw.first * 32 + j, A.R - 1));
+    for (int64_t t = tw.first; t < tw.end; t += tw.stride) {
+        const int64_t row = t * 32 + j;
+        const bool ok = row < A.R;
+        const int64_t rr = ok ? row : A.R - 1;
+        const int64_t b = rr / A.E, m = rr - b * A.E;
+        const int64_t rn = std::min<int64_t>((t + tw.stride < tw.end ? t + tw.stride : t) * 32 + j, A.R - 1);
+        // GEMM2' of both sides over one split of dX per k-step
+        f32x16 d[2][2] = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            bf16x8_t b0, b1, b2;
+            split3(dxr[s], b0, b1, b2);
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                d[side][0] = mfma6o(G2[side], aoff[s], b0, b1, b2, d[side][0]);
+                d[side][1] = mfma6o(G2[side], aoff[s] + 32 * 64, b0, b1, b2, d[side][1]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // GEMM1 of both sides over one split of c, each from its projected row W1_right g + b1
+        f32x16 u[2][2];
+        {
+            const float *pv = A.Mv + (b * A.Gv + A.vgroup[m]) * H + 4 * half;
+            const float *pc = A.Mc + (b * A.Gc + A.cgroup[m]) * H + 4 * half;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+                    const float *pr = side ? pc : pv;
+                    const float4 a = *reinterpret_cast<const float4 *>(pr + 8 * q);
+                    const float4 c = *reinterpret_cast<const float4 *>(pr + 32 + 8 * q);
+                    u[side][0][4 * q] = a.x; u[side][0][4 * q + 1] = a.y; u[side][0][4 * q + 2] = a.z; u[side][0][4 * q + 3] = a.w;
+                    u[side][1][4 * q] = c.x; u[side][1][4 * q + 1] = c.y; u[side][1][4 * q + 2] = c.z; u[side][1][4 * q + 3] = c.w;
+                }
+            }
+        }
+        const float *e = A.emb + A.msg_type[m] * H;
+        const float l = A.x ? 0.0f : A.llr[b * A.N + A.msg_var[m]];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            // c[i] = feature pi16(16 s + 8 h + i) = 32 (s >> 1) + 16 (s & 1) + 8 (i >> 2) + 4 h + (i & 3)
+            float c[8];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int u0 = 32 * (s >> 1) + 16 * (s & 1) + 8 * q + 4 * half;
+                const float4 ev = *reinterpret_cast<const float4 *>(e + u0);
+                float4 xv;
+                if (A.x) {
+                    xv = make_float4(xr[s][4 * q], xr[s][4 * q + 1], xr[s][4 * q + 2], xr[s][4 * q + 3]);
+                } else {
+                    const float4 w = *reinterpret_cast<const float4 *>(A.w_in + u0);
+                    const float4 bi = *reinterpret_cast<const float4 *>(A.b_in + u0);
+                    xv = make_float4(w.x * l + bi.x, w.y * l + bi.y, w.z * l + bi.z, w.w * l + bi.w);
+                }
+                c[4 * q] = xv.x + ev.x; c[4 * q + 1] = xv.y + ev.y; c[4 * q + 2] = xv.z + ev.z; c[4 * q + 3] = xv.w + ev.w;
+                if (ok && A.cbuf)
+                    *reinterpret_cast<float4 *>(A.cbuf + row * H + u0) = make_float4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
+            }
+            bf16x8_t c0, c1, c2;
+            split3(c, c0, c1, c2);
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                u[side][0] = mfma6o(G1[side], aoff[s], c0, c1, c2, u[side][0]);
+                u[side][1] = mfma6o(G1[side], aoff[s] + 32 * 64, c0, c1, c2, u[side][1]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // h = relu(u), dh = d masked by u > 0; lane holds units 32 rt + 8 q + 4 half + i (register 4 q + i)
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            float *ho = (side == 0 ? A.hv : A.hc) + row * H, *dho = (side == 0 ? A.dhv : A.dhc) + row * H;
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float a = u[side][rt][r];
+                    u[side][rt][r] = fmaxf(a, 0.0f);
+                    d[side][rt][r] = a > 0.0f ? d[side][rt][r] : 0.0f;
+                }
+                if (ok)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int o0 = 32 * rt + 8 * q + 4 * half;
+                        const f32x16 &uu = u[side][rt], &dd = d[side][rt];
+                        *reinterpret_cast<float4 *>(ho + o0) = make_float4(uu[4 * q], uu[4 * q + 1], uu[4 * q + 2], uu[4 * q + 3]);
+                        *reinterpret_cast<float4 *>(dho + o0) = make_float4(dd[4 * q], dd[4 * q + 1], dd[4 * q + 2], dd[4 * q + 3]);
+                    }
+            }
+        }
+        load_rows(rn);
+        // GEMM3' of both sides into one tile pair: dz_c[k][msg]
+        f32x16 z0 = {}, z1 = {};
+#pragma unroll
+        for (int side = 0; side < 2; ++side)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                float hv[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) hv[i] = d[side][s >> 1][8 * (s & 1) + i];
+                bf16x8_t r0, r1, r2;
+                split3(hv, r0, r1, r2);
+                z0 = mfma6o(G3[side], aoff[s], r0, r1, r2, z0);
+                z1 = mfma6o(G3[side], aoff[s] + 32 * 64, r0, r1, r2, z1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        if (ok) {
+            float *co = A.dco + row * H;
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const f32x16 &cc = rt ? z1 : z0;
+                    *reinterpret_cast<float4 *>(co + 32 * rt + 8 * q + 4 * half) =
+                        make_float4(cc[4 * q], cc[4 * q + 1], cc[4 * q + 2], cc[4 * q + 3]);
+                }
+        }
+    }
+}
+
 // PJ backward: the group part of dz averaged over a group, formed per group --
 // Mda[b][g][k] = inv[g] sum_u W1v[u][64 + k] S_v[b][g][u] with S the group sums of dh (Mdb: the
 // check side with W1c).  32-row tiles of a side on v_mfma_f32_32x32x2_f32, C[row][k] =
@@ -1545,6 +1725,12 @@ int bwd_proj() {
     return e ? std::atoi(e) : 1;
 }
 
+// LDPC_GNN_TRAIN_S6=0: the projected-group backward MLP on fp32 MFMA (train_mlp_bwd_mfma_kernel)
+// instead of bf16x6 splits (train_mlp_bwd_s6_kernel); read per call (A/B runs, tests)
+int bwd_s6() {
+    const char *e = std::getenv("LDPC_GNN_TRAIN_S6");
+    return e ? std::atoi(e) : 1;
+}
 // LDPC_GNN_TRAIN_OVERLAP=1: the backward's forward recompute (group projections of layer l - 1)
 // runs on a side stream into a second buffer set while layer l's gradients run on the caller's
 // stream; 0: one set, in line.  42.3-42.5 vs 42.7-43.0 ms per B = 256 step (profiles/r03aj, three
@@ -1669,6 +1855,8 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
         LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<256, true>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_s6_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_s6_lds()));
     }
     auto blocks = [](int64_t work, int per) { return dim3((unsigned)((work + per - 1) / per)); };
     const unsigned red_grid = (unsigned)std::min<int64_t>((R + 63) / 64, (int64_t)g_cus_t * kOuterWgs);
@@ -1789,7 +1977,9 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
         if (H == 64 && bwd_mfma()) {  // LDPC_GNN_TRAIN_MFMA=0 selects the VALU kernel (A/B runs)
             const int nt = bwd_mfma() == 2 ? 256 : 512;  // =2: 256 threads, 1 wave per SIMD
             const unsigned grid = (unsigned)std::min<int64_t>((R + 32 * (nt / 64) - 1) / (32 * (nt / 64)), (int64_t)g_cus_t);
-            if (pj && nt == 256)
+            if (pj && nt == 512 && bwd_s6())
+                hipLaunchKernelGGL(train_mlp_bwd_s6_kernel, dim3(grid), dim3(512), mlp_bwd_s6_lds(), s, m);
+            else if (pj && nt == 256)
                 hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<256, true>), dim3(grid), dim3(256), mlp_bwd_mfma_lds(), s, m);
             else if (pj)
                 hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<512, true>), dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);

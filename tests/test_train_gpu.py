@@ -59,14 +59,17 @@ def _check(dec, ref_grads):
     return seen
 
 
-@pytest.mark.parametrize("proj", ["1", "0", "serial"])
+@pytest.mark.parametrize("proj", ["1", "0", "serial", "fp32mfma"])
 @pytest.mark.parametrize("z,layers,hidden,B", [(4, 3, 64, 8), (4, 2, 32, 5), (32, 2, 64, 2)])
 def test_backward_matches_autograd(cuda, oracle_mod, monkeypatch, z, layers, hidden, B, proj):
     """(proj: the H = 64 backward from projected group rows -- GEMM1 over c, the group part of dz
     once per group -- or, LDPC_GNN_TRAIN_PROJ=0, per message over [c; g]; "serial": projected rows with
-    the forward recompute in line instead of on the side stream, LDPC_GNN_TRAIN_OVERLAP=0; same bar)"""
+    the forward recompute in line instead of on the side stream, LDPC_GNN_TRAIN_OVERLAP=0;
+    "fp32mfma": projected rows, the backward MLP on fp32 MFMA instead of bf16x6 splits,
+    LDPC_GNN_TRAIN_S6=0; same bar)"""
     monkeypatch.setenv("LDPC_GNN_TRAIN_PROJ", "0" if proj == "0" else "1")
     monkeypatch.setenv("LDPC_GNN_TRAIN_OVERLAP", "0" if proj == "serial" else "1")
+    monkeypatch.setenv("LDPC_GNN_TRAIN_S6", "0" if proj == "fp32mfma" else "1")
     base, H, dec, conv, types, llr, gt = _setup(z, layers, hidden, B)
     ref_p, ref_loss, ref_g = _oracle_grads(oracle_mod, dec, conv, H, types, llr, gt)
     dec = dec.to(cuda)
