@@ -1467,9 +1467,11 @@ __global__ __launch_bounds__(256, 2) void train_dw2_kernel(Dw2T P) {
     }
 }
 
-// workgroups per CU of the weight-gradient reductions: 2 (40.1 vs 41.0 ms per step at 4 and 43.6
-// at 8, profiles/r04)
-constexpr int kOuterWgs = 2;
+// workgroups per CU of the weight-gradient reductions: 1 (4 waves per CU).  Each wave ends with a
+// 64 x 64 (x 2) block of float atomics into the gradient; fewer waves, fewer atomics: 30.5-30.7 ms
+// per step against 32.8 at 2 workgroups per CU and 32.2-32.7 at 3 (round 5, profiles/r05/ab_r05o;
+// round 4 had measured 2 best among 2, 4 and 8)
+constexpr int kOuterWgs = 1;
 
 int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
     if (o.H > 64 || o.J > 128) {  // tiles of 64 gradient rows x 128 Z columns, one launch each
@@ -2086,7 +2088,7 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
             OuterT g{};
             g.H = H; g.E = (int64_t)Gn; g.R = B * Gn; g.A = dhsum; g.zsrc = Gs; g.J = H; g.ld = 2 * H; g.col0 = H;
             g.out = gw; g.bias = nullptr;
-            const unsigned ggrid = (unsigned)std::min<int64_t>((g.R + 63) / 64, (int64_t)g_cus_t * 4);
+            const unsigned ggrid = (unsigned)std::min<int64_t>((g.R + 63) / 64, (int64_t)g_cus_t * kOuterWgs);
             if (int rc = launch_outer(g, ggrid, s)) return rc;
         }
         if (ovl) LDPC_HIP(hipEventRecord(ev_free[l & 1], s));  // this layer's set is free again
