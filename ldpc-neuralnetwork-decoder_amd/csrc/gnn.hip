@@ -124,6 +124,8 @@ struct GnnLayer {
     int rw_n = 0;
     float *S_out = nullptr;
     const float *S_in = nullptr, *memb = nullptr;
+    const float *memb_v = nullptr;  // this layer's mean type embedding per var group (Gv, 64): the var-side
+                                    // gather then sums x alone (gnn_group_proj_kernel)
 };
 
 
@@ -534,6 +536,52 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
                 *reinterpret_cast<float4 *>(gm + slot * kPS + c4) = mean;
             }
         } else {
+        if (P.x_in && P.memb_v && !md.x) {
+            // var side: the members' x rows summed alone (no type gathers), then mean = sum * inv +
+            // the group's mean type embedding; the member indices two rows ahead are loaded before
+            // this pair's rows, so the rows' wait does not also wait for them
+            const float *xb = P.x_in + (int64_t)b * P.E * 64 + c4;
+            int mi[8], mj[8];
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                mi[p] = mem[4 * p];
+                mj[p] = mem[32 + 4 * p];
+            }
+            for (int i = 0; i < md.y; i += 2) {
+                int ni[8], nj[8];
+                const int i2 = i + 2 < md.y ? i + 2 : i;  // the table holds maxdeg + 1 rows
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    ni[p] = mem[32 * i2 + 4 * p];
+                    nj[p] = mem[32 * (i2 + 1) + 4 * p];
+                }
+                float4 x[8], y[8];
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    x[p] = *reinterpret_cast<const float4 *>(xb + (int64_t)mi[p] * 64);
+                    y[p] = *reinterpret_cast<const float4 *>(xb + (int64_t)mj[p] * 64);
+                }
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    if (i < dg[p]) { acc[p].x += x[p].x; acc[p].y += x[p].y; acc[p].z += x[p].z; acc[p].w += x[p].w; }
+                    if (i + 1 < dg[p]) { acc[p].x += y[p].x; acc[p].y += y[p].y; acc[p].z += y[p].z; acc[p].w += y[p].w; }
+                    mi[p] = ni[p];
+                    mj[p] = nj[p];
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int slot = 4 * p + r4, g = T.grp[32 * t + slot];
+                float4 mean = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (g >= 0) {
+                    const float inv = P.inv_v[g];
+                    const float4 e = *reinterpret_cast<const float4 *>(P.memb_v + (int64_t)g * 64 + c4);
+                    mean = make_float4(acc[p].x * inv + e.x, acc[p].y * inv + e.y, acc[p].z * inv + e.z, acc[p].w * inv + e.w);
+                    if (P.gsave_v) *reinterpret_cast<float4 *>(P.gsave_v + ((int64_t)b * P.Gv + g) * 64 + c4) = mean;
+                }
+                *reinterpret_cast<float4 *>(gm + slot * kPS + c4) = mean;
+            }
+        } else {
         if (P.x_in) {
             const float *xb = P.x_in + (int64_t)b * P.E * 64 + c4;
             const float *eb = lds + kPOffEmb + c4;
@@ -608,6 +656,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
             if (P.gsave_v && g >= 0)
                 *reinterpret_cast<float4 *>((md.x ? P.gsave_c + ((int64_t)b * P.Gc + g) * 64
                                                   : P.gsave_v + ((int64_t)b * P.Gv + g) * 64) + c4) = mean;
+        }
         }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1363,7 +1412,8 @@ __global__ void gnn_fill_kernel(int32_t *p, int64_t n, int32_t v) {
 }
 
 // Row walk: memb[l][g][u] = (1 / |g|) sum over check group g's messages (ascending) of emb_l[type][u],
-// the mean type embedding each layer's check-side group mean adds to S * inv (gnn_group_proj_kernel)
+// the mean type embedding each layer's check-side group mean adds to S * inv (gnn_group_proj_kernel);
+// the same per var group (memb_v), added to the var side's sum of x rows * inv
 __global__ void gnn_memb_kernel(const float *__restrict__ emb0, int64_t layer_stride, const int32_t *__restrict__ msg_type,
                                 const int32_t *__restrict__ cg_ptr, const int32_t *__restrict__ cg_mem,
                                 const float *__restrict__ inv_c, int Gc, int layers, float *__restrict__ memb) {
@@ -1393,6 +1443,7 @@ struct Ws {
     float *xa, *xb, *Mv, *Mc, *msg_out, *wt;
     float *Pv, *Pc, *hbuf;  // wide path: projected group rows (B, G, H), MLP hidden rows (B, E, 2 H)
     float *S, *memb;  // row walk (H = 64, plan rw_*): per-check feature sums (B, Gc, H), mean type embeddings (L, Gc, H)
+    float *memb_v;    // ... and per var group (L, Gv, H)
     int32_t *csr;
     int64_t bytes;
 };
@@ -1419,10 +1470,11 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     const int64_t wtb = H != 64 && H <= kTiledMaxH && !wide ? al(6LL * H * H * 4 * layers) : 0;
     w.wt = wtb ? reinterpret_cast<float *>(c + xb + xb2 + mv + mc + vs + cs) : nullptr;
     const int64_t rwb = H == 64 && p->n_rw > 0 && layers > 1 ? mc : 0;
-    const int64_t mbb = rwb ? al((int64_t)layers * p->Gc * H * es) : 0;
+    const int64_t mbb = rwb ? al((int64_t)layers * (p->Gc + p->Gv) * H * es) : 0;
     char *r = c + xb + xb2 + mv + mc + vs + cs + wtb;
     w.S = rwb ? reinterpret_cast<float *>(r) : nullptr;
     w.memb = rwb ? reinterpret_cast<float *>(r + rwb) : nullptr;
+    w.memb_v = rwb ? w.memb + (int64_t)layers * p->Gc * H : nullptr;
     const int64_t hb = wide ? al(B * p->E * 2 * H * es) : 0;
     char *q = r + rwb + mbb;
     w.Pv = wide ? reinterpret_cast<float *>(q) : nullptr;
@@ -2002,6 +2054,10 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         hipLaunchKernelGGL(gnn_memb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_weights + 2 * H,
                            layer_floats(H, types), d_msg_type, p->cg_ptr, p->cg_mem, p->inv_c, p->Gc, layers, w.memb);
         LDPC_CHECK_LAUNCH("gnn_memb_kernel");
+        const int64_t nv = (int64_t)layers * p->Gv * 64;
+        hipLaunchKernelGGL(gnn_memb_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s, d_weights + 2 * H,
+                           layer_floats(H, types), d_msg_type, p->vg_ptr, p->vg_mem, p->inv_v, p->Gv, layers, w.memb_v);
+        LDPC_CHECK_LAUNCH("gnn_memb_kernel");
     }
     // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
     const GnnLayer L0 = L;
@@ -2061,6 +2117,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
                 L.S_in = l > 0 ? w.S + b0 * p->Gc * H : nullptr;
                 L.S_out = l + 1 < layers ? w.S + b0 * p->Gc * H : nullptr;
                 L.memb = w.memb + (int64_t)l * p->Gc * H;
+                L.memb_v = w.memb_v + (int64_t)l * p->Gv * H;
             } else if (d1t) {
                 L.tperm = p->mt_perm;
                 L.ntile_pf = p->n_mtiles;
