@@ -21,13 +21,20 @@ PY
   cp gpurun_out/prof_${T}_${W}/lib_sha256.txt gpurun_out/prof_${T}_${W}/code_objects_sha256.txt $O/prof_${W}/
   python3 tools/pmc_kernels.py gpurun_out/prof_${T}_${W} > $O/prof_${W}/pmc_per_kernel.txt || true
 }
-if [ "$WHAT" = all ] || [ "$WHAT" = profile ]; then
+# PART=1 / PART=2: the first three / the last three workloads (one GPU call each)
+P1=true; P2=true
+[ "${PART:-}" = 1 ] && P2=false
+[ "${PART:-}" = 2 ] && P1=false
+if { [ "$WHAT" = all ] || [ "$WHAT" = profile ]; } && $P1; then
   bash tools/gpu_profile.sh gnn-z32 $T > $O/prof_gnn-z32.log 2>&1 || exit 1
   summ gnn-z32 "gnn_|csr_" csr_count_kernel 10922.666666666666 "per call = one fp32 GNN forward call on one workspace chunk (bench's B=32768 runs as 3 chunks of ~10923 frames); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
   bash tools/gpu_profile.sh gnn-z32-bf16 $T > $O/prof_gnn-z32-bf16.log 2>&1 || exit 1
   summ gnn-z32-bf16 "gnn_|csr_" gnn_bf16_info_kernel 16384 "per call = one 15-layer bf16 GNN forward with per-frame early termination on one 16384-frame chunk (B=32768 runs as 2 chunks), random codewords at 2 dB; every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1
   bash tools/gpu_profile.sh gnn-z32-bf16-i10 $T > $O/prof_gnn-z32-bf16-i10.log 2>&1 || exit 1
   summ gnn-z32-bf16-i10 "gnn_|csr_" gnn_bf16_info_kernel 16384 "per call = one 10-layer bf16 GNN forward on one 16384-frame chunk (B=32768 runs as 2 chunks); every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1
+  echo "profiles part 1 ok"
+fi
+if { [ "$WHAT" = all ] || [ "$WHAT" = profile ]; } && $P2; then
   bash tools/gpu_profile.sh gnn-z32-h128 $T > $O/prof_gnn-z32-h128.log 2>&1 || exit 1
   summ gnn-z32-h128 "gnn_|csr_" csr_count_kernel 2730.6666666666665 "per call = one H=128 fp32 GNN forward call on one workspace chunk (B=8192 runs as 3 chunks); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
   bash tools/gpu_profile.sh gnn-train-z32 $T > $O/prof_gnn-train-z32.log 2>&1 || exit 1
