@@ -855,7 +855,17 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
 // same value as fmaxf(v, 0) for every non-NaN v, without the canonicalising v_max fmaxf needs
 __device__ __forceinline__ float relu_i(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
 
-// ------------------------------------------------------------------------ MLP over projected groups, fp32 by bf16x6
+// ------------------------------------------------------------------------ MLP over projected groups, fp32 by split MFMAs
+// Default (LDPC_S6_F16, round 5): scaled two-term f16 splits.  The weights are scaled by one power of
+// two (largest |w| to at most 2^15), each message's activation column by another (its largest
+// |value|, bounded by max |x| + max |emb[type]| for GEMM1 and by max relu(h) over both sides for
+// GEMM2), so v = v0 + v1 with v0 = f16(v), v1 = f16(v - v0) holds 22 significant bits in the f16
+// normal range, and a product is a1 b0 + a0 b1 + a0 b0 on v_mfma_f32_32x32x16_f16 (the dropped a1 b1
+// is below 2^-22 of the column's largest product); the accumulators start from the scaled additive
+// term and are scaled back exactly after the GEMM.  3 MFMAs per K = 16 instead of 6: 61.4-61.6 k vs
+// 57.0-57.2 k cw/s on cfg4 (profiles/r05/ab_r05f16e); test_split_mlp_is_fp32_accurate holds its bar
+// (error against the float64 oracle within 2x of an fp32 GEMM's).  The bf16x6 form below remains the
+// LDPC_S6_F16=0 build:
 // gnn_mlp2_kernel's math with every fp32 product on v_mfma_f32_32x32x16_bf16: each fp32 operand is
 // split into three bf16 terms, v = v0 + v1 + v2 (v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 -
 // v1): 24 significant bits, every subtraction exact), and a product a b is the six terms
@@ -868,15 +878,64 @@ __device__ __forceinline__ float relu_i(float v) { return __int_as_float(max(__f
 // 32 (s>>1) + 16 (s&1) + 8 (i>>2) + 4 h + (i&3), which is the unit that lane owns in register
 // 8 (s&1) + i of accumulator tile s>>1: so GEMM2's B operand is GEMM1's accumulator as it stands,
 // and the x values loaded for GEMM1 are the residual the lane adds to its output registers.
-constexpr int kS6Row = 72;                                         // bf16 per image row
-constexpr int kS6Img = 64 * kS6Row;                                // bf16 per split image
-constexpr int kS6OffW2 = 6 * kS6Img;                               // W1L (side, split), then W2
-constexpr int kS6Bytes = 12 * kS6Img * 2;                          // 12 images
+// LDPC_S6_F16 (default): the MLP's fp32 products as scaled two-term f16 splits (3 MFMAs per product)
+// instead of three-term bf16 splits (6); LDPC_S6_PCEARLY: the check side's projected row seeds the
+// accumulators (the f16 kernel's registers have no room for the late add)
+#ifndef LDPC_S6_F16
+#define LDPC_S6_F16 1
+#endif
+#ifndef LDPC_S6_PCEARLY
+#define LDPC_S6_PCEARLY LDPC_S6_F16
+#endif
+#if LDPC_S6_F16
+typedef _Float16 s6_t;
+typedef _Float16 s6x8_t __attribute__((ext_vector_type(8)));
+constexpr int kS6Split = 2;
+#else
+typedef __bf16 s6_t;
+typedef bf16x8_t s6x8_t;
+constexpr int kS6Split = 3;
+#endif
+constexpr int kS6Row = 72;                                         // elements per image row
+constexpr int kS6Img = 64 * kS6Row;                                // elements per split image
+constexpr int kS6OffW2 = 2 * kS6Split * kS6Img;                    // W1L (side, split), then W2
+constexpr int kS6Bytes = 4 * kS6Split * kS6Img * 2;                // 4 matrices x kS6Split images
 constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo
 constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: emb [T][kPS]
 // then, with degree-1 tiles (GnnLayer tperm), the three split images of W1v_left + W1v_right
-__host__ __device__ inline int s6_off_d1(int T) { return ((kS6OffEmb + T * kPS) * 4 + 15) / 16 * 16; }
-inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d1 ? 3 * kS6Img * 2 : 0); }
+// (f16 splits: then max |emb[t]| per type, T floats)
+__host__ __device__ inline int s6_off_d1(int T) { return ((kS6OffEmb + T * kPS + T) * 4 + 15) / 16 * 16; }
+inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d1 ? kS6Split * kS6Img * 2 : 0); }
+#if LDPC_S6_F16
+// f16 two-term split of a scaled value: v = v0 + v1 + O(2^-22 |v|) (v0 = f16(v), v - v0 exact)
+__device__ __forceinline__ void split2h(const float *v, s6x8_t &a, s6x8_t &b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const _Float16 h0 = (_Float16)v[i];
+        a[i] = h0;
+        b[i] = (_Float16)(v[i] - (float)h0);
+    }
+}
+__device__ __forceinline__ void split2h_store(float w, s6_t *d, int stride) {
+    const _Float16 h0 = (_Float16)w;
+    d[0] = h0;
+    d[stride] = (_Float16)(w - (float)h0);
+}
+// acc += A B over one K = 16 step on v_mfma_f32_32x32x16_f16: a1 b0 + a0 b1 + a0 b0
+__device__ __forceinline__ f32x16 mfma3h(const s6_t *img, const s6x8_t &b0, const s6x8_t &b1, f32x16 acc) {
+    const s6x8_t a0 = *reinterpret_cast<const s6x8_t *>(img), a1 = *reinterpret_cast<const s6x8_t *>(img + kS6Img);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+}
+// 2^e as a float (e clamped to the normal range)
+__device__ __forceinline__ float pow2f(int e) { return __int_as_float((min(max(e, -126), 127) + 127) << 23); }
+// the exponent that scales a column whose largest magnitude is m to at most 2^15 (f16 max 65504)
+__device__ __forceinline__ int col_exp(float m) {
+    const int b = (__float_as_int(m) >> 23) & 0xff;  // biased exponent (m >= 0)
+    return b == 0 || b == 255 ? 0 : 141 - b;        // 14 - (b - 127)
+}
+#endif
 
 // Degree-1 tiles (tperm set, var side): a degree-1 var group's mean is the message's own c, so
 // W1v [c; g] = (W1v_left + W1v_right) c -- one fp32 sum per weight, rounded once and split like the
@@ -885,20 +944,48 @@ inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d
 template <int NT, int WPS, bool HYB = false, bool RW = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __bf16 *img = reinterpret_cast<__bf16 *>(lds);
+    s6_t *img = reinterpret_cast<s6_t *>(lds);
     const int tid = threadIdx.x;
+    const bool d1img = (P.tperm || RW) && P.ntile_v1 && P.vside;  // the combined image, when degree-1 tiles exist
+#if LDPC_S6_F16
+    // one power-of-two scale for every weight image: the largest |w| to at most 2^15
+    __shared__ int wmax_bits;
+    if (tid == 0) wmax_bits = 0;
+    __syncthreads();
+    {
+        float m = 0.0f;
+        for (int i = tid; i < 64 * 64; i += NT) {
+            const int o = i >> 6, u = i & 63;
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(P.w1v[o * 128 + u]), fabsf(P.w1c[o * 128 + u])),
+                               fmaxf(fabsf(P.w2v[o * 64 + u]), fabsf(P.w2c[o * 64 + u]))));
+            if (d1img) m = fmaxf(m, fabsf(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u]));
+        }
+        atomicMax(&wmax_bits, __float_as_int(m));
+    }
+    __syncthreads();
+    const int wexp = col_exp(__int_as_float(wmax_bits));
+    const float wsc = pow2f(wexp);
+#endif
     for (int i = tid; i < 64 * 64; i += NT) {
         const int o = i >> 6, p = i & 63, u = pi16(p);
         const float w[4] = {P.w1v[o * 128 + u], P.w1c[o * 128 + u], P.w2v[o * 64 + u], P.w2c[o * 64 + u]};
 #pragma unroll
-        for (int q = 0; q < 4; ++q)  // q: W1v, W1c, W2v, W2c -> images 3q .. 3q + 2
+        for (int q = 0; q < 4; ++q)  // q: W1v, W1c, W2v, W2c -> images kS6Split q ..
+#if LDPC_S6_F16
+            split2h_store(w[q] * wsc, img + 2 * q * kS6Img + o * kS6Row + p, kS6Img);
+#else
             split_store(w[q], img + 3 * q * kS6Img + o * kS6Row + p, kS6Img);
+#endif
     }
-    __bf16 *img_d1 = reinterpret_cast<__bf16 *>(reinterpret_cast<char *>(lds) + s6_off_d1(P.T));
-    if ((P.tperm || RW) && P.ntile_v1 && P.vside)  // the combined image, when degree-1 tiles exist
+    s6_t *img_d1 = reinterpret_cast<s6_t *>(reinterpret_cast<char *>(lds) + s6_off_d1(P.T));
+    if (d1img)
         for (int i = tid; i < 64 * 64; i += NT) {
             const int o = i >> 6, p = i & 63, u = pi16(p);
+#if LDPC_S6_F16
+            split2h_store((P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u]) * wsc, img_d1 + o * kS6Row + p, kS6Img);
+#else
             split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_d1 + o * kS6Row + p, kS6Img);
+#endif
         }
     if (tid < 64) {
         lds[kS6OffB + tid] = (P.vside ? P.b2v[tid] : 0.0f) + P.b2c[tid];  // both output biases
@@ -908,6 +995,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     // emb rows kPS = 68 floats apart: lanes of different types read different rows (64 apart, every
     // row would sit on the same banks)
     for (int i = tid; i < P.T * 64; i += NT) lds[kS6OffEmb + (i >> 6) * kPS + (i & 63)] = P.emb[i];
+#if LDPC_S6_F16
+    for (int t = tid; t < P.T; t += NT) {  // max |emb[t]|: |c| <= max |x| + this bounds a column's scale
+        float m = 0.0f;
+        for (int u = 0; u < 64; ++u) m = fmaxf(m, fabsf(P.emb[t * 64 + u]));
+        lds[kS6OffEmb + P.T * kPS + t] = m;
+    }
+#endif
     __syncthreads();
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the walk's indices in SGPRs
@@ -977,12 +1071,53 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         f32x16 hs[2][2];
         hs[0][0] = pv[0];
         hs[0][1] = pv[1];
+#if LDPC_S6_PCEARLY
+        load_acc(hs[1], pc);
+#else
         // the check side's projected row is added after GEMM1 (its load lands under the MFMAs)
         f32x16 pcr[2];
         load_acc(pcr, pc);
         hs[1][0] = f32x16{};
         hs[1][1] = f32x16{};
-        const __bf16 *W1v = (d1t ? img_d1 : img) + abase, *W1c = img + 3 * kS6Img + abase;
+#endif
+        const s6_t *W1v = (d1t ? img_d1 : img) + abase, *W1c = img + kS6Split * kS6Img + abase;
+#if LDPC_S6_F16
+        // the message's c scaled by a power of two (its largest |c| to at most 2^15), the
+        // accumulators by that times the weights' scale: products of scaled two-term f16 splits
+        float cm = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cm = fmaxf(cm, fabsf(x[s][i]));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64)) + lds[kS6OffEmb + P.T * kPS + typ];  // >= max |c|
+        const int cexp = col_exp(cm);
+        const float csc = pow2f(cexp), asc = pow2f(cexp + wexp), iasc = pow2f(-cexp - wexp);
+        hs[0][0] *= asc;
+        hs[0][1] *= asc;
+#if LDPC_S6_PCEARLY
+        hs[1][0] *= asc;
+        hs[1][1] *= asc;
+#endif
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            float c[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[i] = (x[s][i] + e[pi16(16 * s + 8 * half + i)]) * csc;
+            s6x8_t c0, c1;
+            split2h(c, c0, c1);
+            if (vs) {
+                hs[0][0] = mfma3h(W1v + 16 * s, c0, c1, hs[0][0]);
+                hs[0][1] = mfma3h(W1v + 32 * kS6Row + 16 * s, c0, c1, hs[0][1]);
+            }
+            hs[1][0] = mfma3h(W1c + 16 * s, c0, c1, hs[1][0]);
+            hs[1][1] = mfma3h(W1c + 32 * kS6Row + 16 * s, c0, c1, hs[1][1]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        hs[0][0] *= iasc;
+        hs[0][1] *= iasc;
+        hs[1][0] *= iasc;
+        hs[1][1] *= iasc;
+#else
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             float c[8];
@@ -998,8 +1133,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             hs[1][1] = mfma6(W1c + 32 * kS6Row + 16 * s, c0, c1, c2, hs[1][1], kS6Img);
             __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
         }
+#endif
+#if !LDPC_S6_PCEARLY
         hs[1][0] += pcr[0];
         hs[1][1] += pcr[1];
+#endif
         // GEMM2's accumulators start from the residual and the output biases: register 4 q + i of
         // tile ot is unit 32 ot + 8 q + 4 half + i = x[2 ot + (q >> 1)][4 (q & 1) + i]
         f32x16 y0, y1;
@@ -1021,26 +1159,54 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                         x[s][4 * q] = v.x; x[s][4 * q + 1] = v.y; x[s][4 * q + 2] = v.z; x[s][4 * q + 3] = v.w;
                     }
         }
+#if LDPC_S6_F16
+        // both sides' relu(h) under one column scale (they accumulate into the same y)
+        float hm = 0.0f;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            if (side == 0 && !vs) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hm = fmaxf(hm, fmaxf(hs[side][0][r], hs[side][1][r]));
+        }
+        hm = fmaxf(hm, __shfl_xor(hm, 32, 64));  // >= 0: the largest relu(h)
+        const int hexp = col_exp(hm);
+        const float hsc = pow2f(hexp), ysc = pow2f(hexp + wexp), iysc = pow2f(-hexp - wexp);
+        y0 *= ysc;
+        y1 *= ysc;
+#endif
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             if (side == 0 && !vs) continue;
             const f32x16 &h0 = hs[side][0], &h1 = hs[side][1];
-            const __bf16 *W2 = img + kS6OffW2 + 3 * side * kS6Img + abase;
+            const s6_t *W2 = img + kS6OffW2 + kS6Split * side * kS6Img + abase;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {  // GEMM2: y += W2 relu(h); k-step s = registers 8 (s&1) .. of h_{s>>1}
                 float hr[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) hr[i] = relu_i(s < 2 ? h0[8 * (s & 1) + i] : h1[8 * (s & 1) + i]);
+#if LDPC_S6_F16
+#pragma unroll
+                for (int i = 0; i < 8; ++i) hr[i] *= hsc;
+                s6x8_t r0, r1;
+                split2h(hr, r0, r1);
+                y0 = mfma3h(W2 + 16 * s, r0, r1, y0);
+                y1 = mfma3h(W2 + 32 * kS6Row + 16 * s, r0, r1, y1);
+#else
                 bf16x8_t r0, r1, r2;
                 split3(hr, r0, r1, r2);
                 y0 = mfma6(W2 + 16 * s, r0, r1, r2, y0, kS6Img);
                 y1 = mfma6(W2 + 32 * kS6Row + 16 * s, r0, r1, r2, y1, kS6Img);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (RW) {  // the var side is consumed: the next tile's var-side row
                 if (side == 0) load_acc(pv, (d1n ? P.b1v : P.Mv + (bn * P.Gv + vgn) * 64) + 4 * half);
             }
         }
+#if LDPC_S6_F16
+        y0 *= iysc;
+        y1 *= iysc;
+#endif
         float part = 0.0f;
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {

@@ -134,9 +134,9 @@ def test_cfg5_full_batch_properties(cuda):
 
 
 def test_split_mlp_is_fp32_accurate(cuda, oracle_mod, monkeypatch):
-    """The bf16x6 MLP (gnn_mlp2s_kernel) is an fp32 GEMM up to summation order: against the
-    float64 oracle its error is within 2x (+1e-7) of the fp32-MFMA kernel's and of the float32
-    oracle's own, at 10 layers, Z=32."""
+    """The split MLP (gnn_mlp2s_kernel: scaled two-term f16 splits, 3 MFMAs per product) is
+    fp32-accurate: against the float64 oracle its error is within 2x (+1e-7) of the fp32-MFMA
+    kernel's and of the float32 oracle's own, at 10 layers, Z=32."""
     base, H, dec, conv, types = _model(10, cuda, seed=5)
     llr = awgn_llr(16, H.shape[1], 1.0, seed=9, device=cuda)
     sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
