@@ -889,7 +889,7 @@ __device__ __forceinline__ float relu_i(float v) { return __int_as_float(max(__f
 #endif
 #if LDPC_S6_F16
 typedef _Float16 s6_t;
-typedef _Float16 s6x8_t __attribute__((ext_vector_type(8)));
+typedef f16x8_t s6x8_t;
 constexpr int kS6Split = 2;
 #else
 typedef __bf16 s6_t;
@@ -906,36 +906,6 @@ constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: em
 // (f16 splits: then max |emb[t]| per type, T floats)
 __host__ __device__ inline int s6_off_d1(int T) { return ((kS6OffEmb + T * kPS + T) * 4 + 15) / 16 * 16; }
 inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d1 ? kS6Split * kS6Img * 2 : 0); }
-#if LDPC_S6_F16
-// f16 two-term split of a scaled value: v = v0 + v1 + O(2^-22 |v|) (v0 = f16(v), v - v0 exact)
-__device__ __forceinline__ void split2h(const float *v, s6x8_t &a, s6x8_t &b) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const _Float16 h0 = (_Float16)v[i];
-        a[i] = h0;
-        b[i] = (_Float16)(v[i] - (float)h0);
-    }
-}
-__device__ __forceinline__ void split2h_store(float w, s6_t *d, int stride) {
-    const _Float16 h0 = (_Float16)w;
-    d[0] = h0;
-    d[stride] = (_Float16)(w - (float)h0);
-}
-// acc += A B over one K = 16 step on v_mfma_f32_32x32x16_f16: a1 b0 + a0 b1 + a0 b0
-__device__ __forceinline__ f32x16 mfma3h(const s6_t *img, const s6x8_t &b0, const s6x8_t &b1, f32x16 acc) {
-    const s6x8_t a0 = *reinterpret_cast<const s6x8_t *>(img), a1 = *reinterpret_cast<const s6x8_t *>(img + kS6Img);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
-}
-// 2^e as a float (e clamped to the normal range)
-__device__ __forceinline__ float pow2f(int e) { return __int_as_float((min(max(e, -126), 127) + 127) << 23); }
-// the exponent that scales a column whose largest magnitude is m to at most 2^15 (f16 max 65504)
-__device__ __forceinline__ int col_exp(float m) {
-    const int b = (__float_as_int(m) >> 23) & 0xff;  // biased exponent (m >= 0)
-    return b == 0 || b == 255 ? 0 : 141 - b;        // 14 - (b - 127)
-}
-#endif
 
 // Degree-1 tiles (tperm set, var side): a degree-1 var group's mean is the message's own c, so
 // W1v [c; g] = (W1v_left + W1v_right) c -- one fp32 sum per weight, rounded once and split like the
@@ -1106,11 +1076,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             s6x8_t c0, c1;
             split2h(c, c0, c1);
             if (vs) {
-                hs[0][0] = mfma3h(W1v + 16 * s, c0, c1, hs[0][0]);
-                hs[0][1] = mfma3h(W1v + 32 * kS6Row + 16 * s, c0, c1, hs[0][1]);
+                hs[0][0] = mfma3h(W1v + 16 * s, c0, c1, hs[0][0], kS6Img);
+                hs[0][1] = mfma3h(W1v + 32 * kS6Row + 16 * s, c0, c1, hs[0][1], kS6Img);
             }
-            hs[1][0] = mfma3h(W1c + 16 * s, c0, c1, hs[1][0]);
-            hs[1][1] = mfma3h(W1c + 32 * kS6Row + 16 * s, c0, c1, hs[1][1]);
+            hs[1][0] = mfma3h(W1c + 16 * s, c0, c1, hs[1][0], kS6Img);
+            hs[1][1] = mfma3h(W1c + 32 * kS6Row + 16 * s, c0, c1, hs[1][1], kS6Img);
             __builtin_amdgcn_sched_barrier(0);
         }
         hs[0][0] *= iasc;
@@ -1189,8 +1159,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 for (int i = 0; i < 8; ++i) hr[i] *= hsc;
                 s6x8_t r0, r1;
                 split2h(hr, r0, r1);
-                y0 = mfma3h(W2 + 16 * s, r0, r1, y0);
-                y1 = mfma3h(W2 + 32 * kS6Row + 16 * s, r0, r1, y1);
+                y0 = mfma3h(W2 + 16 * s, r0, r1, y0, kS6Img);
+                y1 = mfma3h(W2 + 32 * kS6Row + 16 * s, r0, r1, y1, kS6Img);
 #else
                 bf16x8_t r0, r1, r2;
                 split3(hr, r0, r1, r2);

@@ -182,6 +182,40 @@ __device__ __forceinline__ void split_store(float w, __bf16 *d, int stride) {
     d[2 * stride] = (__bf16)(r1 - (float)h1);
 }
 __device__ __forceinline__ bf16x8_t lds8(const __bf16 *p) { return *reinterpret_cast<const bf16x8_t *>(p); }
+// ---- fp32 products as scaled two-term f16 splits on v_mfma_f32_32x32x16_f16 (gnn.hip
+// gnn_mlp2s_kernel, gnn_train.hip train_mlp_bwd_s6_kernel): an operand column scaled by a power of
+// two (its largest magnitude to at most 2^15, inside f16's normal range) splits as v = v0 + v1,
+// v0 = f16(v), v1 = f16(v - v0) (22 significant bits); a product is a1 b0 + a0 b1 + a0 b0
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split2h(const float *v, f16x8_t &a, f16x8_t &b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const _Float16 h0 = (_Float16)v[i];
+        a[i] = h0;
+        b[i] = (_Float16)(v[i] - (float)h0);
+    }
+}
+__device__ __forceinline__ void split2h_store(float w, _Float16 *d, int stride) {
+    const _Float16 h0 = (_Float16)w;
+    d[0] = h0;
+    d[stride] = (_Float16)(w - (float)h0);
+}
+// 2^e as a float (e clamped to the normal range)
+__device__ __forceinline__ float pow2f(int e) { return __int_as_float((min(max(e, -126), 127) + 127) << 23); }
+// the exponent that scales a column whose largest magnitude is m (>= 0) to at most 2^15 (0: m is
+// zero, subnormal, inf or NaN)
+__device__ __forceinline__ int col_exp(float m) {
+    const int b = (__float_as_int(m) >> 23) & 0xff;
+    return b == 0 || b == 255 ? 0 : 141 - b;  // 14 - (b - 127)
+}
+// acc += A B over one K = 16 step: A's two split images at img and img + img_stride
+__device__ __forceinline__ f32x16_t mfma3h(const _Float16 *img, const f16x8_t &b0, const f16x8_t &b1, f32x16_t acc,
+                                           int img_stride) {
+    const f16x8_t a0 = *reinterpret_cast<const f16x8_t *>(img), a1 = *reinterpret_cast<const f16x8_t *>(img + img_stride);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+}
 // acc += A B over one K = 16 step, A from the three split images at img (+ img_stride, + 2 img_stride)
 __device__ __forceinline__ f32x16_t mfma6(const __bf16 *img, const bf16x8_t &b0, const bf16x8_t &b1,
                                         const bf16x8_t &b2, f32x16_t acc, int img_stride) {
