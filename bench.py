@@ -514,7 +514,7 @@ def main():
         # (two sides x (W1 over [c; g]: 4 H^2 + W2: 2 H^2)); W1's group half is applied once per group
         # (gnn.hip, gnn_group_proj_kernel), so 8 H^2 per message + 2 H^2 per var / check group
         fwd_flops = 8 * hid * hid * E + 2 * hid * hid * (g_n + g_m)
-        mlp_flops = 8 * hid * hid * E  # of which on the MLP kernel (bf16x6 splits)
+        mlp_flops = 8 * hid * hid * E  # of which on the MLP kernel (f16 splits)
         nominal_flops = 12 * hid * hid * E
         if kind == "hybrid-gnn":
             # check side only: 4 H^2 per message (W1 over c + W2) + 2 H^2 per check group (projection)
@@ -544,6 +544,13 @@ def main():
             # outer products) per frame-layer, fp32 (VALU fp32 peak = fp32 MFMA peak)
             per_launch_alg = 36 * 64 * 64 * E * B * iters
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
+        elif kind == "gnn" and os.environ.get("LDPC_GNN_SPLIT", "1") != "0":
+            # cfg2 shape on the split MLP: its products run as scaled two-term f16 splits, three
+            # v_mfma_f32_32x32x16_f16 products per fp32 product (gnn.hip gnn_mlp2s_kernel), so the
+            # bound is the f16 MFMA pipe on those executed FLOPs; the reference's FLOPs against the fp32
+            # MFMA peak (SURVEY 8(d) cfg2's yardstick, > 1 here) are in the notes
+            per_launch_alg = 3 * mlp_flops * B * iters
+            bound, unit, peak = "mfma", "TFLOP/s", BF16_MFMA_PEAK_TFS
         else:
             # the reference's useful FLOPs, 12 H^2 E per frame-layer
             # (this build executes fewer: see the notes' executed_frac)
@@ -630,20 +637,24 @@ def main():
             secs = kern_ms * 1e-3
             notes = {"flop_model": "the reference's per-message MLPs cost 12 H^2 E FLOP per frame-layer (SURVEY 8(d)); "
                                    "this build executes 8 H^2 E + 2 H^2 (N + M) fp32-equivalent FLOPs (W1's group half "
-                                   "once per group). Reported for reference only: the bound is HBM (roofline.bound)",
+                                   "once per group). Reported for reference only: roofline.bound names the binding resource",
                      "nominal_fp32_tflops": nominal_flops * B * iters * reps / secs / 1e12,
                      "nominal_frac_of_fp32_mfma": nominal_flops * B * iters * reps / secs / 1e12 / FP32_MFMA_PEAK_TFS,
                      "executed_flops_per_launch": fwd_flops * B * iters * reps}
-            if bound != "hbm":  # Z = 4 (cfg2 shape): FLOPs against the fp32 MFMA peak, as SURVEY 8(d) cfg2
+            if bound != "hbm" and not split:  # Z = 4 (cfg2 shape) on the fp32 MFMA kernels
                 notes["executed_frac"] = fwd_flops / nominal_flops * achieved / peak
             if split:
-                # gnn_mlp2s_kernel: the per-message products (8 H^2 E) as six bf16 products each on the
-                # bf16 MFMA; the group projection (2 H^2 (N + M)) stays on the fp32 MFMA
-                mlp_bf16 = 6 * mlp_flops * B * iters * reps
-                notes["mlp_products"] = ("bf16x6 split (fp32-accurate, tests/test_gnn_depth_gpu.py::"
-                                         "test_split_mlp_is_fp32_accurate)")
-                notes["mlp_bf16_mfma_flops_per_launch"] = mlp_bf16
-                notes["mlp_bf16_mfma_frac_whole_forward"] = mlp_bf16 / (kern_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFS
+                # gnn_mlp2s_kernel: the per-message products (8 H^2 E) as three f16 products each on the
+                # f16 MFMA (scaled two-term splits); the group projection (2 H^2 (N + M)) stays on the
+                # fp32 MFMA
+                mlp_f16 = 3 * mlp_flops * B * iters * reps
+                notes["mlp_products"] = ("scaled two-term f16 split, 3 f16 MFMA products per fp32 product "
+                                         "(fp32-accurate: tests/test_gnn_depth_gpu.py::test_split_mlp_is_fp32_accurate)")
+                notes["mlp_f16_mfma_flops_per_launch"] = mlp_f16
+                notes["mlp_f16_mfma_frac_whole_forward"] = mlp_f16 / (kern_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFS
+                if bound == "mfma":
+                    notes["nominal_over_fp32_peak"] = ("the reference's FLOPs per second exceed the fp32 MFMA "
+                                                       "peak: the products run on the f16 MFMA (three per product)")
         if bound == "valu":
             achieved, notes = valu_roofline(B, n, kern_ms, traffic, tjd, tj if tjd else None, per_launch_alg)
             if tjd is None:
