@@ -896,8 +896,31 @@ typedef __bf16 s6_t;
 typedef bf16x8_t s6x8_t;
 constexpr int kS6Split = 3;
 #endif
+// LDPC_S6_PCLDS (default): the row walk copies its unit's 32 projected check rows into LDS at the
+// unit's first tile (lane-private slots), so the unit's other tiles do not re-read them from L2,
+// where the walk's streaming rows have long evicted them (+7.1 % on gnn-z32, profiles/r05/ab_r05pcl);
+// it needs the swizzled unpadded weight images (LDPC_S6_SW) to fit 160 KB
+#ifndef LDPC_S6_PCLDS
+#define LDPC_S6_PCLDS 1
+#endif
+#ifndef LDPC_S6_SW
+#define LDPC_S6_SW LDPC_S6_PCLDS
+#endif
+#if LDPC_S6_SW
+constexpr int kS6Row = 64;                                         // elements per image row
+#else
 constexpr int kS6Row = 72;                                         // elements per image row
+#endif
 constexpr int kS6Img = 64 * kS6Row;                                // elements per split image
+// element (row o, column p) of a split image: padded rows, or 128-B rows whose 16-B chunks are
+// XOR-swizzled by row pair (a fragment read's 16 lanes then cover all 64 banks)
+__host__ __device__ constexpr int s6_at(int o, int p) {
+#if LDPC_S6_SW
+    return o * 64 + ((((p >> 3) ^ ((o >> 1) & 7))) << 3) + (p & 7);
+#else
+    return o * kS6Row + p;
+#endif
+}
 constexpr int kS6OffW2 = 2 * kS6Split * kS6Img;                    // W1L (side, split), then W2
 constexpr int kS6Bytes = 4 * kS6Split * kS6Img * 2;                // 4 matrices x kS6Split images
 constexpr int kS6OffB = kS6Bytes / 4;                              // floats: b2v, b2c, wo
@@ -906,6 +929,11 @@ constexpr int kS6OffEmb = kS6OffB + 3 * 64;                        // floats: em
 // (f16 splits: then max |emb[t]| per type, T floats)
 __host__ __device__ inline int s6_off_d1(int T) { return ((kS6OffEmb + T * kPS + T) * 4 + 15) / 16 * 16; }
 inline size_t mlp2s_lds_bytes(int T, bool d1) { return (size_t)s6_off_d1(T) + (d1 ? kS6Split * kS6Img * 2 : 0); }
+// row walk with LDPC_S6_PCLDS: after the degree-1 image's slot, 8 KB per wave of staged check rows
+__host__ __device__ inline int s6_off_pc(int T) { return s6_off_d1(T) + kS6Split * kS6Img * 2; }
+inline size_t mlp2s_rw_lds_bytes(int T, bool d1, int waves) {
+    return LDPC_S6_PCLDS ? (size_t)s6_off_pc(T) + (size_t)waves * 32 * 64 * 4 : mlp2s_lds_bytes(T, d1);
+}
 
 // Degree-1 tiles (tperm set, var side): a degree-1 var group's mean is the message's own c, so
 // W1v [c; g] = (W1v_left + W1v_right) c -- one fp32 sum per weight, rounded once and split like the
@@ -942,9 +970,9 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)  // q: W1v, W1c, W2v, W2c -> images kS6Split q ..
 #if LDPC_S6_F16
-            split2h_store(w[q] * wsc, img + 2 * q * kS6Img + o * kS6Row + p, kS6Img);
+            split2h_store(w[q] * wsc, img + 2 * q * kS6Img + s6_at(o, p), kS6Img);
 #else
-            split_store(w[q], img + 3 * q * kS6Img + o * kS6Row + p, kS6Img);
+            split_store(w[q], img + 3 * q * kS6Img + s6_at(o, p), kS6Img);
 #endif
     }
     s6_t *img_d1 = reinterpret_cast<s6_t *>(reinterpret_cast<char *>(lds) + s6_off_d1(P.T));
@@ -952,9 +980,9 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         for (int i = tid; i < 64 * 64; i += NT) {
             const int o = i >> 6, p = i & 63, u = pi16(p);
 #if LDPC_S6_F16
-            split2h_store((P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u]) * wsc, img_d1 + o * kS6Row + p, kS6Img);
+            split2h_store((P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u]) * wsc, img_d1 + s6_at(o, p), kS6Img);
 #else
-            split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_d1 + o * kS6Row + p, kS6Img);
+            split_store(P.w1v[o * 128 + u] + P.w1v[o * 128 + 64 + u], img_d1 + s6_at(o, p), kS6Img);
 #endif
         }
     if (tid < 64) {
@@ -976,8 +1004,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 
     const int lane = tid & 63, j = lane & 31, half = lane >> 5, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the walk's indices in SGPRs
     const float bo = P.last ? P.bo[0] : 0.0f;
-    const int abase = j * kS6Row + 8 * half;
-  // A fragment of row j (+ 32 rows: tile 1), k-step s at + 16 s
+    // A fragment of row j (+ 32 kS6Row: rows 32 .., whose swizzle equals row j's), k-step s
+    auto aof = [&](int s) { return s6_at(j, 16 * s + 8 * half); };
     const bool vs = HYB ? P.vside != 0 : true;  // the var side (only the hybrid kernel runs without it)
     float S[32];  // row walk: this lane's check's running sum of output rows (its half's 32 units)
 
@@ -1029,7 +1057,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     // this tile's) and var-side row (frame bn, var group vgn, degree-1 d1n; once GEMM2 has consumed
     // this tile's var side) into x and pv, so their latency hides under this tile's MFMAs.
     auto tile = [&](int64_t b, int64_t m, int64_t rr, bool ok, const float *pc, float (&x)[4][8], int typ,
-                    f32x16 (&pv)[2], bool d1t, const float *xn, int64_t bn, int vgn, bool d1n) {
+                    f32x16 (&pv)[2], bool d1t, const float *xn, int64_t bn, int vgn, bool d1n, int pcm) {
         const float *e = lds + kS6OffEmb + typ * kPS;
         // the per-walk constants are re-read from LDS at every tile (an opaque offset: hoisted out of the
         // walk they would hold 64 VGPRs)
@@ -1042,7 +1070,23 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         hs[0][0] = pv[0];
         hs[0][1] = pv[1];
 #if LDPC_S6_PCEARLY
+#if LDPC_S6_PCLDS
+        // pcm (uniform): 0 = the check row from global, else from the lane's LDS slots, which the row
+        // walk fills at the unit's first tile (float4 q of lane l at pcs[64 q + l]: conflict-free)
+        if (RW && pcm) {
+            const float4 *pcs = reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(lds) + s6_off_pc(P.T)) + wave * 512 + lane;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 a = pcs[64 * q], c = pcs[64 * (4 + q)];
+                hs[1][0][4 * q] = a.x; hs[1][0][4 * q + 1] = a.y; hs[1][0][4 * q + 2] = a.z; hs[1][0][4 * q + 3] = a.w;
+                hs[1][1][4 * q] = c.x; hs[1][1][4 * q + 1] = c.y; hs[1][1][4 * q + 2] = c.z; hs[1][1][4 * q + 3] = c.w;
+            }
+        } else {
+            load_acc(hs[1], pc);
+        }
+#else
         load_acc(hs[1], pc);
+#endif
 #else
         // the check side's projected row is added after GEMM1 (its load lands under the MFMAs)
         f32x16 pcr[2];
@@ -1050,7 +1094,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         hs[1][0] = f32x16{};
         hs[1][1] = f32x16{};
 #endif
-        const s6_t *W1v = (d1t ? img_d1 : img) + abase, *W1c = img + kS6Split * kS6Img + abase;
+        const s6_t *W1v = d1t ? img_d1 : img, *W1c = img + kS6Split * kS6Img;
 #if LDPC_S6_F16
         // the message's c scaled by a power of two (its largest |c| to at most 2^15), the
         // accumulators by that times the weights' scale: products of scaled two-term f16 splits
@@ -1076,11 +1120,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             s6x8_t c0, c1;
             split2h(c, c0, c1);
             if (vs) {
-                hs[0][0] = mfma3h(W1v + 16 * s, c0, c1, hs[0][0], kS6Img);
-                hs[0][1] = mfma3h(W1v + 32 * kS6Row + 16 * s, c0, c1, hs[0][1], kS6Img);
+                hs[0][0] = mfma3h(W1v + aof(s), c0, c1, hs[0][0], kS6Img);
+                hs[0][1] = mfma3h(W1v + 32 * kS6Row + aof(s), c0, c1, hs[0][1], kS6Img);
             }
-            hs[1][0] = mfma3h(W1c + 16 * s, c0, c1, hs[1][0], kS6Img);
-            hs[1][1] = mfma3h(W1c + 32 * kS6Row + 16 * s, c0, c1, hs[1][1], kS6Img);
+            hs[1][0] = mfma3h(W1c + aof(s), c0, c1, hs[1][0], kS6Img);
+            hs[1][1] = mfma3h(W1c + 32 * kS6Row + aof(s), c0, c1, hs[1][1], kS6Img);
             __builtin_amdgcn_sched_barrier(0);
         }
         hs[0][0] *= iasc;
@@ -1096,11 +1140,11 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             bf16x8_t c0, c1, c2;
             split3(c, c0, c1, c2);
             if (vs) {
-                hs[0][0] = mfma6(W1v + 16 * s, c0, c1, c2, hs[0][0], kS6Img);
-                hs[0][1] = mfma6(W1v + 32 * kS6Row + 16 * s, c0, c1, c2, hs[0][1], kS6Img);
+                hs[0][0] = mfma6(W1v + aof(s), c0, c1, c2, hs[0][0], kS6Img);
+                hs[0][1] = mfma6(W1v + 32 * kS6Row + aof(s), c0, c1, c2, hs[0][1], kS6Img);
             }
-            hs[1][0] = mfma6(W1c + 16 * s, c0, c1, c2, hs[1][0], kS6Img);
-            hs[1][1] = mfma6(W1c + 32 * kS6Row + 16 * s, c0, c1, c2, hs[1][1], kS6Img);
+            hs[1][0] = mfma6(W1c + aof(s), c0, c1, c2, hs[1][0], kS6Img);
+            hs[1][1] = mfma6(W1c + 32 * kS6Row + aof(s), c0, c1, c2, hs[1][1], kS6Img);
             __builtin_amdgcn_sched_barrier(0);  // one k-step's A fragments live at a time (VGPRs)
         }
 #endif
@@ -1148,7 +1192,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         for (int side = 0; side < 2; ++side) {
             if (side == 0 && !vs) continue;
             const f32x16 &h0 = hs[side][0], &h1 = hs[side][1];
-            const s6_t *W2 = img + kS6OffW2 + kS6Split * side * kS6Img + abase;
+            const s6_t *W2 = img + kS6OffW2 + kS6Split * side * kS6Img;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {  // GEMM2: y += W2 relu(h); k-step s = registers 8 (s&1) .. of h_{s>>1}
                 float hr[8];
@@ -1159,13 +1203,13 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
                 for (int i = 0; i < 8; ++i) hr[i] *= hsc;
                 s6x8_t r0, r1;
                 split2h(hr, r0, r1);
-                y0 = mfma3h(W2 + 16 * s, r0, r1, y0, kS6Img);
-                y1 = mfma3h(W2 + 32 * kS6Row + 16 * s, r0, r1, y1, kS6Img);
+                y0 = mfma3h(W2 + aof(s), r0, r1, y0, kS6Img);
+                y1 = mfma3h(W2 + 32 * kS6Row + aof(s), r0, r1, y1, kS6Img);
 #else
                 bf16x8_t r0, r1, r2;
                 split3(hr, r0, r1, r2);
-                y0 = mfma6(W2 + 16 * s, r0, r1, r2, y0, kS6Img);
-                y1 = mfma6(W2 + 32 * kS6Row + 16 * s, r0, r1, r2, y1, kS6Img);
+                y0 = mfma6(W2 + aof(s), r0, r1, r2, y0, kS6Img);
+                y1 = mfma6(W2 + 32 * kS6Row + aof(s), r0, r1, r2, y1, kS6Img);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -1265,8 +1309,22 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             const int typq = P.msg_type[mq], vgq = P.vgroup[mq];
             const int cg = cg0 + (okc ? j : 0);
             if (!P.x_in) load_x(x, b, m, b * P.E + m);  // layer 0: x from the LLR at the tile
+#if LDPC_S6_PCLDS
+            if (i == 0) {  // the unit's first tile: its 32 projected check rows into the lanes' LDS slots
+                const float *pc = P.Mc + (b * P.Gc + cg) * 64 + 4 * half;
+                float4 *pcs = reinterpret_cast<float4 *>(reinterpret_cast<char *>(lds) + s6_off_pc(P.T)) + wave * 512 + lane;
+                float4 v[8];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    v[q] = *reinterpret_cast<const float4 *>(pc + 8 * q);
+                    v[4 + q] = *reinterpret_cast<const float4 *>(pc + 32 + 8 * q);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) pcs[64 * q] = v[q];
+            }
+#endif
             tile(b, m, b * P.E + m, okc, P.Mc + (b * P.Gc + cg) * 64 + 4 * half, x, typ, pv, d1,
-                 P.x_in + (bq * P.E + mq) * 64 + 4 * half, bq, vgq, d1q);
+                 P.x_in + (bq * P.E + mq) * 64 + 4 * half, bq, vgq, d1q, 1);
             if (!inunit) {  // the unit's last tile: its checks' sums
                 if (okc && P.S_out) {
                     float *dst = P.S_out + (b * P.Gc + cg) * 64;
@@ -1325,7 +1383,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         f32x16 pv[2];
         load_x(x, b, m, rr);
         if (vs) load_acc(pv, pv_row(b, m, d1t));
-        tile(b, m, rr, ok, P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half, x, P.msg_type[m], pv, d1t, nullptr, 0, 0, false);
+        tile(b, m, rr, ok, P.Mc + (b * P.Gc + P.cgroup[m]) * 64 + 4 * half, x, P.msg_type[m], pv, d1t, nullptr, 0, 0, false, 0);
     }
 }
 
@@ -2166,10 +2224,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     // degree-1 message tiles first (gnn_mlp2s_kernel) when the combined image fits
     const bool d1t = split && p->n_mtiles_v1 > 0 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
     // row walk (gnn_mlp2s_kernel RW): check tile groups, per-check sums out of the MLP (w.S set by carve)
-    const bool rw = split && w.S && rowwalk_path();
+    const bool rw = split && w.S && rowwalk_path() && mlp2s_rw_lds_bytes(types, true, kMlp2sNt / 64) <= 160 * 1024;
     const bool rwd1 = rw && p->rw_d1 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
-                 mlp2_lds = split ? mlp2s_lds_bytes(types, rw ? rwd1 : d1t) : mlp2_lds_bytes(types);
+                 mlp2_lds = split ? (rw ? mlp2s_rw_lds_bytes(types, rwd1, kMlp2sNt / 64) : mlp2s_lds_bytes(types, d1t))
+                                  : mlp2_lds_bytes(types);
     const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
     int mlp2_per_cu = 1, proj_per_cu = 1;
