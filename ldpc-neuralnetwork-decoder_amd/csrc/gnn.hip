@@ -469,7 +469,15 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_mlp_mfma_kernel(GnnLayer P
 // against W1_right (LDS) and + b1.  Rows go to Mv / Mc (same shape as the group means).
 // LDS (floats): W1vR [64][68], W1cR [64][68], b1v, b1c, w_in, b_in [64 each], emb [T][68].
 constexpr int kPS = 68;
-constexpr int kPOffW1c = 64 * kPS, kPOffB = 2 * 64 * kPS, kPOffEmb = kPOffB + 4 * 64;
+// LDPC_PROJ_F16 (default): W1_right g as scaled two-term f16 splits on v_mfma_f32_32x32x16_f16 (as
+// the MLP's products, gnn_mlp2s_kernel): 24 MFMAs of 32 cycles per tile instead of 64 fp32 MFMAs of
+// 64 cycles (+2.6 % on gnn-z32, profiles/r05/ab_r05pf16).  The images are W1vR (hi, lo), W1cR (hi,
+// lo), rows of kPRow halves (16-B aligned, padded).
+#ifndef LDPC_PROJ_F16
+#define LDPC_PROJ_F16 1
+#endif
+constexpr int kPRow = 72, kPImg = 64 * kPRow;
+constexpr int kPOffW1c = 64 * kPS, kPOffB = LDPC_PROJ_F16 ? 4 * kPImg / 2 : 2 * 64 * kPS, kPOffEmb = kPOffB + 4 * 64;
 inline size_t proj_lds_bytes(int T, int waves) { return (size_t)(kPOffEmb + T * kPS + waves * 32 * kPS) * 4; }  // + 32 group means per wave
 
 struct ProjTiles {
@@ -483,11 +491,33 @@ template <int NT, bool HYB = false>
 __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group_proj_kernel(GnnLayer P, ProjTiles T) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
+#if LDPC_PROJ_F16
+    // one power-of-two scale for both images: the largest |w| to at most 2^15
+    __shared__ int wmax_bits;
+    if (tid == 0) wmax_bits = 0;
+    __syncthreads();
+    {
+        float m = 0.0f;
+        for (int i = tid; i < 64 * 64; i += NT)
+            m = fmaxf(m, fmaxf(fabsf(P.w1v[(i >> 6) * 128 + 64 + (i & 63)]), fabsf(P.w1c[(i >> 6) * 128 + 64 + (i & 63)])));
+        atomicMax(&wmax_bits, __float_as_int(m));
+    }
+    __syncthreads();
+    const int wexp = col_exp(__int_as_float(wmax_bits));
+    const float wsc = pow2f(wexp);
+    _Float16 *pimg = reinterpret_cast<_Float16 *>(lds);
+    for (int i = tid; i < 64 * 64; i += NT) {
+        const int o = i >> 6, k = i & 63;
+        split2h_store(P.w1v[o * 128 + 64 + k] * wsc, pimg + o * kPRow + k, kPImg);
+        split2h_store(P.w1c[o * 128 + 64 + k] * wsc, pimg + 2 * kPImg + o * kPRow + k, kPImg);
+    }
+#else
     for (int i = tid; i < 64 * 64; i += NT) {
         const int o = i >> 6, k = i & 63;
         lds[o * kPS + k] = P.w1v[o * 128 + 64 + k];
         lds[kPOffW1c + o * kPS + k] = P.w1c[o * 128 + 64 + k];
     }
+#endif
     if (tid < 64) {
         lds[kPOffB + tid] = P.b1v[tid];
         lds[kPOffB + 64 + tid] = P.b1c[tid];
@@ -660,6 +690,34 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         }
         }
         __builtin_amdgcn_wave_barrier();
+#if LDPC_PROJ_F16
+        // B operand of k-step s: lane (j, half) <- group j's units 16 s + 8 half .. + 7, scaled by a
+        // power of two (the group's largest |g| to at most 2^15); the accumulators are scaled back
+        float4 gv[8];
+        float gmx = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            gv[q] = *reinterpret_cast<const float4 *>(gm + j * kPS + 16 * (q >> 1) + 8 * half + 4 * (q & 1));
+            gmx = fmaxf(gmx, fmaxf(fmaxf(fabsf(gv[q].x), fabsf(gv[q].y)), fmaxf(fabsf(gv[q].z), fabsf(gv[q].w))));
+        }
+        __builtin_amdgcn_wave_barrier();
+        gmx = fmaxf(gmx, __shfl_xor(gmx, 32, 64));
+        const int gexp = col_exp(gmx);
+        const float gsc = pow2f(gexp), igsc = pow2f(-gexp - wexp);
+        const _Float16 *Wi = pimg + (md.x ? 2 * kPImg : 0) + j * kPRow + 8 * half;
+        f32x16 h0 = {}, h1 = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const float4 a = gv[2 * s], c = gv[2 * s + 1];
+            const float v[8] = {a.x * gsc, a.y * gsc, a.z * gsc, a.w * gsc, c.x * gsc, c.y * gsc, c.z * gsc, c.w * gsc};
+            f16x8_t b0, b1;
+            split2h(v, b0, b1);
+            h0 = mfma3h(Wi + 16 * s, b0, b1, h0, kPImg);
+            h1 = mfma3h(Wi + 32 * kPRow + 16 * s, b0, b1, h1, kPImg);
+        }
+        h0 *= igsc;
+        h1 *= igsc;
+#else
         // B operand: lane (j, half) <- group j's units 8 q + 4 half + i (q < 8)
         float g32[32];
 #pragma unroll
@@ -683,6 +741,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
                 h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b4[i], g32[kk + i], h1, 0, 0, 0);
             }
         }
+#endif
         const int g = T.grp[32 * t + j];
         if (g < 0) continue;
         const float *b1 = lds + kPOffB + 64 * md.x;
