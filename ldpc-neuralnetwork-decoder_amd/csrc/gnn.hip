@@ -477,7 +477,10 @@ constexpr int kPS = 68;
 #define LDPC_PROJ_F16 1
 #endif
 constexpr int kPRow = 72, kPImg = 64 * kPRow;
-constexpr int kPOffW1c = 64 * kPS, kPOffB = LDPC_PROJ_F16 ? 4 * kPImg / 2 : 2 * 64 * kPS, kPOffEmb = kPOffB + 4 * 64;
+constexpr int kPOffB = LDPC_PROJ_F16 ? 4 * kPImg / 2 : 2 * 64 * kPS, kPOffEmb = kPOffB + 4 * 64;
+#if !LDPC_PROJ_F16
+constexpr int kPOffW1c = 64 * kPS;
+#endif
 inline size_t proj_lds_bytes(int T, int waves) { return (size_t)(kPOffEmb + T * kPS + waves * 32 * kPS) * 4; }  // + 32 group means per wave
 
 struct ProjTiles {
