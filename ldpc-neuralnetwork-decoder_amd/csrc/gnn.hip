@@ -1660,6 +1660,33 @@ __global__ void gnn_output_csr_kernel(const float *__restrict__ msg_out, const i
     for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[mem[q]];
     probs[i] = 1.0f / (1.0f + expf(-(s + llr[i])));  // sigmoid(var_llrs + input_llr) (:298-307)
 }
+// The same sums with the frame's msg_out row staged in LDS (coalesced 16-B loads) when it fits: the
+// per-variable 4-B gathers above touch a cache line per message and re-fetch evicted lines (their
+// counter bytes were ~50x the row's).  One workgroup per frame, frames grid-strided; same order.
+constexpr int64_t kOutLdsMaxE = 16384;
+__global__ __launch_bounds__(256) void gnn_output_lds_kernel(const float *__restrict__ msg_out, const int32_t *__restrict__ ints,
+                                                             const float *__restrict__ llr, int64_t E, int N, int64_t B,
+                                                             const uint8_t *__restrict__ active, float *__restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) float mo[];
+    const int32_t *ptr = ints, *mem = ints + 2 * N + 2;
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        if (active && !active[b]) continue;  // uniform over the workgroup
+        __syncthreads();                     // the previous frame's reads are done
+        const float *src = msg_out + b * E;
+        if ((E & 3) == 0)
+            for (int64_t e = threadIdx.x; e < E / 4; e += 256)
+                reinterpret_cast<float4 *>(mo)[e] = reinterpret_cast<const float4 *>(src)[e];
+        else
+            for (int64_t e = threadIdx.x; e < E; e += 256) mo[e] = src[e];
+        __syncthreads();
+        for (int v = threadIdx.x; v < N; v += 256) {
+            float s = 0.0f;
+            for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[mem[q]];
+            const int64_t i = b * N + v;
+            probs[i] = 1.0f / (1.0f + expf(-(s + llr[i])));
+        }
+    }
+}
 
 
 __global__ void gnn_fill_kernel(int32_t *p, int64_t n, int32_t v) {
@@ -1909,6 +1936,18 @@ int ldpc::gnn_build_var_csr(const int32_t *d_msg_var, int64_t E, int N, int32_t 
 int ldpc::gnn_output(const float *d_msg_out, const int32_t *d_ints, const float *d_llr, int64_t E, int N, int64_t B,
                      const uint8_t *d_active, float *d_probs, hipStream_t s) {
     const int64_t n = B * N;
+    if (E <= kOutLdsMaxE && B > 0) {
+        if (g_num_cus == 0) {
+            int dev = 0;
+            LDPC_HIP(hipGetDevice(&dev));
+            LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        const unsigned grid = (unsigned)std::min<int64_t>(B, (int64_t)std::max(g_num_cus, 1) * 8);
+        hipLaunchKernelGGL(gnn_output_lds_kernel, dim3(grid), dim3(256), (size_t)E * 4, s, d_msg_out, d_ints, d_llr, E, N, B,
+                           d_active, d_probs);
+        LDPC_CHECK_LAUNCH("gnn_output_lds_kernel");
+        return LDPC_OK;
+    }
     hipLaunchKernelGGL(gnn_output_csr_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_msg_out, d_ints,
                        d_llr, E, N, n, d_active, d_probs);
     LDPC_CHECK_LAUNCH("gnn_output_csr_kernel");
