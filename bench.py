@@ -114,6 +114,11 @@ PMC_KERNEL_SYMBOL = {
     "minsum-z32": "_ZN4ldpc18flood_fixed_kernelINS_5fixed7BG2_Z32ELi0ELi0E",
     "bp-z32": "_ZN4ldpc18flood_fixed_kernelINS_5fixed7BG2_Z32ELi1ELi0E",
     "bp-z4": "_ZN4ldpc18flood_fixed_kernelINS_5fixed6BG2_Z4ELi1ELi0E",
+    # the dominant kernel's translation unit (its PMC summary also sums the small gnn.hip output pass)
+    "gnn-z32-bf16": "gnn_bf16_mlp_kernel",
+    "gnn-z32-bf16-i10": "gnn_bf16_mlp_kernel",
+    "gnn-z32-h128": "gnn_wide",
+    "lay-z32": "check_group",
 }
 
 
