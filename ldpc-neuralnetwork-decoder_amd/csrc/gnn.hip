@@ -1001,7 +1001,8 @@ inline size_t mlp2s_rw_lds_bytes(int T, bool d1, int waves) {
 // W1v [c; g] = (W1v_left + W1v_right) c -- one fp32 sum per weight, rounded once and split like the
 // other weights -- and GEMM1 starts from b1v instead of a projected row, which the projection
 // kernel then does not write for those groups (ProjTiles first = n_ptiles_v1).
-template <int NT, int WPS, bool HYB = false, bool RW = false>
+// PCL (row walk only): the units' check rows staged in LDS (LDPC_S6_PCLDS, when the LDS has room)
+template <int NT, int WPS, bool HYB = false, bool RW = false, bool PCL = false>
 __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     s6_t *img = reinterpret_cast<s6_t *>(lds);
@@ -1135,7 +1136,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 #if LDPC_S6_PCLDS
         // pcm (uniform): 0 = the check row from global, else from the lane's LDS slots, which the row
         // walk fills at the unit's first tile (float4 q of lane l at pcs[64 q + l]: conflict-free)
-        if (RW && pcm) {
+        if (PCL && pcm) {
             const float4 *pcs = reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(lds) + s6_off_pc(P.T)) + wave * 512 + lane;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1372,7 +1373,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             const int cg = cg0 + (okc ? j : 0);
             if (!P.x_in) load_x(x, b, m, b * P.E + m);  // layer 0: x from the LLR at the tile
 #if LDPC_S6_PCLDS
-            if (i == 0) {  // the unit's first tile: its 32 projected check rows into the lanes' LDS slots
+            if (PCL && i == 0) {  // the unit's first tile: its 32 projected check rows into the lanes' LDS slots
                 const float *pc = P.Mc + (b * P.Gc + cg) * 64 + 4 * half;
                 float4 *pcs = reinterpret_cast<float4 *>(reinterpret_cast<char *>(lds) + s6_off_pc(P.T)) + wave * 512 + lane;
                 float4 v[8];
@@ -1869,6 +1870,13 @@ bool rowwalk_path() {
     return !(e && std::atoi(e) == 0);
 }
 
+// LDPC_GNN_PCLDS=0 runs the row walk without its LDS-staged check rows (the kernel that codes with
+// too many message types for the staging get); default: staged when they fit.  Read per call.
+bool pclds_path() {
+    const char *e = std::getenv("LDPC_GNN_PCLDS");
+    return !(e && std::atoi(e) == 0);
+}
+
 // LDPC_GNN_PROJ=0 keeps the per-message [c; g] GEMM1 (gnn_mlp_mfma_kernel) for A/B runs
 bool proj_path() {
     static bool t = [] {
@@ -2325,10 +2333,12 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     // degree-1 message tiles first (gnn_mlp2s_kernel) when the combined image fits
     const bool d1t = split && p->n_mtiles_v1 > 0 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
     // row walk (gnn_mlp2s_kernel RW): check tile groups, per-check sums out of the MLP (w.S set by carve)
-    const bool rw = split && w.S && rowwalk_path() && mlp2s_rw_lds_bytes(types, true, kMlp2sNt / 64) <= 160 * 1024;
+    const bool rw = split && w.S && rowwalk_path();
     const bool rwd1 = rw && p->rw_d1 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
+    // the staged check rows need 8 KB per wave beside the images (types up to ~50 at 8 waves)
+    const bool pc_lds = rw && LDPC_S6_PCLDS && pclds_path() && mlp2s_rw_lds_bytes(types, true, kMlp2sNt / 64) <= 160 * 1024;
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
-                 mlp2_lds = split ? (rw ? mlp2s_rw_lds_bytes(types, rwd1, kMlp2sNt / 64) : mlp2s_lds_bytes(types, d1t))
+                 mlp2_lds = split ? (pc_lds ? mlp2s_rw_lds_bytes(types, rwd1, kMlp2sNt / 64) : mlp2s_lds_bytes(types, rw ? rwd1 : d1t))
                                   : mlp2_lds_bytes(types);
     const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                          : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
@@ -2340,7 +2350,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
-        LDPC_HIP(hipFuncSetAttribute(split ? (rw ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>)
+        LDPC_HIP(hipFuncSetAttribute(split ? (rw ? (pc_lds ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true, true>)
+                                                           : reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>))
                                                  : reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>))
                                            : reinterpret_cast<const void *>(gnn_mlp2_kernel<kMlp2Nt, kMlp2Wps>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp2_lds));
@@ -2443,11 +2454,13 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             const int64_t tiles = d1t ? nb * p->n_mtiles : (nb * p->E + 31) / 32;
             constexpr int wpb = kMlp2Nt / 64;
             const unsigned grid = (unsigned)std::min<int64_t>((tiles + wpb - 1) / wpb, (int64_t)g_num_cus * mlp2_per_cu);
-            if (rw)
-                hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>),
-                                   dim3((unsigned)std::min<int64_t>((nb * p->n_rw + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64),
-                                                                    (int64_t)g_num_cus)),
-                                   dim3(kMlp2sNt), mlp2_lds, st, L);
+            if (rw) {
+                const dim3 rgrid((unsigned)std::min<int64_t>((nb * p->n_rw + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus));
+                if (pc_lds)
+                    hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true, true>), rgrid, dim3(kMlp2sNt), mlp2_lds, st, L);
+                else
+                    hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>), rgrid, dim3(kMlp2sNt), mlp2_lds, st, L);
+            }
             else if (split)
                 hipLaunchKernelGGL((gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>),
                                    dim3((unsigned)std::min<int64_t>((tiles + kMlp2sNt / 64 - 1) / (kMlp2sNt / 64), (int64_t)g_num_cus)),

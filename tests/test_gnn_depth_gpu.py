@@ -77,6 +77,18 @@ def test_cfg4_depth_fp32_vs_oracle(cuda, oracle_mod, monkeypatch, split):
     assert np.array_equal(bits.cpu().numpy()[sure], (ref > 0.5)[sure].astype(np.float32))
 
 
+def test_rowwalk_staged_check_rows_bitwise(cuda, monkeypatch):
+    """The row walk reads each unit's projected check rows from LDS after the unit's first tile
+    (default) or from global memory at every tile (LDPC_GNN_PCLDS=0: the kernel that codes with too
+    many message types for the staging run): the same values, so the outputs are bit for bit equal."""
+    base, H, dec, conv, types = _model(10, cuda, seed=3)
+    llr = awgn_llr(512, H.shape[1], 1.0, seed=31, device=cuda)
+    p = _native(dec, conv, types, llr, cuda)
+    monkeypatch.setenv("LDPC_GNN_PCLDS", "0")
+    q = _native(dec, conv, types, llr, cuda)
+    assert torch.equal(p, q)
+
+
 def test_cfg4_full_batch_properties(cuda, oracle_mod):
     """cfg4's per-GPU batch (32768 frames, 10 layers): the (B, E, H) buffers pass 2^31 elements,
     the 48 GB workspace budget chunks the batch.  Chunked (4096) == default chunking, a sub-batch
