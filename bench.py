@@ -4,6 +4,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload minsum-z32|...]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+`--gpus N` without a launcher starts the N ranks itself (torch.distributed.run, before anything
+touches the GPU); under a launcher it must equal WORLD_SIZE, and with RCCL every rank needs its own
+GPU -- otherwise the run exits 2 instead of timing fewer GPUs than it reports
+(BENCH_DIST_BACKEND=gloo: the rehearsal with ranks sharing a card).
+
 One step = one decode pass over this rank's batch of synthetic frames that are already resident
 in HBM (all-zero codeword through the on-device QPSK/AWGN channel at a fixed SNR).  Frames shard
 across ranks (weak scaling, no collective on the data path); the BER/FER counters and the timing
@@ -159,6 +164,47 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (profiles/*_pmc.json) to report as roofline.traffic")
     return ap.parse_args()
+
+
+def resolve_launch(gpus, env, device_count):
+    """What `bench.py --gpus N` does, before anything touches the GPU:
+      ("run", None)    this process is the job (N = 1), or one rank of a launcher's job
+                       (WORLD_SIZE set, equal to N);
+      ("spawn", None)  N > 1 and no launcher: start N ranks under torch.distributed.run and exit with
+                       their status (the parent never initialises HIP);
+      ("error", msg)   a run that would misreport: --gpus differs from the launcher's WORLD_SIZE, or
+                       fewer GPUs are visible than ranks with RCCL.  BENCH_DIST_BACKEND=gloo is the
+                       explicit rehearsal of the multi-rank path with ranks sharing fewer cards."""
+    gloo = env.get("BENCH_DIST_BACKEND", "nccl") == "gloo"
+    world = env.get("WORLD_SIZE")
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: need at least one"
+    if world is None:
+        if gpus == 1:
+            return "run", None
+        if not gloo and device_count < gpus:
+            return "error", f"--gpus {gpus} but {device_count} GPU(s) visible (RCCL needs one per rank)"
+        return "spawn", None
+    if int(world) != gpus:
+        return "error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+    if not gloo and device_count < int(world):
+        return "error", f"WORLD_SIZE={world} but {device_count} GPU(s) visible (RCCL needs one per rank)"
+    return "run", None
+
+
+def spawn_ranks(gpus, argv):
+    """torch.distributed.run with one rank per GPU on this node, rendezvous on 127.0.0.1 at a free
+    port; returns its exit status.  The ranks inherit stdout: rank 0's JSON line is this run's."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, BENCH_LAUNCH="self", MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
 
 
 def setup_dist():
@@ -329,6 +375,14 @@ def cpu_baseline(workload, z, iters, target_s):
 
 def main():
     a = parse()
+    # torch.cuda.device_count() does not initialise the GPU on this image (a launcher parent may
+    # still spawn its ranks after it)
+    action, msg = resolve_launch(a.gpus, os.environ, torch.cuda.device_count())
+    if action == "error":
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if action == "spawn":
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
     world, rank, dev = setup_dist()
     kind, z, iters, bdef, snr = WORKLOADS[a.workload]
     snr = a.snr if a.snr is not None else snr
@@ -723,6 +777,12 @@ def main():
             "avg_iterations": itsum / max(fr, 1) if kind in ("minsum", "bp") else None,
             "cpu_baseline": cpu,
             "dist_backend": dist.get_backend() if dist.is_initialized() else None,
+            # the process group's own rank count (the GPUs that did the work) beside the launch
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "launch": ("bench.py --gpus (self-spawned ranks)" if os.environ.get("BENCH_LAUNCH") == "self"
+                       else "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process"),
+            # the last step's counters summed over ranks (bits / frames in error, frames counted)
+            "counters": {"bit_errors": be, "frame_errors": fe, "frames": fr, "iterations_sum": itsum},
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

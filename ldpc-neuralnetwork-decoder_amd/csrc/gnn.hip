@@ -397,8 +397,8 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_mlp_mfma_kernel(GnnLayer P
             // bias + ReLU; register r of row tile rt holds unit 32*rt + crow(r, half)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                h0[r] = fmaxf(h0[r] + b1[crow(r, half)], 0.0f);
-                h1[r] = fmaxf(h1[r] + b1[32 + crow(r, half)], 0.0f);
+                h0[r] = relu_nan(h0[r] + b1[crow(r, half)]);
+                h1[r] = relu_nan(h1[r] + b1[32 + crow(r, half)]);
             }
             // GEMM2^T: y[o][msg] += sum_u W2[o][u] * h[u][msg]; step (rt, r) pairs unit
             // crow(r,0) (half 0) with crow(r,1) (half 1) -- exactly the registers each lane holds
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         atomicMax(&wmax_bits, __float_as_int(m));
     }
     __syncthreads();
-    const int wexp = col_exp(__int_as_float(wmax_bits));
+    const int wexp = min(col_exp(__int_as_float(wmax_bits)), 126);
     const float wsc = pow2f(wexp);
     _Float16 *pimg = reinterpret_cast<_Float16 *>(lds);
     for (int i = tid; i < 64 * 64; i += NT) {
@@ -705,7 +705,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         }
         __builtin_amdgcn_wave_barrier();
         gmx = fmaxf(gmx, __shfl_xor(gmx, 32, 64));
-        const int gexp = col_exp(gmx);
+        const int gexp = col_exp_w(gmx, wexp);
         const float gsc = pow2f(gexp), igsc = pow2f(-gexp - wexp);
         const _Float16 *Wi = pimg + (md.x ? 2 * kPImg : 0) + j * kPRow + 8 * half;
         f32x16 h0 = {}, h1 = {};
@@ -859,8 +859,8 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                h0[r] = fmaxf(h0[r], 0.0f);
-                h1[r] = fmaxf(h1[r], 0.0f);
+                h0[r] = relu_nan(h0[r]);
+                h1[r] = relu_nan(h1[r]);
             }
 #pragma unroll
             for (int rq = 0; rq < 4; ++rq) {
@@ -913,9 +913,6 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2_kernel(GnnLayer P) {
     }
 }
 
-// ReLU as one integer max on the bits (a negative float, -0 included, is a negative int32): the
-// same value as fmaxf(v, 0) for every non-NaN v, without the canonicalising v_max fmaxf needs
-__device__ __forceinline__ float relu_i(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
 
 // ------------------------------------------------------------------------ MLP over projected groups, fp32 by split MFMAs
 // Default (LDPC_S6_F16, round 5): scaled two-term f16 splits.  The weights are scaled by one power of
@@ -1024,7 +1021,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
         atomicMax(&wmax_bits, __float_as_int(m));
     }
     __syncthreads();
-    const int wexp = col_exp(__int_as_float(wmax_bits));
+    const int wexp = min(col_exp(__int_as_float(wmax_bits)), 126);
     const float wsc = pow2f(wexp);
 #endif
     for (int i = tid; i < 64 * 64; i += NT) {
@@ -1167,7 +1164,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) cm = fmaxf(cm, fabsf(x[s][i]));
         cm = fmaxf(cm, __shfl_xor(cm, 32, 64)) + lds[kS6OffEmb + P.T * kPS + typ];  // >= max |c|
-        const int cexp = col_exp(cm);
+        const int cexp = col_exp_w(cm, wexp);
         const float csc = pow2f(cexp), asc = pow2f(cexp + wexp), iasc = pow2f(-cexp - wexp);
         hs[0][0] *= asc;
         hs[0][1] *= asc;
@@ -1246,7 +1243,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             for (int r = 0; r < 16; ++r) hm = fmaxf(hm, fmaxf(hs[side][0][r], hs[side][1][r]));
         }
         hm = fmaxf(hm, __shfl_xor(hm, 32, 64));  // >= 0: the largest relu(h)
-        const int hexp = col_exp(hm);
+        const int hexp = col_exp_w(hm, wexp);
         const float hsc = pow2f(hexp), ysc = pow2f(hexp + wexp), iysc = pow2f(-hexp - wexp);
         y0 *= ysc;
         y1 *= ysc;
@@ -1260,7 +1257,7 @@ __global__ __launch_bounds__(NT, WPS) void gnn_mlp2s_kernel(GnnLayer P) {
             for (int s = 0; s < 4; ++s) {  // GEMM2: y += W2 relu(h); k-step s = registers 8 (s&1) .. of h_{s>>1}
                 float hr[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) hr[i] = relu_i(s < 2 ? h0[8 * (s & 1) + i] : h1[8 * (s & 1) + i]);
+                for (int i = 0; i < 8; ++i) hr[i] = relu_nan(s < 2 ? h0[8 * (s & 1) + i] : h1[8 * (s & 1) + i]);
 #if LDPC_S6_F16
 #pragma unroll
                 for (int i = 0; i < 8; ++i) hr[i] *= hsc;
@@ -1474,7 +1471,7 @@ __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H)
             for (int o = lane; o < H; o += 64) {
                 float s = b1[o];
                 for (int k = 0; k < 2 * H; ++k) s += W1[o * 2 * H + k] * in[k];
-                in[2 * H + o] = fmaxf(s, 0.0f);
+                in[2 * H + o] = relu_nan(s);
             }
             __builtin_amdgcn_wave_barrier();
             for (int o = lane; o < H; o += 64) {
@@ -1505,7 +1502,10 @@ __global__ __launch_bounds__(256) void gnn_mlp_generic_kernel(GnnLayer P, int H)
 // each product is one fma.  (fp32 with fma chains in k order: within the fp32 bar of the reference,
 // not bit-identical to gnn_mlp_generic_kernel's mul-then-add.)  VALU, not MFMA: H = 64 is the
 // tuned width.
-constexpr int kTiledNM = 8, kTiledMaxH = 256;
+// Up to kTiledMaxH = 1024: one wave's rows are 128 H bytes of LDS (128 KB at H = 1024).  The training
+// backward (gnn_train.hip train_mlp_bwd_wide_kernel) recomputes these products in the same fma order,
+// so this is the training forward at every H != 64.
+constexpr int kTiledNM = 8, kTiledMaxH = 1024;
 inline int tiled_waves(int H) { return std::max(1, std::min(4, (64 * 1024) / (kTiledNM * 4 * H * 4))); }
 
 __global__ void gnn_wt_kernel(const float *__restrict__ w1v, const float *__restrict__ w2v,
@@ -1569,8 +1569,8 @@ __global__ __launch_bounds__(256) void gnn_mlp_tiled_kernel(GnnLayer P, int H) {
                     s[6] = fmaf(wk, x1.z, s[6]); s[7] = fmaf(wk, x1.w, s[7]);
                 }
                 float4 *h4 = reinterpret_cast<float4 *>(hh + o * NM);
-                h4[0] = make_float4(fmaxf(s[0], 0.0f), fmaxf(s[1], 0.0f), fmaxf(s[2], 0.0f), fmaxf(s[3], 0.0f));
-                h4[1] = make_float4(fmaxf(s[4], 0.0f), fmaxf(s[5], 0.0f), fmaxf(s[6], 0.0f), fmaxf(s[7], 0.0f));
+                h4[0] = make_float4(relu_nan(s[0]), relu_nan(s[1]), relu_nan(s[2]), relu_nan(s[3]));
+                h4[1] = make_float4(relu_nan(s[4]), relu_nan(s[5]), relu_nan(s[6]), relu_nan(s[7]));
             }
             __builtin_amdgcn_wave_barrier();
             for (int o = lane; o < H; o += 64) {
@@ -1732,12 +1732,14 @@ struct Ws {
     int64_t bytes;
 };
 
-Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precision, void *base) {
+// train: the training forward (d_saved), which never takes the wide path -- the backward
+// (gnn_train.hip) recomputes h and the ReLU masks with gnn_mlp_tiled_kernel's fma chains
+Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precision, void *base, bool train = false) {
     Ws w{};
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     const int64_t es = 4;  // bytes per stored feature (fp32 path)
     (void)precision;
-    const bool wide = wide_on(p, H);  // the last layer's rows are stored too (its head reads them)
+    const bool wide = wide_on(p, H) && !train;  // the last layer's rows are stored too (its head reads them)
     const int64_t xb = layers > 1 || wide ? al(B * p->E * H * es) : 0;
     const int64_t xb2 = layers > 2 || (wide && layers > 1) ? xb : 0;
     const int64_t mv = al(B * (int64_t)p->Gv * H * es), mc = al(B * (int64_t)p->Gc * H * es);
@@ -2225,19 +2227,47 @@ extern "C" int ldpc_gnn_plan_create_csr(int64_t E, const int32_t *h_v_ptr, const
     wts.insert(wts.end(), h_v_val, h_v_val + nv);
     wts.insert(wts.end(), h_c_val, h_c_val + nc);
     wts.push_back(0.0f);
+    // the transposes: a counting sort of the nonzeros by column, rows ascending within a column
+    std::vector<int32_t> tt;
+    std::vector<float> tw;
+    tt.reserve(2 * (E + 1) + nv + nc);
+    tw.reserve(nv + nc + 1);
+    auto transpose = [&](const int32_t *ptr, const int32_t *col, const float *val, int64_t nnz) {
+        const size_t p0 = tt.size();
+        tt.resize(p0 + E + 1, 0);
+        int32_t *tp = tt.data() + p0;
+        for (int64_t i = 0; i < nnz; ++i) tp[col[i] + 1]++;
+        for (int64_t j = 0; j < E; ++j) tp[j + 1] += tp[j];
+        std::vector<int32_t> cur(tp, tp + E), mem(nnz);
+        std::vector<float> w(nnz);
+        for (int64_t m = 0; m < E; ++m)
+            for (int32_t i = ptr[m]; i < ptr[m + 1]; ++i) {
+                const int32_t k = cur[col[i]]++;
+                mem[k] = (int32_t)m;
+                w[k] = val[i];
+            }
+        tt.insert(tt.end(), mem.begin(), mem.end());
+        tw.insert(tw.end(), w.begin(), w.end());
+    };
+    transpose(h_v_ptr, h_v_col, h_v_val, nv);
+    transpose(h_c_ptr, h_c_col, h_c_val, nc);
+    tw.push_back(0.0f);
     auto *p = new ldpc_gnn_plan();
     p->E = E;
     p->Gv = (int)E;
     p->Gc = (int)E;
     p->weighted = true;
     if (hipGetDevice(&p->device) != hipSuccess || hipMalloc(&p->d_tab, blob.size() * 4) != hipSuccess ||
-        hipMalloc(&p->d_inv, inv.size() * 4) != hipSuccess || hipMalloc(&p->d_w, wts.size() * 4) != hipSuccess) {
+        hipMalloc(&p->d_inv, inv.size() * 4) != hipSuccess || hipMalloc(&p->d_w, wts.size() * 4) != hipSuccess ||
+        hipMalloc(&p->d_tt, tt.size() * 4) != hipSuccess || hipMalloc(&p->d_tw, tw.size() * 4) != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan allocation failed");
     }
     if (hipMemcpy(p->d_tab, blob.data(), blob.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_inv, inv.data(), inv.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->d_w, wts.data(), wts.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(p->d_w, wts.data(), wts.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_tt, tt.data(), tt.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_tw, tw.data(), tw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         ldpc_gnn_plan_destroy(p);
         return fail(LDPC_EHIP, "GNN plan upload failed");
     }
@@ -2251,6 +2281,12 @@ extern "C" int ldpc_gnn_plan_create_csr(int64_t E, const int32_t *h_v_ptr, const
     p->inv_c = p->d_inv + E;
     p->vg_w = p->d_w;
     p->cg_w = p->d_w + nv;
+    p->vt_ptr = p->d_tt;
+    p->vt_mem = p->vt_ptr + E + 1;
+    p->ct_ptr = p->vt_mem + nv;
+    p->ct_mem = p->ct_ptr + E + 1;
+    p->vt_w = p->d_tw;
+    p->ct_w = p->d_tw + nv;
     *out = p;
     return LDPC_OK;
 }
@@ -2260,6 +2296,8 @@ extern "C" int ldpc_gnn_plan_destroy(ldpc_gnn_plan *p) {
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_inv) (void)hipFree(p->d_inv);
     if (p->d_w) (void)hipFree(p->d_w);
+    if (p->d_tt) (void)hipFree(p->d_tt);
+    if (p->d_tw) (void)hipFree(p->d_tw);
     if (p->d_gt) (void)hipFree(p->d_gt);
     if (p->d_pt) (void)hipFree(p->d_pt);
     if (p->d_ct) (void)hipFree(p->d_ct);
@@ -2280,8 +2318,13 @@ extern "C" int64_t ldpc_gnn_workspace_size(const ldpc_gnn_plan *p, int hidden, i
     return carve(p, hidden, N, B, layers, precision, nullptr).bytes;
 }
 
+int64_t ldpc::gnn_fp32_train_workspace(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers) {
+    return carve(p, hidden, N, B, layers, 0, nullptr, true).bytes;
+}
+
+// the forward writes the area only on its projected-group path (the same predicate as its `proj`)
 int64_t ldpc::gnn_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int layers) {
-    if (hidden != kMfmaH || p->weighted || p->n_ptiles <= 0) return 0;
+    if (hidden != kMfmaH || p->weighted || p->n_ptiles <= 0 || !proj_path()) return 0;
     return (int64_t)layers * B * (p->Gv + p->Gc) * 2 * hidden;
 }
 
@@ -2290,7 +2333,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
                            float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s,
                            float *d_proj) {
     const int H = hidden;
-    Ws w = carve(p, H, N, B, layers, 0, d_work);
+    const bool train = d_saved != nullptr;
+    Ws w = carve(p, H, N, B, layers, 0, d_work, train);
     if (!d_work || work_bytes < w.bytes)
         return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(w.bytes) + " bytes");
     if (!g_num_cus) {
@@ -2316,7 +2360,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     L.Mv = w.Mv; L.Mc = w.Mc;
     L.vside = 1;
     const bool mfma = H == kMfmaH;
-    const bool wide = wide_on(p, H);
+    const bool wide = wide_on(p, H) && !train;
     if (!mfma && H > kMaxGenericH) return fail(LDPC_EUNSUPPORTED, "hidden_dim must be <= " + std::to_string(kMaxGenericH));
     const size_t mfma_lds = (size_t)(kOffEmb + types * kEmbStride) * 4;
     if (mfma && mfma_lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the LDS image");
@@ -2494,7 +2538,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
                 T.wt = w.wt + 6LL * H * H * l;
                 const int tw = tiled_waves(H);
                 const int64_t want = (nb * p->E + (int64_t)tw * kTiledNM - 1) / ((int64_t)tw * kTiledNM);
-                const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)g_num_cus * 16 / tw);
+                const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)std::max(1, g_num_cus * 16 / tw));
+                const size_t tl = (size_t)tw * kTiledNM * 4 * H * 4;
+                if (tl > 64 * 1024)
+                    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp_tiled_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
                 hipLaunchKernelGGL(gnn_mlp_tiled_kernel, dim3(grid), dim3(64 * tw), (size_t)tw * kTiledNM * 4 * H * 4, st,
                                    T, H);
                 LDPC_CHECK_LAUNCH("gnn_mlp_tiled_kernel");

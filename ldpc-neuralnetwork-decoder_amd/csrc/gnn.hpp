@@ -17,6 +17,12 @@ struct ldpc_gnn_plan {
     bool weighted = false;
     float *d_w = nullptr;
     const float *vg_w = nullptr, *cg_w = nullptr;
+    // ... and the transposes (training backward: dc += A^T d(aggregated)), column j's nonzero rows
+    // ascending with their weights: vt_ptr[E+1] vt_mem vt_w, ct_ptr[E+1] ct_mem ct_w
+    int32_t *d_tt = nullptr;
+    float *d_tw = nullptr;
+    const int32_t *vt_ptr = nullptr, *vt_mem = nullptr, *ct_ptr = nullptr, *ct_mem = nullptr;
+    const float *vt_w = nullptr, *ct_w = nullptr;
     // bf16 path: "group tiles" of 8 groups of one degree each (var groups first, then check
     // groups, each side sorted by degree), so one wave sums 8 groups with no divergence.
     //   gt_meta[t] = {degree, offset into gt_mem}, gt_grp[8 t + q] = group id (check groups
@@ -89,6 +95,8 @@ int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, 
                      float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s,
                      float *d_proj = nullptr);
 int64_t gnn_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int layers);
+// workspace of the training forward (gnn_fp32_forward with d_saved: never the wide path)
+int64_t gnn_fp32_train_workspace(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers);
 
 // Layer `layer`'s projected group rows W1_s,right g + b1_s (d_pv / d_pc, (B, G, 64)) and, when
 // d_gv is set, the group means g themselves (d_gv / d_gc) of c = x + emb (x = d_x, or the LLR
@@ -200,6 +208,10 @@ __device__ __forceinline__ void split2h_store(float w, _Float16 *d, int stride) 
     d[0] = h0;
     d[stride] = (_Float16)(w - (float)h0);
 }
+// ReLU as torch.relu computes it (message_gnn_decoder.py:36-46): max(v, 0) for numbers, a NaN stays
+// NaN.  One v_maximum3_f32 on gfx950 (IEEE 754-2019 maximum), the cost of the fmaxf / integer max it
+// replaced, which both map a NaN to 0 (a NaN feature would then vanish from its frame mid-graph)
+__device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.0f); }
 // 2^e as a float (e clamped to the normal range)
 __device__ __forceinline__ float pow2f(int e) { return __int_as_float((min(max(e, -126), 127) + 127) << 23); }
 // the exponent that scales a column whose largest magnitude is m (>= 0) to at most 2^15 (0: m is
@@ -208,6 +220,11 @@ __device__ __forceinline__ int col_exp(float m) {
     const int b = (__float_as_int(m) >> 23) & 0xff;
     return b == 0 || b == 255 ? 0 : 141 - b;  // 14 - (b - 127)
 }
+// ... for an activation column multiplied by weights scaled 2^wexp: clamped so that the product scale
+// 2^(e + wexp) and its inverse stay normal floats, so csc * wsc, asc and iasc invert each other
+// exactly.  The upper clamp only lowers the column's scale (its split stays in range);
+// the lower one binds only where the fp32 products themselves overflow.
+__device__ __forceinline__ int col_exp_w(float m, int wexp) { return min(max(col_exp(m), -126 - wexp), 126 - wexp); }
 // acc += A B over one K = 16 step: A's two split images at img and img + img_stride
 __device__ __forceinline__ f32x16_t mfma3h(const _Float16 *img, const f16x8_t &b0, const f16x8_t &b1, f32x16_t acc,
                                            int img_stride) {

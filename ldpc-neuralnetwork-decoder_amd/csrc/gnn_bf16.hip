@@ -248,17 +248,18 @@ __device__ __forceinline__ f32x16 ld16(const float *p) {
     }
     return v;
 }
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-// ReLU of 8 accumulators as bf16: round first, then max(., 0) on the bf16 bit patterns as int16
-// (v_pk_max_i16, two values per instruction): a negative bf16 -- -0 included -- is a negative
-// int16, a positive one keeps its bits.  Same values as rounding max(x, 0.0f) (rounding keeps the
-// sign), without the per-value canonicalize + max pair fmaxf costs on an MFMA result.
+// ReLU of 8 accumulators as bf16 (torch.relu semantics: a NaN stays NaN): round first, then
+// v_pk_maximum3_f16 with 0 on the bf16 bit patterns viewed as f16 -- two values per instruction.
+// The view keeps the sign bit, so a negative bf16 (-0 included) is a negative f16 and becomes +0, a
+// positive one keeps its bits, and every pattern a bf16 NaN / inf / |v| >= 2^121 has is an f16 NaN,
+// which maximum returns with its payload (tools/ubench/relu_bf16.hip checks all 65536 patterns).
+typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ bf16x8 relu8(const f32x16 &a, int half) {
     bf16x8 o;
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (__bf16)a[8 * half + i];
-    s16x8 b = __builtin_bit_cast(s16x8, o);
-    b = __builtin_elementwise_max(b, (s16x8)0);
+    f16x8v b = __builtin_bit_cast(f16x8v, o);
+    b = __builtin_elementwise_maximum(b, (f16x8v)0);
     return __builtin_bit_cast(bf16x8, b);
 }
 __device__ __forceinline__ bf16x8 pack8(const f32x16 &a, int half) {

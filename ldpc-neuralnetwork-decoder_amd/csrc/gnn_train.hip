@@ -41,10 +41,10 @@ namespace ldpc {
 namespace {
 
 constexpr int kMaxH = 64;         // widest H of the LDS-image kernels (train_mlp_bwd_kernel, train_outer_kernel)
-// widest H trained: the forward runs gnn_mlp_tiled_kernel (fma chains) up to 256, the products the wide
-// backward recomputes; past 256 the forward's generic kernel rounds mul + add, so hv and the ReLU masks
-// the backward rebuilt could differ from the forward's in the last bit
-constexpr int kMaxTrainH = 256;
+// widest H trained: the training forward runs gnn_mlp_tiled_kernel (fma chains in k order) at every
+// H != 64 up to 1024 -- never the wide MFMA path (gnn.hip carve(train)) -- and the wide backward
+// recomputes exactly those products, so hv and the ReLU masks it rebuilds are the forward's bit for bit
+constexpr int kMaxTrainH = 1024;
 
 struct TW {  // one layer's weights in the blob (see ldpc_amd.h)
     const float *emb, *w1v, *b1v, *w2v, *b2v, *w1c, *b1c, *w2c, *b2c, *wo, *bo;
@@ -115,6 +115,7 @@ struct GmT {
     int src_mode, G, H, N;
     int sum_only = 0;  // 1: plain group sums (inv ignored)
     int64_t E, B;
+    const float *w = nullptr;  // weighted plan: member weights (s += w c, gnn_group_mean_kernel's expression)
 };
 
 __device__ __forceinline__ float c_value(const GmT &A, int64_t b, int64_t m, int u) {
@@ -132,7 +133,12 @@ __global__ __launch_bounds__(256) void train_group_mean_kernel(GmT A) {
     const int g = (int)(w - b * A.G);
     for (int u = threadIdx.x & 63; u < A.H; u += 64) {
         float s = 0.0f;
-        for (int q = A.ptr[g]; q < A.ptr[g + 1]; ++q) s += c_value(A, b, A.mem[q], u);
+        for (int q = A.ptr[g]; q < A.ptr[g + 1]; ++q) {
+            if (A.w)
+                s += A.w[q] * c_value(A, b, A.mem[q], u);
+            else
+                s += c_value(A, b, A.mem[q], u);
+        }
         A.dst[w * A.H + u] = A.sum_only ? s : s * A.inv[g];
     }
 }
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256) void train_group_mean_h64_kernel(GmT A) {
 
 int launch_group_mean(const GmT &g, hipStream_t s) {
     const int64_t n = g.B * g.G;
-    if (g.H == 64)
+    if (g.H == 64 && !g.w)
         hipLaunchKernelGGL(train_group_mean_h64_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, g);
     else
         hipLaunchKernelGGL(train_group_mean_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, g);
@@ -298,8 +304,8 @@ __global__ __launch_bounds__(256) void train_mlp_bwd_kernel(MlpT A) {
                 dh[(i * 2) * H + u] = dv;
                 dh[(i * 2 + 1) * H + u] = dc;
                 if (r < A.R) {
-                    A.hv[r * H + u] = fmaxf(uv[i], 0.0f);
-                    A.hc[r * H + u] = fmaxf(uc[i], 0.0f);
+                    A.hv[r * H + u] = relu_nan(uv[i]);
+                    A.hc[r * H + u] = relu_nan(uc[i]);
                     A.dhv[r * H + u] = dv;
                     A.dhc[r * H + u] = dc;
                 }
@@ -417,8 +423,8 @@ __global__ __launch_bounds__(256) void train_mlp_bwd_wide_kernel(MlpT A) {
                 dh[(i * 2) * H + u] = dv;
                 dh[(i * 2 + 1) * H + u] = dc;
                 if (r < A.R) {
-                    A.hv[r * H + u] = fmaxf(uv[i], 0.0f);
-                    A.hc[r * H + u] = fmaxf(uc[i], 0.0f);
+                    A.hv[r * H + u] = relu_nan(uv[i]);
+                    A.hc[r * H + u] = relu_nan(uc[i]);
                     A.dhv[r * H + u] = dv;
                     A.dhc[r * H + u] = dc;
                 }
@@ -642,8 +648,8 @@ __global__ __launch_bounds__(NT, NT / 256 > 1 ? NT / 256 : 1) void train_mlp_bwd
             for (int r = 0; r < 16; ++r) {
                 const float a0 = PJ ? u0[r] : u0[r] + bs[crow_t(r, half)];
                 const float a1 = PJ ? u1[r] : u1[r] + bs[32 + crow_t(r, half)];
-                u0[r] = fmaxf(a0, 0.0f);
-                u1[r] = fmaxf(a1, 0.0f);
+                u0[r] = relu_nan(a0);
+                u1[r] = relu_nan(a1);
                 d0[r] = a0 > 0.0f ? d0[r] : 0.0f;
                 d1[r] = a1 > 0.0f ? d1[r] : 0.0f;
             }
@@ -835,7 +841,7 @@ __global__ __launch_bounds__(512, 1) void train_mlp_bwd_s6_kernel(MlpT A) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float a = u[side][rt][r];
-                    u[side][rt][r] = fmaxf(a, 0.0f);
+                    u[side][rt][r] = relu_nan(a);
                     d[side][rt][r] = a > 0.0f ? d[side][rt][r] : 0.0f;
                 }
                 if (ok)
@@ -1630,7 +1636,15 @@ int launch_vecfinal(const VecT &v0, const float *S0, const float *S1, hipStream_
     const int nblk = (int)((v0.E + kChunkV - 1) / kChunkV);
     const dim3 g2((unsigned)nblk);
     const size_t lds = vecfinal_lds(v0.T, v0.H);
-    if (lds > 64 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the embedding gradient");
+    if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the embedding gradient");
+    if (lds > 64 * 1024) {
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_vecfinal_kernel<0>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_vecfinal_kernel<1>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_vecfinal_kernel<2>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
     const int n = v0.mode == 0 ? v0.T * v0.H : 2 * v0.H;
     VecT v = v0;
     if ((int64_t)nblk * n > v.part_cap) v.part = nullptr;
@@ -1654,10 +1668,7 @@ int launch_vecfinal(const VecT &v0, const float *S0, const float *S1, hipStream_
 int launch_vec(const VecT &v, float *S0, float *S1, hipStream_t s) {
     const int64_t EH = v.E * v.H;
     const dim3 g1((unsigned)((EH + 255) / 256)), g2((unsigned)((v.E + kChunkV - 1) / kChunkV));
-    const size_t lds = vecfinal_lds(v.T, v.H);
-    if (lds > 64 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the embedding gradient");
     (void)g2;
-    (void)lds;
     if (v.mode == 0)
         hipLaunchKernelGGL(train_colsum_kernel<0>, g1, dim3(256), 0, s, v, S0, S1);
     else if (v.mode == 1)
@@ -1758,8 +1769,8 @@ using namespace ldpc;
 
 extern "C" int64_t ldpc_gnn_train_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers) {
     if (!p || hidden <= 0 || hidden > kMaxTrainH || N <= 0 || B < 0 || layers <= 0)
-        return fail(LDPC_EINVAL, "bad arguments (training needs hidden_dim <= 256)");
-    const int64_t fwd = ldpc_gnn_workspace_size(p, hidden, N, B, layers, 0);
+        return fail(LDPC_EINVAL, "bad arguments (training needs hidden_dim <= 1024)");
+    const int64_t fwd = gnn_fp32_train_workspace(p, hidden, N, B, layers);
     const int64_t bwd = carve_train(p, hidden, N, B, nullptr).bytes;
     return fwd > bwd ? fwd : bwd;
 }
@@ -1782,9 +1793,8 @@ extern "C" int ldpc_gnn_forward_train_ex(const ldpc_gnn_plan *p, int hidden, int
                                          const float *d_llr, int N, int64_t B, float *d_probs, float *d_saved,
                                          float *d_proj, void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
-    if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     if (hidden <= 0 || hidden > kMaxTrainH || types <= 0 || layers <= 0 || N <= 0 || B < 0)
-        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 256)");
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 1024)");
     if (B == 0) return LDPC_OK;
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_saved)
         return fail(LDPC_EINVAL, "NULL tensor");
@@ -1811,10 +1821,9 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
                                        const float *d_layer_probs, const float *d_grad_layer_probs,
                                        float *d_grad_weights, void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
-    if (p->weighted) return fail(LDPC_EUNSUPPORTED, "training needs a group plan (clique adjacencies)");
     const int H = hidden, T = types, L = layers;
     if (H <= 0 || H > kMaxTrainH || T <= 0 || L <= 0 || N <= 0 || B < 0)
-        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 256)");
+        return fail(LDPC_EINVAL, "bad dimensions (training needs hidden_dim <= 1024)");
     if (!d_weights || !d_msg_type || !d_msg_var || !d_llr || !d_probs || !d_grad_probs || !d_saved || !d_grad_weights)
         return fail(LDPC_EINVAL, "NULL tensor");
     if ((d_layer_probs == nullptr) != (d_grad_layer_probs == nullptr))
@@ -1961,9 +1970,9 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
             g.src = x; g.emb = W[0]; g.llr = d_llr; g.w_in = d_weights; g.b_in = d_weights + H;
             g.msg_type = d_msg_type; g.msg_var = d_msg_var;
             g.src_mode = x ? 1 : 2; g.H = H; g.N = N; g.E = E; g.B = B;
-            g.ptr = p->vg_ptr; g.mem = p->vg_mem; g.inv = p->inv_v; g.G = p->Gv; g.dst = w.Mv;
+            g.ptr = p->vg_ptr; g.mem = p->vg_mem; g.inv = p->inv_v; g.G = p->Gv; g.dst = w.Mv; g.w = p->vg_w;
             if (int rc = launch_group_mean(g, s)) return rc;
-            g.ptr = p->cg_ptr; g.mem = p->cg_mem; g.inv = p->inv_c; g.G = p->Gc; g.dst = w.Mc;
+            g.ptr = p->cg_ptr; g.mem = p->cg_mem; g.inv = p->inv_c; g.G = p->Gc; g.dst = w.Mc; g.w = p->cg_w;
             if (int rc = launch_group_mean(g, s)) return rc;
         }
         // MLP backward
@@ -2017,12 +2026,15 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
                                p->inv_c, p->Gv, p->Gc, B, w.Mda, w.Mdb);
             LDPC_CHECK_LAUNCH("train_group_back_kernel");
         } else {
-            // group means of the aggregated-input gradients (the mean operator is symmetric)
+            // group means of the aggregated-input gradients (the mean operator is symmetric); a
+            // general adjacency A (weighted plan): A^T of them, over the plan's transposed CSR
             GmT d{};
             d.src_mode = 0; d.H = H; d.N = N; d.E = E; d.B = B;
             d.src = w.da; d.ptr = p->vg_ptr; d.mem = p->vg_mem; d.inv = p->inv_v; d.G = p->Gv; d.dst = w.Mda;
+            if (p->weighted) { d.ptr = p->vt_ptr; d.mem = p->vt_mem; d.w = p->vt_w; }
             if (int rc = launch_group_mean(d, s)) return rc;
             d.src = w.db; d.ptr = p->cg_ptr; d.mem = p->cg_mem; d.inv = p->inv_c; d.G = p->Gc; d.dst = w.Mdb;
+            if (p->weighted) { d.ptr = p->ct_ptr; d.mem = p->ct_mem; d.w = p->ct_w; }
             if (int rc = launch_group_mean(d, s)) return rc;
         }
         if (pj) {
@@ -2078,7 +2090,7 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
                 c.out = gw; c.bias = gb;
                 if (int rc = launch_outer(c, red_grid, s)) return rc;
             }
-            if (!pj) {
+            if (!pj && !p->weighted) {  // weighted: every message reads its own aggregated row
                 GmT gs{};
                 gs.src = dh; gs.src_mode = 0; gs.sum_only = 1; gs.H = H; gs.N = N; gs.E = E; gs.B = B;
                 gs.ptr = side ? p->cg_ptr : p->vg_ptr; gs.mem = side ? p->cg_mem : p->vg_mem;
@@ -2086,7 +2098,7 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
                 if (int rc = launch_group_mean(gs, s)) return rc;
             }
             OuterT g{};
-            g.H = H; g.E = (int64_t)Gn; g.R = B * Gn; g.A = dhsum; g.zsrc = Gs; g.J = H; g.ld = 2 * H; g.col0 = H;
+            g.H = H; g.E = (int64_t)Gn; g.R = B * Gn; g.A = p->weighted ? dh : dhsum; g.zsrc = Gs; g.J = H; g.ld = 2 * H; g.col0 = H;
             g.out = gw; g.bias = nullptr;
             const unsigned ggrid = (unsigned)std::min<int64_t>((g.R + 63) / 64, (int64_t)g_cus_t * kOuterWgs);
             if (int rc = launch_outer(g, ggrid, s)) return rc;

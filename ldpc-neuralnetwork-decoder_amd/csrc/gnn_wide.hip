@@ -77,15 +77,16 @@ __device__ __forceinline__ void split3w(const float *v, bf16x8_t &a, bf16x8_t &b
     }
 }
 
-// ReLU as one integer max on the bits (gnn.hip relu_i)
-__device__ __forceinline__ float relu_w(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
 
 // NT accumulator tiles of 32 output units per wave; 512 threads (8 waves) per workgroup, one or two
 // workgroups per CU by the LDS image
 constexpr int kWThreads = 512, kWWaves = kWThreads / 64;
-constexpr int kWAhead = 4;  // input k-steps in flight ahead of the one being multiplied
-template <int NT>
+// AH: input k-steps in flight ahead of the one being multiplied.  The ring slot of chunk s is s % AH
+// on every tile, so AH must divide the k-step count: 4 when it does (K = 64 k), else 2 (K = 32 k,
+// the odd multiples of 32: H = 96, 160, 224 in the projection and GEMM1)
+template <int NT, int AH>
 __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int nslices) {
+    constexpr int kWAhead = AH;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
     constexpr int NS = 32 * NT;
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
     // chunk s + kWAhead -- of this tile, or of the next one near the end -- is in flight
     float ring[kWAhead][8];
 #pragma unroll
-    for (int a = 0; a < kWAhead; ++a) chunk(cur, a, ring[a]);  // K >= 96: ksteps >= kWAhead
+    for (int a = 0; a < kWAhead; ++a) chunk(cur, a, ring[a]);  // K >= 96: ksteps >= kWAhead, ksteps % kWAhead == 0
     const __bf16 *wl = img + j * rowb + 8 * h;
     while (cur.live) {
         const Ctx nxt = ctx_of(cur.t + stride);
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     float4 o = make_float4(acc[tt][4 * q], acc[tt][4 * q + 1], acc[tt][4 * q + 2], acc[tt][4 * q + 3]);
-                    if (A.mode == kGemm1) o = make_float4(relu_w(o.x), relu_w(o.y), relu_w(o.z), relu_w(o.w));
+                    if (A.mode == kGemm1) o = make_float4(relu_nan(o.x), relu_nan(o.y), relu_nan(o.z), relu_nan(o.w));
                     *reinterpret_cast<float4 *>(op + 32 * tt + 8 * q) = o;
                 }
         }
@@ -301,6 +302,14 @@ __global__ __launch_bounds__(256) void gnn_wide_head_kernel(const float *__restr
 
 int g_wcus = 0;
 
+template <int NT, int AH>
+int go_wgemm(const WArgs &a, int nslices, dim3 grid, size_t lds, hipStream_t s) {
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_wgemm_kernel<NT, AH>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((gnn_wgemm_kernel<NT, AH>), grid, dim3(kWThreads), lds, s, a, nslices);
+    return LDPC_OK;
+}
+
 int launch_wgemm(WArgs a, hipStream_t s) {
     if (!g_wcus) {
         int dev = 0;
@@ -323,16 +332,14 @@ int launch_wgemm(WArgs a, hipStream_t s) {
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
     // blocks per XCD: a multiple of the slice count, about per_cu workgroups per CU
     const int per_x = std::max(nslices, (g_wcus / 8) * per_cu / nslices * nslices);
-    const void *fn = a.NS == 128 ? reinterpret_cast<const void *>(gnn_wgemm_kernel<4>)
-                     : a.NS == 64 ? reinterpret_cast<const void *>(gnn_wgemm_kernel<2>)
-                                  : reinterpret_cast<const void *>(gnn_wgemm_kernel<1>);
-    LDPC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (a.NS == 128)
-        hipLaunchKernelGGL(gnn_wgemm_kernel<4>, dim3(8 * per_x), dim3(kWThreads), lds, s, a, nslices);
-    else if (a.NS == 64)
-        hipLaunchKernelGGL(gnn_wgemm_kernel<2>, dim3(8 * per_x), dim3(kWThreads), lds, s, a, nslices);
-    else
-        hipLaunchKernelGGL(gnn_wgemm_kernel<1>, dim3(8 * per_x), dim3(kWThreads), lds, s, a, nslices);
+    if ((a.K / 16) % 2) return fail(LDPC_EUNSUPPORTED, "row GEMM reduction length must be a multiple of 32");
+    const bool ah4 = (a.K / 16) % 4 == 0;
+    const dim3 grid(8 * per_x);
+    int rc;
+    if (a.NS == 128) rc = ah4 ? go_wgemm<4, 4>(a, nslices, grid, lds, s) : go_wgemm<4, 2>(a, nslices, grid, lds, s);
+    else if (a.NS == 64) rc = ah4 ? go_wgemm<2, 4>(a, nslices, grid, lds, s) : go_wgemm<2, 2>(a, nslices, grid, lds, s);
+    else rc = ah4 ? go_wgemm<1, 4>(a, nslices, grid, lds, s) : go_wgemm<1, 2>(a, nslices, grid, lds, s);
+    if (rc) return rc;
     LDPC_CHECK_LAUNCH("gnn_wgemm_kernel");
     return LDPC_OK;
 }

@@ -3,8 +3,11 @@
 Same classes, constructor arguments, parameter names (so the same state_dict keys and
 saved_models checkpoints) and forward/decode signatures as the reference; the forward pass
 runs in libldpc_amd (csrc/gnn.hip): segment-mean aggregation instead of the dense E x E
-normalized-adjacency bmm, the four message MLPs on fp32 MFMA (bf16 optional), and the
-input embedding, residuals, output projection, per-variable sum and sigmoid fused around them.
+normalized-adjacency bmm, the four message MLPs on the matrix cores, and the input embedding,
+residuals, output projection, per-variable sum and sigmoid fused around them.  fp32 contract:
+H = 64 runs each fp32 product as a scaled two-term f16 split (three v_mfma_f32_32x32x16_f16
+products, fp32 accumulate; <= 2x an fp32 GEMM's error against float64), other widths as bf16x6
+splits (H = 96..256) or fp32 fma chains; precision="bf16" is bf16 features and bf16 MFMA.
 
 Compatibility notes (each mirrors the reference line cited):
   * a 2-D ``message_to_var_mapping`` uses its column 0 as the variable index (:220-226, :287-292),
@@ -16,7 +19,8 @@ Compatibility notes (each mirrors the reference line cited):
     reference, :93).  A mis-sized pair is zero-padded / cropped as :92-104 does.  The
     normalized cliques TannerToMessageGraph builds (:410-469) are recognised (groups read off the
     matrix once, verified by probing A @ r == group-mean(r)) and aggregated as group means; any
-    other matrix runs as a general sparse bmm(A, c) over its nonzeros (fp32 forward only).
+    other matrix runs as a general sparse bmm(A, c) over its nonzeros (fp32 only; trainable: the
+    backward applies A^T over the plan's transposed CSR).
   * the unused ``output_layer`` (:188) is kept so state_dicts round-trip.
   * with grad enabled and trainable parameters, forward() runs the fp32 training path (every
     layer's features saved for the HIP backward, csrc/gnn_train.hip); otherwise the inference
@@ -305,9 +309,6 @@ class MessageGNNDecoder(nn.Module):
             # training: fp32 forward that saves every layer's features + the HIP backward
             # (precision="bf16" is an inference setting: it always takes the no-grad path)
             plan = self._plan(vg, cg, dev)
-            if plan.weighted:
-                raise NotImplementedError("training through a general (non-clique) adjacency is not supported; "
-                                          "use the TannerToMessageGraph adjacencies")
             probs, _ = _NativeGnnTrain.apply(self, llr, io_map, types, plan, False, *params)
         else:
             with torch.no_grad():
@@ -326,8 +327,8 @@ class MessageGNNDecoder(nn.Module):
         decoder's output stage; the last entry is forward()'s probs.  A loss on all of them (deep
         supervision) trains the intermediate layers to decode, which is what lets the bf16 path's
         per-frame early termination (cfg5) stop before the last layer -- its syndrome check reads
-        exactly these decisions.  fp32, group (clique) adjacencies, with autograd through the HIP
-        backward (ldpc_gnn_backward_ds)."""
+        exactly these decisions.  fp32, any adjacency, with autograd through the HIP backward
+        (ldpc_gnn_backward_ds)."""
         dev = N.device_of(input_llr)
         E = self.num_messages
         vg, cg = _aggregation_specs(var_to_check_adjacency, check_to_var_adjacency, E)
@@ -336,8 +337,6 @@ class MessageGNNDecoder(nn.Module):
         T = self.gnn_layers[0].message_type_embeddings.shape[0]
         types = _types_for(message_types, E, T, dev)
         plan = self._plan(vg, cg, dev)
-        if plan.weighted:
-            raise NotImplementedError("forward_all_layers needs the TannerToMessageGraph adjacencies")
         if self.precision != "fp32":
             raise NotImplementedError("forward_all_layers runs the fp32 training forward")
         probs, layer_probs = _NativeGnnTrain.apply(self, llr, io_map, types, plan, True, *self._blob_params())
@@ -371,9 +370,9 @@ class _NativeGnnTrain(torch.autograd.Function):
         dev = llr.device
         H, L = dec.hidden_dim, len(dec.gnn_layers)
         T = dec.gnn_layers[0].message_type_embeddings.shape[0]
-        if H > 256:
-            raise NotImplementedError("the native backward supports hidden_dim <= 256 (the widths whose forward "
-                                      "products it recomputes bit for bit)")
+        if H > 1024:
+            raise NotImplementedError("the native backward supports hidden_dim <= 1024 (the widths of the tiled "
+                                      "training forward, whose products it recomputes bit for bit)")
         B, Nv = llr.shape
         E = dec.num_messages
         blob = torch.cat([p.detach().reshape(-1).to(dev, torch.float32) for p in params]).contiguous()

@@ -162,3 +162,49 @@ def test_cfg4_fp32_checkpoint_vs_oracle(cuda, oracle_mod):
     ber = float(((p > 0.5) != bits.bool()).double().mean())
     print(f"cfg4 trained checkpoint, 4096 codewords at 2 dB: BER {ber:.2e}")
     assert ber < 1e-3
+
+
+def _strata(B, chunk, E, H, extra=16, seed=5):
+    """Frames where the fp32 forward's indexing changes regime: the first and last frame of every
+    chunk (LDPC_GNN_WORKSPACE_BYTES), of every frame half (the two streams of gnn_fp32_forward), and
+    either side of the frames whose (B, E, H) offsets cross 2^29 / 2^30 / 2^31 elements within a
+    half, plus `extra` random frames."""
+    picks = set()
+    for s in range(0, B, chunk):
+        n = min(chunk, B - s)
+        halves = [(s, n)] if n < 128 else [(s, n // 2), (s + n // 2, n - n // 2)]
+        for h0, hn in halves:
+            picks.update({h0, h0 + 1, h0 + hn - 2, h0 + hn - 1})
+            for k in (29, 30, 31):
+                f = (1 << k) // (E * H)
+                picks.update({h0 + f - 1, h0 + f, h0 + f + 1} if f + 1 < hn else set())
+    rng = np.random.default_rng(seed)
+    picks.update(rng.integers(0, B, extra).tolist())
+    return sorted(p for p in picks if 0 <= p < B)
+
+
+def test_cfg4_full_batch_stratified_vs_oracle(cuda, oracle_mod):
+    """cfg4 at its full per-GPU batch (32768 frames, 10 layers, the trained checkpoint, random
+    codewords at 0 dB: decoding errors present) against the oracle on >= 64 frames chosen where the
+    indexing changes regime (_strata), at the fp32 bar (|dp| <= 2e-5)."""
+    from ldpc_neural_decoder import _native as N
+    H, dec, conv, types = _load(10, cuda, "fp32")
+    bits, llr = _codewords(H, CFG_BATCH, 0.0, 6060, cuda)
+    p = _native(dec, conv, types, llr, cuda)
+    assert bool(torch.isfinite(p).all())
+    # the chunk native_forward used (the same budget arithmetic)
+    plan = dec._plan(conv.var_groups, conv.check_groups, cuda)
+    ws = lambda b: N.check(N.lib().ldpc_gnn_workspace_size(plan.handle, 64, H.shape[1], b, 10, 0))
+    budget = int(os.environ.get("LDPC_GNN_WORKSPACE_BYTES", 48 << 30))
+    chunk = max(1, min(CFG_BATCH, (budget - ws(1)) // max(ws(2) - ws(1), 1)))
+    E = len(conv.messages)
+    pick = _strata(CFG_BATCH, chunk, E, 64)
+    assert len(pick) >= 64, (len(pick), chunk)
+    idx = torch.tensor(pick, device=cuda)
+    ref = _oracle_layers(oracle_mod, dec, conv, H, types, llr[idx])[-1]
+    got = p[idx].cpu().numpy()
+    err = np.abs(got - ref).max(axis=1)
+    print(f"cfg4 stratified: chunk {chunk}, {len(pick)} frames, max |dp| {err.max():.2e}, "
+          f"BER {float(((p > 0.5) != bits.bool()).double().mean()):.2e}")
+    bad = [(f, float(e)) for f, e in zip(pick, err) if e > 2e-5]
+    assert not bad, bad[:8]

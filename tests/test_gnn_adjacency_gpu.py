@@ -75,7 +75,5 @@ def test_general_adjacency_refusals(cuda):
         with torch.no_grad():
             dec(*args)
     dec.precision = "fp32"
-    with pytest.raises(NotImplementedError):  # training needs the clique adjacencies
-        dec(*args)
     with pytest.raises(AttributeError):
         dec(llr.to(cuda), conv.message_to_var_index(), None, None, None)

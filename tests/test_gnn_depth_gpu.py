@@ -58,7 +58,7 @@ def _native(dec, conv, types, llr, cuda, chunk=None):
 def test_cfg4_depth_fp32_vs_oracle(cuda, oracle_mod, monkeypatch, split):
     """10-layer fp32 forward at Z=32, H=64 through native_forward, forward() under no_grad and
     decode() (which must take the inference path even with grad enabled).  split: the MLP's fp32
-    products as three-term bf16 splits on the bf16 MFMA (default) or on the fp32 MFMA
+    products as scaled two-term f16 splits on the f16 MFMA (default) or on the fp32 MFMA
     (LDPC_GNN_SPLIT=0); same bar."""
     monkeypatch.setenv("LDPC_GNN_SPLIT", split)
     base, H, dec, conv, types = _model(10, cuda)
@@ -177,3 +177,17 @@ def test_wide_hidden_mfma_vs_oracle(cuda, oracle_mod, hidden, layers):
     assert err <= TOL, err
     sub = _native(dec, conv, types, llr[2:5].contiguous(), cuda).cpu().numpy()
     assert np.array_equal(sub, got[2:5])
+
+
+@pytest.mark.parametrize("hidden", [96, 160, 224])
+def test_wide_hidden_multi_tile_walk(cuda, oracle_mod, hidden):
+    """H = 96 / 160 / 224: the projection's and GEMM1's reduction (K = H) has a k-step count that 4
+    does not divide, so gnn_wgemm_kernel's input ring runs 2 deep there (a 4-deep ring
+    fed the next tile permuted chunks).  B = 48 frames at Z=32 give every wave several tiles to walk;
+    the oracle checks every frame at the H = 64 bar."""
+    base, H, dec, conv, types = _model(2, cuda, seed=hidden + 1, hidden=hidden)
+    llr = awgn_llr(48, H.shape[1], 1.0, seed=hidden + 2, device=cuda)
+    got = _native(dec, conv, types, llr, cuda).cpu().numpy()
+    ref = _oracle(oracle_mod, dec, conv, H, types, llr)
+    err = float(np.abs(got - ref).max())
+    assert err <= TOL, err

@@ -2,8 +2,10 @@
 
 Tolerance (floating point, stated): |probs - ref| <= 2e-5 absolute for the fp32 path.  The
 reference aggregates with a dense normalized-adjacency bmm and MKL GEMMs, this build with
-segment means and fp32 MFMA (exact fp32 products, different summation order), so results agree
-to float32 rounding, not bitwise."""
+segment means and the matrix cores: at H = 64 every fp32 product runs as a scaled two-term f16
+split (22 significant bits per operand, three f16 MFMA products, fp32 accumulate; within 2x an
+fp32 GEMM's error against float64, tests/test_gnn_depth_gpu.py::test_split_mlp_is_fp32_accurate),
+in a different summation order, so results agree to float32 rounding, not bitwise."""
 import numpy as np
 import pytest
 import torch
