@@ -150,12 +150,15 @@ int ldpc_count_errors(const void *d_bits, int bits_dtype, const uint8_t *d_ref, 
  * d_msg_type (E,) int32 already padded/truncated/clamped to [0,T) (the Python layer does
  *   :68-81).  d_msg_var (E,) int32 message -> variable for the LLR gather and the output sum
  *   (the reference's message_to_var_mapping, or its column-0 quirk: :218-229 / :285-295).
- * precision: 0 = float32 features, fp32 MFMA; 1 = bf16 MLP operands, fp32 accumulate.
+ * precision: 0 = float32 features and fp32-accurate products (H = 64: scaled two-term f16 splits on
+ *   the f16 MFMA, each weight matrix group under one power-of-two scale; other widths: bf16x6 splits
+ *   or fp32 fma chains); 1 = bf16 MLP operands, fp32 accumulate.
  * d_probs (B, N) float32 = sigmoid(llr + sum of each variable's projected messages).
  * d_work: at least ldpc_gnn_workspace_size(plan, H, N, B, precision) bytes. */
 typedef struct ldpc_gnn_plan ldpc_gnn_plan;
 /* ldpc_gnn_forward_ex flags */
 #define LDPC_GNN_EARLY_STOP 1 /* cfg5 per-frame early termination (bf16 path; see below) */
+#define LDPC_GNN_FP32_PRODUCTS 2 /* fp32 path, H = 64: every product on the fp32 MFMA (see below) */
 int ldpc_gnn_plan_create(int64_t E, int n_vgroups, const int32_t *h_vgroup, int n_cgroups,
                          const int32_t *h_cgroup, ldpc_gnn_plan **out);
 /* General adjacencies: the reference runs a dense bmm with whatever (E x E) matrices it is given
@@ -191,13 +194,17 @@ int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
  * BASELINE cfg5): after every layer but the last, each frame still decoding takes the hard
  * decision [llr + sum of the LAST layer's output_projection over its messages > 0] on its current
  * features; a frame whose decision satisfies every parity check stops there, gets its probs from
- * that decision's soft values and d_iters = layers used; the others run on. */
+ * that decision's soft values and d_iters = layers used; the others run on.
+ * LDPC_GNN_FP32_PRODUCTS (precision 0): the products of W1_right g and of the MLP run on the fp32 MFMA
+ * instead of as f16 splits.  The splits hold 22 bits of every weight whose row's largest |w| is at least
+ * 2^-17 of its matrix group's; a caller whose weights span more (MessageGNNDecoder checks this per
+ * weight version) sets the flag to keep fp32 accuracy. */
 int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                         const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
                         const float *d_llr, int N, int64_t B, int precision, int flags, float *d_probs,
                         int32_t *d_iters, void *d_work, int64_t work_bytes, void *stream);
 
-/* ---- training (fp32, hidden_dim <= 256) ------------------------------------------------------
+/* ---- training (fp32, hidden_dim <= 1024, any plan) ---------------------------------------------
  * Replaces torch autograd through MessageGNNDecoder.forward + F.binary_cross_entropy
  * (message_gnn_decoder.py:190-317, :314), as driven by trainer.py:70-102 (zero_grad, forward,
  * loss.backward(), SGD step).

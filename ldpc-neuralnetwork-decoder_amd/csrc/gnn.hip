@@ -469,18 +469,15 @@ __global__ __launch_bounds__(kMlpThreads, 2) void gnn_mlp_mfma_kernel(GnnLayer P
 // against W1_right (LDS) and + b1.  Rows go to Mv / Mc (same shape as the group means).
 // LDS (floats): W1vR [64][68], W1cR [64][68], b1v, b1c, w_in, b_in [64 each], emb [T][68].
 constexpr int kPS = 68;
-// LDPC_PROJ_F16 (default): W1_right g as scaled two-term f16 splits on v_mfma_f32_32x32x16_f16 (as
-// the MLP's products, gnn_mlp2s_kernel): 24 MFMAs of 32 cycles per tile instead of 64 fp32 MFMAs of
-// 64 cycles (+2.6 % on gnn-z32, profiles/r05/ab_r05pf16).  The images are W1vR (hi, lo), W1cR (hi,
-// lo), rows of kPRow halves (16-B aligned, padded).
-#ifndef LDPC_PROJ_F16
-#define LDPC_PROJ_F16 1
-#endif
+// F16 (default): W1_right g as scaled two-term f16 splits on v_mfma_f32_32x32x16_f16 (as the MLP's
+// products, gnn_mlp2s_kernel): 24 MFMAs of 32 cycles per tile instead of 64 fp32 MFMAs of 64 cycles
+// (+2.6 % on gnn-z32, profiles/r05/ab_r05pf16).  The images are W1vR (hi, lo), W1cR (hi, lo), rows of
+// kPRow halves (16-B aligned, padded).  !F16 (weights whose rows span more than the split's range,
+// LDPC_GNN_FP32_PRODUCTS): the fp32 images W1vR [64][68], W1cR [64][68] in the same region.
 constexpr int kPRow = 72, kPImg = 64 * kPRow;
-constexpr int kPOffB = LDPC_PROJ_F16 ? 4 * kPImg / 2 : 2 * 64 * kPS, kPOffEmb = kPOffB + 4 * 64;
-#if !LDPC_PROJ_F16
+constexpr int kPOffB = 4 * kPImg / 2, kPOffEmb = kPOffB + 4 * 64;
 constexpr int kPOffW1c = 64 * kPS;
-#endif
+static_assert(2 * 64 * kPS <= kPOffB, "the fp32 images fit the f16 images' region");
 inline size_t proj_lds_bytes(int T, int waves) { return (size_t)(kPOffEmb + T * kPS + waves * 32 * kPS) * 4; }  // + 32 group means per wave
 
 struct ProjTiles {
@@ -490,37 +487,38 @@ struct ProjTiles {
     int first;  // tiles before `first` are skipped (the var-side tiles, for the check side alone)
 };
 
-template <int NT, bool HYB = false>
+template <int NT, bool HYB = false, bool F16 = true>
 __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group_proj_kernel(GnnLayer P, ProjTiles T) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
-#if LDPC_PROJ_F16
-    // one power-of-two scale for both images: the largest |w| to at most 2^15
     __shared__ int wmax_bits;
-    if (tid == 0) wmax_bits = 0;
-    __syncthreads();
-    {
-        float m = 0.0f;
-        for (int i = tid; i < 64 * 64; i += NT)
-            m = fmaxf(m, fmaxf(fabsf(P.w1v[(i >> 6) * 128 + 64 + (i & 63)]), fabsf(P.w1c[(i >> 6) * 128 + 64 + (i & 63)])));
-        atomicMax(&wmax_bits, __float_as_int(m));
-    }
-    __syncthreads();
-    const int wexp = min(col_exp(__int_as_float(wmax_bits)), 126);
-    const float wsc = pow2f(wexp);
+    int wexp = 0;
     _Float16 *pimg = reinterpret_cast<_Float16 *>(lds);
-    for (int i = tid; i < 64 * 64; i += NT) {
-        const int o = i >> 6, k = i & 63;
-        split2h_store(P.w1v[o * 128 + 64 + k] * wsc, pimg + o * kPRow + k, kPImg);
-        split2h_store(P.w1c[o * 128 + 64 + k] * wsc, pimg + 2 * kPImg + o * kPRow + k, kPImg);
+    if constexpr (F16) {
+        // one power-of-two scale for both images: the largest |w| to at most 2^15
+        if (tid == 0) wmax_bits = 0;
+        __syncthreads();
+        {
+            float m = 0.0f;
+            for (int i = tid; i < 64 * 64; i += NT)
+                m = fmaxf(m, fmaxf(fabsf(P.w1v[(i >> 6) * 128 + 64 + (i & 63)]), fabsf(P.w1c[(i >> 6) * 128 + 64 + (i & 63)])));
+            atomicMax(&wmax_bits, __float_as_int(m));
+        }
+        __syncthreads();
+        wexp = min(col_exp(__int_as_float(wmax_bits)), 126);
+        const float wsc = pow2f(wexp);
+        for (int i = tid; i < 64 * 64; i += NT) {
+            const int o = i >> 6, k = i & 63;
+            split2h_store(P.w1v[o * 128 + 64 + k] * wsc, pimg + o * kPRow + k, kPImg);
+            split2h_store(P.w1c[o * 128 + 64 + k] * wsc, pimg + 2 * kPImg + o * kPRow + k, kPImg);
+        }
+    } else {
+        for (int i = tid; i < 64 * 64; i += NT) {
+            const int o = i >> 6, k = i & 63;
+            lds[o * kPS + k] = P.w1v[o * 128 + 64 + k];
+            lds[kPOffW1c + o * kPS + k] = P.w1c[o * 128 + 64 + k];
+        }
     }
-#else
-    for (int i = tid; i < 64 * 64; i += NT) {
-        const int o = i >> 6, k = i & 63;
-        lds[o * kPS + k] = P.w1v[o * 128 + 64 + k];
-        lds[kPOffW1c + o * kPS + k] = P.w1c[o * 128 + 64 + k];
-    }
-#endif
     if (tid < 64) {
         lds[kPOffB + tid] = P.b1v[tid];
         lds[kPOffB + 64 + tid] = P.b1c[tid];
@@ -693,7 +691,8 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         }
         }
         __builtin_amdgcn_wave_barrier();
-#if LDPC_PROJ_F16
+        f32x16 h0 = {}, h1 = {};
+        if constexpr (F16) {
         // B operand of k-step s: lane (j, half) <- group j's units 16 s + 8 half .. + 7, scaled by a
         // power of two (the group's largest |g| to at most 2^15); the accumulators are scaled back
         float4 gv[8];
@@ -708,7 +707,6 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         const int gexp = col_exp_w(gmx, wexp);
         const float gsc = pow2f(gexp), igsc = pow2f(-gexp - wexp);
         const _Float16 *Wi = pimg + (md.x ? 2 * kPImg : 0) + j * kPRow + 8 * half;
-        f32x16 h0 = {}, h1 = {};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const float4 a = gv[2 * s], c = gv[2 * s + 1];
@@ -720,7 +718,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         }
         h0 *= igsc;
         h1 *= igsc;
-#else
+        } else {
         // B operand: lane (j, half) <- group j's units 8 q + 4 half + i (q < 8)
         float g32[32];
 #pragma unroll
@@ -732,7 +730,6 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
         const float *W = lds + (md.x ? kPOffW1c : 0);
         int wl = j * kPS + 4 * half;  // step kk + i pairs unit 8 (kk/4) + i (half 0) with + 4 (half 1)
         asm volatile("" : "+v"(wl));
-        f32x16 h0 = {}, h1 = {};
 #pragma unroll
         for (int kk = 0; kk < 32; kk += 4) {
             const float4 wa = *reinterpret_cast<const float4 *>(W + wl + 2 * kk);
@@ -744,7 +741,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
                 h1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b4[i], g32[kk + i], h1, 0, 0, 0);
             }
         }
-#endif
+        }
         const int g = T.grp[32 * t + j];
         if (g < 0) continue;
         const float *b1 = lds + kPOffB + 64 * md.x;
@@ -1647,23 +1644,35 @@ __global__ void csr_sort_kernel(const int32_t *__restrict__ ptr, int N, int32_t 
         mem[j + 1] = x;
     }
 }
-__global__ void gnn_output_csr_kernel(const float *__restrict__ msg_out, const int32_t *__restrict__ ints,
-                                      const float *__restrict__ llr, int64_t E, int N, int64_t n,
-                                      const uint8_t *__restrict__ active, float *__restrict__ probs) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t b = i / N;
-    const int v = (int)(i - b * N);
-    if (active && !active[b]) return;
+// A frame whose LLRs or projected messages hold an inf or NaN decodes to NaN everywhere: the
+// reference aggregates with a dense bmm (message_gnn_decoder.py:108, :118), where 0 * inf = 0 * NaN
+// = NaN reaches every message of the frame in the first layer that carries one (an inf LLR already
+// in layer 0; in this build's segment means only the group's neighbours would see it).  A
+// non-finite feature stays non-finite through the residual to the last layer's messages, so the
+// frame's LLR row and its msg_out row decide.  One workgroup per frame, frames grid-strided.
+__device__ __forceinline__ bool nonfinite(float v) { return (__float_as_uint(v) & 0x7f800000u) == 0x7f800000u; }
+
+__global__ __launch_bounds__(256) void gnn_output_csr_kernel(const float *__restrict__ msg_out, const int32_t *__restrict__ ints,
+                                                             const float *__restrict__ llr, int64_t E, int N, int64_t B,
+                                                             const uint8_t *__restrict__ active, float *__restrict__ probs) {
     const int32_t *ptr = ints, *mem = ints + 2 * N + 2;
-    const float *mo = msg_out + b * E;
-    float s = 0.0f;  // var_llrs[var] += decoded_llrs[b, msg] in ascending msg (:277-296)
-    for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[mem[q]];
-    probs[i] = 1.0f / (1.0f + expf(-(s + llr[i])));  // sigmoid(var_llrs + input_llr) (:298-307)
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        if (active && !active[b]) continue;  // uniform over the workgroup
+        const float *mo = msg_out + b * E, *lr = llr + b * N;
+        bool bad = false;
+        for (int64_t e = threadIdx.x; e < E; e += 256) bad |= nonfinite(mo[e]);
+        for (int v = threadIdx.x; v < N; v += 256) bad |= nonfinite(lr[v]);
+        bad = __syncthreads_or(bad);
+        for (int v = threadIdx.x; v < N; v += 256) {
+            float s = 0.0f;  // var_llrs[var] += decoded_llrs[b, msg] in ascending msg (:277-296)
+            for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[mem[q]];
+            probs[b * N + v] = bad ? __int_as_float(0x7fc00000) : 1.0f / (1.0f + expf(-(s + lr[v])));  // (:298-307)
+        }
+    }
 }
 // The same sums with the frame's msg_out row staged in LDS (coalesced 16-B loads) when it fits: the
 // per-variable 4-B gathers above touch a cache line per message and re-fetch evicted lines (their
-// counter bytes were ~50x the row's).  One workgroup per frame, frames grid-strided; same order.
+// counter bytes were ~50x the row's).  Same order.
 constexpr int64_t kOutLdsMaxE = 16384;
 __global__ __launch_bounds__(256) void gnn_output_lds_kernel(const float *__restrict__ msg_out, const int32_t *__restrict__ ints,
                                                              const float *__restrict__ llr, int64_t E, int N, int64_t B,
@@ -1674,17 +1683,25 @@ __global__ __launch_bounds__(256) void gnn_output_lds_kernel(const float *__rest
         if (active && !active[b]) continue;  // uniform over the workgroup
         __syncthreads();                     // the previous frame's reads are done
         const float *src = msg_out + b * E;
+        bool bad = false;
         if ((E & 3) == 0)
-            for (int64_t e = threadIdx.x; e < E / 4; e += 256)
-                reinterpret_cast<float4 *>(mo)[e] = reinterpret_cast<const float4 *>(src)[e];
+            for (int64_t e = threadIdx.x; e < E / 4; e += 256) {
+                const float4 v = reinterpret_cast<const float4 *>(src)[e];
+                bad = bad || nonfinite(v.x) || nonfinite(v.y) || nonfinite(v.z) || nonfinite(v.w);
+                reinterpret_cast<float4 *>(mo)[e] = v;
+            }
         else
-            for (int64_t e = threadIdx.x; e < E; e += 256) mo[e] = src[e];
-        __syncthreads();
+            for (int64_t e = threadIdx.x; e < E; e += 256) {
+                mo[e] = src[e];
+                bad |= nonfinite(mo[e]);
+            }
+        for (int v = threadIdx.x; v < N; v += 256) bad |= nonfinite(llr[b * N + v]);
+        bad = __syncthreads_or(bad);
         for (int v = threadIdx.x; v < N; v += 256) {
             float s = 0.0f;
             for (int q = ptr[v]; q < ptr[v + 1]; ++q) s += mo[mem[q]];
             const int64_t i = b * N + v;
-            probs[i] = 1.0f / (1.0f + expf(-(s + llr[i])));
+            probs[i] = bad ? __int_as_float(0x7fc00000) : 1.0f / (1.0f + expf(-(s + llr[i])));
         }
     }
 }
@@ -1958,8 +1975,14 @@ int ldpc::gnn_output(const float *d_msg_out, const int32_t *d_ints, const float 
         LDPC_CHECK_LAUNCH("gnn_output_lds_kernel");
         return LDPC_OK;
     }
-    hipLaunchKernelGGL(gnn_output_csr_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_msg_out, d_ints,
-                       d_llr, E, N, n, d_active, d_probs);
+    if (g_num_cus == 0) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    (void)n;
+    hipLaunchKernelGGL(gnn_output_csr_kernel, dim3((unsigned)std::min<int64_t>(B, (int64_t)std::max(g_num_cus, 1) * 8)), dim3(256),
+                       0, s, d_msg_out, d_ints, d_llr, E, N, B, d_active, d_probs);
     LDPC_CHECK_LAUNCH("gnn_output_csr_kernel");
     return LDPC_OK;
 }
@@ -2331,7 +2354,7 @@ int64_t ldpc::gnn_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int
 int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
                            const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
                            float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s,
-                           float *d_proj) {
+                           float *d_proj, bool fp32_products) {
     const int H = hidden;
     const bool train = d_saved != nullptr;
     Ws w = carve(p, H, N, B, layers, 0, d_work, train);
@@ -2373,7 +2396,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     // projection workgroups of 12 waves (one LDS weight image for 12 waves' gathers) when the
     // type table leaves room, else 4
     const int proj_nt = LDPC_PROJ_NT != 256 && proj_lds_bytes(types, LDPC_PROJ_NT / 64) <= 160 * 1024 ? LDPC_PROJ_NT : 256;
-    const bool split = split_path() && mlp2s_lds_bytes(types, false) <= 160 * 1024;
+    const bool split = !fp32_products && split_path() && mlp2s_lds_bytes(types, false) <= 160 * 1024;
     // degree-1 message tiles first (gnn_mlp2s_kernel) when the combined image fits
     const bool d1t = split && p->n_mtiles_v1 > 0 && mlp2s_lds_bytes(types, true) <= 160 * 1024 && d1_skip();
     // row walk (gnn_mlp2s_kernel RW): check tile groups, per-check sums out of the MLP (w.S set by carve)
@@ -2384,8 +2407,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     const size_t proj_lds = proj_lds_bytes(types, proj_nt / 64),
                  mlp2_lds = split ? (pc_lds ? mlp2s_rw_lds_bytes(types, rwd1, kMlp2sNt / 64) : mlp2s_lds_bytes(types, rw ? rwd1 : d1t))
                                   : mlp2_lds_bytes(types);
-    const void *proj_fn = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
-                                         : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>);
+    const void *proj_fn = fp32_products
+                              ? (proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT, false, false>)
+                                                : reinterpret_cast<const void *>(gnn_group_proj_kernel<256, false, false>))
+                              : (proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
+                                                : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>));
     int mlp2_per_cu = 1, proj_per_cu = 1;
     if (proj) {
         if (mlp2_lds > 160 * 1024 || proj_lds > 160 * 1024)
@@ -2490,7 +2516,11 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;
             const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
-            if (proj_nt != 256)
+            if (fp32_products && proj_nt != 256)
+                hipLaunchKernelGGL((gnn_group_proj_kernel<LDPC_PROJ_NT, false, false>), dim3(pgrid), dim3(LDPC_PROJ_NT), proj_lds, st, L, T);
+            else if (fp32_products)
+                hipLaunchKernelGGL((gnn_group_proj_kernel<256, false, false>), dim3(pgrid), dim3(256), proj_lds, st, L, T);
+            else if (proj_nt != 256)
                 hipLaunchKernelGGL(gnn_group_proj_kernel<LDPC_PROJ_NT>, dim3(pgrid), dim3(LDPC_PROJ_NT), proj_lds, st, L, T);
             else
                 hipLaunchKernelGGL(gnn_group_proj_kernel<256>, dim3(pgrid), dim3(256), proj_lds, st, L, T);
@@ -2650,7 +2680,7 @@ extern "C" int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types
     if (hidden <= 0 || types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
     if (precision != 0 && precision != 1) return fail(LDPC_EINVAL, "precision must be 0 (fp32) or 1 (bf16)");
     if (precision == 1 && hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "bf16 path needs hidden_dim 64");
-    if (flags & ~LDPC_GNN_EARLY_STOP) return fail(LDPC_EINVAL, "unknown flags");
+    if (flags & ~(LDPC_GNN_EARLY_STOP | LDPC_GNN_FP32_PRODUCTS)) return fail(LDPC_EINVAL, "unknown flags");
     if ((flags & LDPC_GNN_EARLY_STOP) && precision != 1)
         return fail(LDPC_EUNSUPPORTED, "early termination is implemented on the bf16 path (precision 1)");
     if (B == 0) return LDPC_OK;
@@ -2666,7 +2696,7 @@ extern "C" int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types
         LDPC_CHECK_LAUNCH("gnn_fill_kernel");
     }
     return gnn_fp32_forward(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
-                            nullptr, d_work, work_bytes, s);
+                            nullptr, d_work, work_bytes, s, nullptr, (flags & LDPC_GNN_FP32_PRODUCTS) != 0);
 }
 
 extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,

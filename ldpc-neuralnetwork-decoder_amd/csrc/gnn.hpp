@@ -93,7 +93,7 @@ __device__ __forceinline__ const int32_t *csr_mem(const int32_t *ints, int N) { 
 int gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers, const float *d_weights,
                      const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
                      float *d_probs, float *d_saved, void *d_work, int64_t work_bytes, hipStream_t s,
-                     float *d_proj = nullptr);
+                     float *d_proj = nullptr, bool fp32_products = false);
 int64_t gnn_proj_floats(const ldpc_gnn_plan *p, int hidden, int64_t B, int layers);
 // workspace of the training forward (gnn_fp32_forward with d_saved: never the wide path)
 int64_t gnn_fp32_train_workspace(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers);

@@ -248,19 +248,16 @@ __device__ __forceinline__ f32x16 ld16(const float *p) {
     }
     return v;
 }
-// ReLU of 8 accumulators as bf16 (torch.relu semantics: a NaN stays NaN): round first, then
-// v_pk_maximum3_f16 with 0 on the bf16 bit patterns viewed as f16 -- two values per instruction.
-// The view keeps the sign bit, so a negative bf16 (-0 included) is a negative f16 and becomes +0, a
-// positive one keeps its bits, and every pattern a bf16 NaN / inf / |v| >= 2^121 has is an f16 NaN,
-// which maximum returns with its payload (tools/ubench/relu_bf16.hip checks all 65536 patterns).
-typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+// ReLU of 8 accumulators as bf16 (torch.relu semantics: a NaN stays NaN): v_maximum3_f32 with 0
+// (IEEE maximum), then round.  The integer max on the bf16 bits this replaced (v_pk_max_i16, half the
+// instructions) mapped a negative-signed NaN to 0; max on the bits viewed as f16 (v_pk_maximum3_f16)
+// keeps -inf and quiets f16-signalling patterns (1407 of the 65536 bf16 patterns wrong,
+// tools/ubench/relu_bf16.hip).
 __device__ __forceinline__ bf16x8 relu8(const f32x16 &a, int half) {
     bf16x8 o;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (__bf16)a[8 * half + i];
-    f16x8v b = __builtin_bit_cast(f16x8v, o);
-    b = __builtin_elementwise_maximum(b, (f16x8v)0);
-    return __builtin_bit_cast(bf16x8, b);
+    for (int i = 0; i < 8; ++i) o[i] = (__bf16)relu_nan(a[8 * half + i]);
+    return o;
 }
 __device__ __forceinline__ bf16x8 pack8(const f32x16 &a, int half) {
     bf16x8 o;
@@ -673,6 +670,8 @@ __global__ __launch_bounds__(256) void gnn_bf16_syndrome_kernel(const float *__r
         const float zv = zsum(mo, lr, v);
         if constexpr (ZS) zs[v] = zv;
         if (zv > 0.0f) atomicOr(&bits[v >> 5], 1u << (v & 31));
+        if ((__float_as_uint(zv) & 0x7f800000u) == 0x7f800000u) odd = 1;  // inf / NaN: never a decision;
+        // the frame runs on to gnn_output, which makes all of it NaN (the reference's dense bmm)
     }
     __syncthreads();
     for (int g = threadIdx.x; g < Gc; g += blockDim.x) {

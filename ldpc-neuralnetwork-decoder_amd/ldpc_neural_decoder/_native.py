@@ -17,6 +17,7 @@ LDPC_ALGO_MINSUM, LDPC_ALGO_BP = 0, 1
 LDPC_ES_OFF, LDPC_ES_BATCH, LDPC_ES_FRAME = 0, 1, 2
 LDPC_OUT_U8, LDPC_OUT_F32 = 0, 1
 LDPC_GNN_EARLY_STOP = 1
+LDPC_GNN_FP32_PRODUCTS = 2
 LDPC_EINVAL, LDPC_EHIP, LDPC_EUNSUPPORTED, LDPC_ENOMEM = -1, -2, -3, -4
 
 _P = ctypes.c_void_p

@@ -214,6 +214,7 @@ class MessageGNNDecoder(nn.Module):
         self._plans = {}
         self._blob_key = None
         self._blob = None
+        self._split_ok = True
 
     # -------------------------------------------------------------- native plumbing
     def _blob_params(self):
@@ -240,7 +241,33 @@ class MessageGNNDecoder(nn.Module):
             want = N.check(N.lib().ldpc_gnn_weights_size(self.hidden_dim, T, len(self.gnn_layers)))
             assert blob.numel() == want, (blob.numel(), want)
             self._blob, self._blob_key = blob, key
+            self._split_ok = self._split_range_ok()
         return self._blob
+
+    SPLIT_RANGE = 2.0 ** -17
+
+    def _split_range_ok(self):
+        """Whether the H = 64 fp32 kernels' f16 splits hold every weight row to fp32 accuracy: each
+        weight group shares one power-of-two scale (the projection: W1v / W1c right halves; the MLP:
+        the left halves, W2v, W2c and W1v_left + W1v_right), and a row keeps 22 bits while its largest
+        |w| is >= 2^-17 of its group's.  Checked once per weight version; otherwise the forward runs
+        the products on the fp32 MFMA (LDPC_GNN_FP32_PRODUCTS)."""
+        H = self.hidden_dim
+        if H != 64:
+            return True
+        with torch.no_grad():
+            for layer in self.gnn_layers:
+                v, c = layer.var_to_check_update, layer.check_to_var_update
+                w1v, w1c = v[0].weight.detach().float(), c[0].weight.detach().float()
+                groups = ((w1v[:, H:], w1c[:, H:]),
+                          (w1v[:, :H], w1c[:, :H], v[2].weight.detach().float(), c[2].weight.detach().float(),
+                           w1v[:, :H] + w1v[:, H:]))
+                for g in groups:
+                    rows = torch.cat([w.abs().amax(dim=1) for w in g])
+                    live = rows[rows > 0]
+                    if live.numel() and bool(live.min() < rows.max() * self.SPLIT_RANGE):
+                        return False
+        return True
 
     def _plan(self, vspec, cspec, device):
         """vspec / cspec: (labels, count) or ("groups", labels, count) or ("csr", ptr, col, val)."""
@@ -271,6 +298,8 @@ class MessageGNNDecoder(nn.Module):
         flags = N.LDPC_GNN_EARLY_STOP if self.early_termination else 0
         if flags and prec != 1:
             raise NotImplementedError("early termination is implemented on the bf16 path (precision='bf16')")
+        if prec == 0 and not self._split_ok:
+            flags |= N.LDPC_GNN_FP32_PRODUCTS  # weights beyond the f16 splits' range (_split_range_ok)
         probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
         iters = torch.empty(B, dtype=torch.int32, device=dev)
         self.last_iterations = iters

@@ -2,7 +2,11 @@
 
 The reference runs whatever float32 LLRs it is given through dense torch ops
 (message_gnn_decoder.py:190-317): a NaN or inf stays inside its frame (bmm and the MLPs act on
-one frame at a time), and magnitudes far from the training range simply saturate the sigmoid.
+one frame at a time) but reaches every message of that frame in the first layer, because its dense
+bmm with the normalized adjacency multiplies it by the zeros too (0 * inf = 0 * NaN = NaN,
+MGD:108, :118) -- so such a frame's probs are NaN everywhere (checked on oracle.gnn_forward_dense, the
+reference's dense formulation).  Magnitudes far from the training range simply saturate the
+sigmoid.
 This build's fp32 MLP runs its products as scaled two-term f16 splits whose scales come from each
 message column's largest magnitude (csrc/gnn.hpp col_exp / col_exp_w) and from one power of two
 per call for the weights; these tests reach that range logic.
@@ -11,8 +15,7 @@ Bars (stated):
   * frames of only finite LLRs (0, +-1e4, normal): the fp32 path within 2e-5 of the fp32 oracle
     (the bar of test_gnn_gpu.py); the bf16 path within the bf16 bar (mean |dp| <= 5e-3, >= 99.5 % of
     confident decisions equal);
-  * frames holding inf / NaN: the NaN pattern of the probs equals the oracle's, and where both are
-    numbers they agree at the same bars;
+  * frames holding inf / NaN: every prob NaN, as the reference's dense bmm makes them;
   * no other frame changes by a bit: the batch with the special frames replaced by ordinary ones
     decodes the ordinary frames bit-identically;
   * weights whose rows span 1e-4 .. 1e2 and the trained cfg4 checkpoint at 3 seeds: the split MLP
@@ -104,18 +107,26 @@ def test_special_llr_frames(cuda, oracle_mod, precision, z, layers):
     # no ordinary frame changes by a bit
     assert np.array_equal(p[others], q[others], equal_nan=True)
     ref = _oracle(oracle_mod, dec, conv, H, types, llr)
+    dense = None
+    if z == 4:  # the reference's own formulation (dense bmm): small enough here
+        sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+        dense = oracle_mod.gnn_forward_dense(sd, llr, conv.edge_var, n, conv.var_to_check_adjacency,
+                                             conv.check_to_var_adjacency, types).numpy()
     for f in range(llr.shape[0]):
         kind = where.get(f, "ordinary")
-        nan_p, nan_r = np.isnan(p[f]), np.isnan(ref[f])
-        assert np.array_equal(nan_p, nan_r), (f, kind, int(nan_p.sum()), int(nan_r.sum()))
-        ok = ~nan_r
-        if not ok.any():
+        if not bool(torch.isfinite(llr[f]).all()):
+            assert np.isnan(p[f]).all(), (f, kind, int(np.isnan(p[f]).sum()))
+            if dense is not None:
+                assert np.isnan(dense[f]).all(), (f, kind)
             continue
+        assert np.isfinite(p[f]).all() and np.isfinite(ref[f]).all(), (f, kind)
+        if dense is not None:
+            assert float(np.abs(dense[f] - ref[f]).max()) <= TOL, (f, kind)
         if precision == "fp32":
-            err = float(np.abs(p[f][ok] - ref[f][ok]).max())
+            err = float(np.abs(p[f] - ref[f]).max())
             assert err <= TOL, (f, kind, err)
         else:
-            good, stats = _bf16_ok(p[f][ok], ref[f][ok])
+            good, stats = _bf16_ok(p[f], ref[f])
             assert good, (f, kind, stats)
 
 
@@ -142,7 +153,7 @@ def test_split_mlp_fp32_accurate_wide_range(cuda, oracle_mod, monkeypatch, weigh
         ck = torch.load(path, map_location="cpu", weights_only=True)
         base, H, dec, conv, types = _model(32, 10, cuda, seed=seed, scale=1.0)
         dec.load_state_dict(ck["model_state_dict"])
-        llr = awgn_llr(16, H.shape[1], seed - 3.0, seed=100 + seed, device=cuda)  # -2 .. 0 dB: probs in flight
+        llr = awgn_llr(64, H.shape[1], seed - 5.0, seed=100 + seed, device=cuda)  # -4 .. -2 dB: probs in flight
     else:
         base, H, dec, conv, types = _model(32, 4, cuda, seed=seed)
         _spread_rows(dec, seed)
@@ -157,5 +168,9 @@ def test_split_mlp_fp32_accurate_wide_range(cuda, oracle_mod, monkeypatch, weigh
     unsure = float((np.abs(exact - 0.5) < 0.49).mean())
     print(f"{weights} seed {seed}: split {err['1']:.3e}  fp32-mfma {err['0']:.3e}  oracle-f32 {ref_err:.3e}  "
           f"(probs within 0.49 of 0.5: {unsure:.3f})")
-    assert unsure > 0.01  # the comparison is made where the outputs are not saturated
+    assert unsure > (0.01 if weights == "spread" else 0.001)  # the outputs are not all saturated
+    if weights == "spread":  # beyond the splits' range: the decoder chose the fp32-MFMA products
+        assert not dec._split_ok
+    else:
+        assert dec._split_ok
     assert err["1"] <= 2 * max(err["0"], ref_err) + 1e-7, (err, ref_err)
