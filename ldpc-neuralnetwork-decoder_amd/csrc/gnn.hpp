@@ -195,13 +195,36 @@ __device__ __forceinline__ bf16x8_t lds8(const __bf16 *p) { return *reinterpret_
 // two (its largest magnitude to at most 2^15, inside f16's normal range) splits as v = v0 + v1,
 // v0 = f16(v), v1 = f16(v - v0) (22 significant bits); a product is a1 b0 + a0 b1 + a0 b0
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+// v1 = f16(v - v0) as one v_fma_mixlo / mixhi_f16 per value: fma(-v0, 1, v) with v0 read as f16
+// straight from the packed pair and rounded once to f16 -- the same value as converting v0 back,
+// subtracting in f32 (exact: v0 is v rounded) and converting again (tools/ubench/split_mix.hip,
+// 2^23 pairs bit for bit), in 12 instead of ~24 VALU per 8 values.  LDPC_SPLIT_MIX=0: that form.
+#ifndef LDPC_SPLIT_MIX
+#define LDPC_SPLIT_MIX 1
+#endif
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split2h(const float *v, f16x8_t &a, f16x8_t &b) {
+#if LDPC_SPLIT_MIX
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f16x2_t h = {(_Float16)v[2 * p], (_Float16)v[2 * p + 1]};  // v_cvt_pk_f16_f32
+        hi[p] = __builtin_bit_cast(uint32_t, h);
+        uint32_t r;
+        asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hi[p]), "v"(v[2 * p]));
+        asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(r) : "v"(hi[p]), "v"(v[2 * p + 1]));
+        lo[p] = r;
+    }
+    a = __builtin_bit_cast(f16x8_t, hi);
+    b = __builtin_bit_cast(f16x8_t, lo);
+#else
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const _Float16 h0 = (_Float16)v[i];
         a[i] = h0;
         b[i] = (_Float16)(v[i] - (float)h0);
     }
+#endif
 }
 __device__ __forceinline__ void split2h_store(float w, _Float16 *d, int stride) {
     const _Float16 h0 = (_Float16)w;
