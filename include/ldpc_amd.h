@@ -151,8 +151,8 @@ int ldpc_count_errors(const void *d_bits, int bits_dtype, const uint8_t *d_ref, 
  *   :68-81).  d_msg_var (E,) int32 message -> variable for the LLR gather and the output sum
  *   (the reference's message_to_var_mapping, or its column-0 quirk: :218-229 / :285-295).
  * precision: 0 = float32 features and fp32-accurate products (H = 64: scaled two-term f16 splits on
- *   the f16 MFMA, each weight matrix group under one power-of-two scale; other widths: bf16x6 splits
- *   or fp32 fma chains); 1 = bf16 MLP operands, fp32 accumulate.
+ *   the f16 MFMA, each weight matrix group under one power-of-two scale; H = 96..256: the same splits
+ *   per weight slice; other widths: fp32 fma chains); 1 = bf16 MLP operands, fp32 accumulate.
  * d_probs (B, N) float32 = sigmoid(llr + sum of each variable's projected messages).
  * d_work: at least ldpc_gnn_workspace_size(plan, H, N, B, precision) bytes. */
 typedef struct ldpc_gnn_plan ldpc_gnn_plan;
@@ -196,9 +196,10 @@ int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
  * features; a frame whose decision satisfies every parity check stops there, gets its probs from
  * that decision's soft values and d_iters = layers used; the others run on.
  * LDPC_GNN_FP32_PRODUCTS (precision 0): the products of W1_right g and of the MLP run on the fp32 MFMA
- * instead of as f16 splits.  The splits hold 22 bits of every weight whose row's largest |w| is at least
- * 2^-17 of its matrix group's; a caller whose weights span more (MessageGNNDecoder checks this per
- * weight version) sets the flag to keep fp32 accuracy. */
+ * (H = 64) or as three-term bf16 splits (H = 96..256) instead of as scaled two-term f16 splits.  The
+ * splits hold 22 bits of every weight whose row's largest |w| is at least 2^-17 of its matrix group's; a
+ * caller whose weights span more (MessageGNNDecoder checks this per weight version) sets the flag to
+ * keep fp32 accuracy. */
 int ldpc_gnn_forward_ex(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                         const float *d_weights, const int32_t *d_msg_type, const int32_t *d_msg_var,
                         const float *d_llr, int N, int64_t B, int precision, int flags, float *d_probs,

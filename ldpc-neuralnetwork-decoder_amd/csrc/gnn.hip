@@ -1743,6 +1743,7 @@ bool wide_on(const ldpc_gnn_plan *p, int H) {
 struct Ws {
     float *xa, *xb, *Mv, *Mc, *msg_out, *wt;
     float *Pv, *Pc, *hbuf;  // wide path: projected group rows (B, G, H), MLP hidden rows (B, E, 2 H)
+    uint32_t *xmax[2], *hmax, *gmax_v, *gmax_c;  // wide path: each row's largest |value| (f16 splits)
     float *S, *memb;  // row walk (H = 64, plan rw_*): per-check feature sums (B, Gc, H), mean type embeddings (L, Gc, H)
     float *memb_v;    // ... and per var group (L, Gv, H)
     int32_t *csr;
@@ -1783,7 +1784,15 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     w.Pv = wide ? reinterpret_cast<float *>(q) : nullptr;
     w.Pc = wide ? reinterpret_cast<float *>(q + mv) : nullptr;
     w.hbuf = wide ? reinterpret_cast<float *>(q + mv + mc) : nullptr;
-    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb + (wide ? mv + mc + hb : 0);
+    // row maxima: x (two, with the feature ping-pong), h, group rows: 4 B per row
+    const int64_t rm = al(B * p->E * 4), gmv = al(B * (int64_t)p->Gv * 4), gmc = al(B * (int64_t)p->Gc * 4);
+    char *z = q + (wide ? mv + mc + hb : 0);
+    w.xmax[0] = wide ? reinterpret_cast<uint32_t *>(z) : nullptr;
+    w.xmax[1] = wide ? reinterpret_cast<uint32_t *>(z + rm) : nullptr;
+    w.hmax = wide ? reinterpret_cast<uint32_t *>(z + 2 * rm) : nullptr;
+    w.gmax_v = wide ? reinterpret_cast<uint32_t *>(z + 3 * rm) : nullptr;
+    w.gmax_c = wide ? reinterpret_cast<uint32_t *>(z + 3 * rm + gmv) : nullptr;
+    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb + (wide ? mv + mc + hb + 3 * rm + gmv + gmc : 0);
     return w;
 }
 
@@ -2479,6 +2488,13 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             W.y = L.x_out ? L.x_out : ((l % 2 == 0) ? w.xa : w.xb) + xoff;  // the last layer: a free buffer
             W.residual = l > 0;
             W.msg_out = L.last ? L.msg_out : nullptr;
+            W.f16 = !fp32_products;
+            const int64_t roff = b0 * p->E;
+            W.xmax_in = l > 0 ? w.xmax[(l - 1) & 1] + roff : nullptr;
+            W.xmax_out = w.xmax[l & 1] + roff;
+            W.hmax = w.hmax + roff;
+            W.gmax_v = w.gmax_v + b0 * p->Gv;
+            W.gmax_c = w.gmax_c + b0 * p->Gc;
             if (int rc = gnn_wide_layer(W, st)) return rc;
             x_in = W.y;
             continue;

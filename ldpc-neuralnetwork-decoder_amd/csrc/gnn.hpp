@@ -120,6 +120,12 @@ struct GnnWideLayer {
     float *Mv, *Mc, *Pv, *Pc, *hbuf, *y;
     int residual;
     float *msg_out;
+    // f16: the row GEMMs on scaled two-term f16 splits (else bf16x6), with each row's largest |value|
+    // (float bits) recorded by its producer: x_in's (null at layer 0), y's (written here), h's and
+    // the group rows' (scratch)
+    bool f16;
+    const uint32_t *xmax_in;
+    uint32_t *xmax_out, *hmax, *gmax_v, *gmax_c;
 };
 bool gnn_wide_supported(int H);
 int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s);

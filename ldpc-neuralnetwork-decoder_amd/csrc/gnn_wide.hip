@@ -1,6 +1,13 @@
 // gnn_wide.hip -- MessageGNNLayer (message_gnn_decoder.py:51-129) for hidden widths H = 32 k other
-// than 64 (96 .. 256) on the bf16 MFMA, with every fp32 product as the three-term split of
-// gnn_mlp2s_kernel (fp32-accurate: v = v0 + v1 + v2 in bf16, six cross products, fp32 accumulator).
+// than 64 (96 .. 256) on the MFMA, every fp32 product fp32-accurate:
+//   F16 (default, round 6): scaled two-term f16 splits on v_mfma_f32_32x32x16_f16, as the H = 64
+//       kernels (gnn.hpp split2h / mfma3h): each workgroup's weight slice under one power of two
+//       (its largest |w| to at most 2^15), each input row under its own, from the row's largest
+//       |value| that the row's producer recorded (GEMM2's epilogue for the next layer's x, GEMM1's
+//       for h, the group-mean kernel for the group rows; layer 0 from its LLR), so both operands
+//       hold 22 significant bits in f16's normal range: 3 MFMAs per K = 16 step.
+//   !F16 (LDPC_GNN_FP32_PRODUCTS: weights whose rows span more than the splits' range): the three-term
+//       bf16 split of gnn_mlp2s_kernel's earlier form (v = v0 + v1 + v2 in bf16, six cross products).
 //
 // The H = 64 path keeps a layer's four weight matrices in LDS and runs the whole MLP per 32-message
 // tile.  At H = 128 the split images of those matrices are 384 KB, so a layer here is a sequence of
@@ -16,6 +23,7 @@
 // slices of one XCD walk the same tiles in step, so the input rows are read from HBM once per XCD
 // and hit L2 for the other slices (placement changes speed only, never results).
 #include <algorithm>
+#include <type_traits>
 #include <cstdint>
 #include <cstdlib>
 
@@ -54,13 +62,19 @@ struct WArgs {
     const float *resid;    // GEMM2: x (B E, H) or null
     float *out;
     int64_t out_stride;    // floats per output row
+    // F16: per input row, the bits of its largest |value| (GEMM2: h; GEMM1: x, null at layer 0; PROJ:
+    // the group row); per output row, atomicMax of the largest |output| (GEMM1: h; GEMM2: the next
+    // layer's x; null: not recorded).  Non-negative floats order as their bits.
+    const uint32_t *in_max;
+    uint32_t *out_max;
 };
 
 constexpr int kWRowPad = 8;  // bf16 per image row past K: conflict-free ds_read_b128 (as gnn_bf16.hip's W1)
-__host__ __device__ inline size_t wgemm_img_bytes(int NS, int K) { return (size_t)3 * NS * (K + kWRowPad) * 2; }
-inline size_t wgemm_lds_bytes(const WArgs &a) {
-    size_t b = wgemm_img_bytes(a.NS, a.K);
-    if (a.mode == kGemm1) b += (size_t)(a.T + 2) * a.H * 4;  // emb rows, w_in, b_in (fp32)
+// split images of the slice's weights: 2 (f16) or 3 (bf16) terms, 2 bytes each
+__host__ __device__ inline size_t wgemm_img_bytes(int NS, int K, bool f16) { return (size_t)(f16 ? 2 : 3) * NS * (K + kWRowPad) * 2; }
+inline size_t wgemm_lds_bytes(const WArgs &a, bool f16) {
+    size_t b = wgemm_img_bytes(a.NS, a.K, f16);
+    if (a.mode == kGemm1) b += (size_t)(a.T + 2) * a.H * 4 + (size_t)(a.T + 2) * 4;  // emb rows, w_in, b_in; their maxima
     b += (size_t)a.NS * 4;                                  // the slice's init vector (PROJ / GEMM2)
     return (b + 15) / 16 * 16;
 }
@@ -84,10 +98,12 @@ constexpr int kWThreads = 512, kWWaves = kWThreads / 64;
 // AH: input k-steps in flight ahead of the one being multiplied.  The ring slot of chunk s is s % AH
 // on every tile, so AH must divide the k-step count: 4 when it does (K = 64 k), else 2 (K = 32 k,
 // the odd multiples of 32: H = 96, 160, 224 in the projection and GEMM1)
-template <int NT, int AH>
+template <int NT, int AH, bool F16>
 __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int nslices) {
     constexpr int kWAhead = AH;
+    typedef typename std::conditional<F16, _Float16, __bf16>::type w_t;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ uint32_t wmax_bits;
     const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
     constexpr int NS = 32 * NT;
     // placement: XCD x = blockIdx % 8 hosts every slice; the blocks of (x, slice) share x's tile range
@@ -97,18 +113,37 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
     const int nrank = per_x / nslices;
     if (rank >= nrank) return;
     const int n0 = slice * NS;
-    const int K = A.K, rowb = K + kWRowPad;  // bf16 per image row
-    __bf16 *img = reinterpret_cast<__bf16 *>(smem);
+    const int K = A.K, rowb = K + kWRowPad;  // elements per image row
+    w_t *img = reinterpret_cast<w_t *>(smem);
     const int imgstride = NS * rowb;
-    for (int i = tid; i < NS * K; i += kWThreads) {
-        const int u = i / K, k = i - u * K;
-        const float w = A.mode == kGemm2 ? (k < A.H ? A.w_a[(int64_t)(n0 + u) * A.H + k] : A.w_b[(int64_t)(n0 + u) * A.H + k - A.H])
-                                         : A.w_a[(int64_t)(n0 + u) * A.ld + A.col0 + k];
-        split_store(w, img + u * rowb + k, imgstride);
+    auto wval = [&](int u, int k) {
+        return A.mode == kGemm2 ? (k < A.H ? A.w_a[(int64_t)(n0 + u) * A.H + k] : A.w_b[(int64_t)(n0 + u) * A.H + k - A.H])
+                                : A.w_a[(int64_t)(n0 + u) * A.ld + A.col0 + k];
+    };
+    int wexp = 0;
+    if constexpr (F16) {  // the slice's weights under one power of two: its largest |w| to at most 2^15
+        if (tid == 0) wmax_bits = 0u;
+        __syncthreads();
+        float m = 0.0f;
+        for (int i = tid; i < NS * K; i += kWThreads) m = fmaxf(m, fabsf(wval(i / K, i % K)));
+        atomicMax(&wmax_bits, __float_as_uint(m));
+        __syncthreads();
+        wexp = min(col_exp(__uint_as_float(wmax_bits)), 126);
+        const float wsc = pow2f(wexp);
+        for (int i = tid; i < NS * K; i += kWThreads) {
+            const int u = i / K, k = i - u * K;
+            split2h_store(wval(u, k) * wsc, img + u * rowb + k, imgstride);
+        }
+    } else {
+        for (int i = tid; i < NS * K; i += kWThreads) {
+            const int u = i / K, k = i - u * K;
+            split_store(wval(u, k), img + u * rowb + k, imgstride);
+        }
     }
-    float *tabs = reinterpret_cast<float *>(smem + wgemm_img_bytes(NS, K));
+    float *tabs = reinterpret_cast<float *>(smem + wgemm_img_bytes(NS, K, F16));
     float *initv = tabs;  // [NS]
-    float *embs = tabs + NS;  // GEMM1: emb [T][H], w_in [H], b_in [H]
+    float *embs = tabs + NS;  // GEMM1: emb [T][H], w_in [H], b_in [H], then max |emb[t]| [T], max |w_in|, max |b_in|
+    float *embmax = embs + (A.T + 2) * A.H;
     if (A.mode != kGemm1)
         for (int i = tid; i < NS; i += kWThreads)
             initv[i] = A.mode == kGemm2 ? A.init_a[n0 + i] + A.init_b[n0 + i] : A.init_a[n0 + i];
@@ -118,6 +153,15 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
             embs[A.T * A.H + i] = A.w_in[i];
             embs[(A.T + 1) * A.H + i] = A.b_in[i];
         }
+        if constexpr (F16) {
+            for (int r = wave; r < A.T + 2; r += kWWaves) {  // one wave per row: its largest |value|
+                const float *src = r < A.T ? A.emb + (int64_t)r * A.H : r == A.T ? A.w_in : A.b_in;
+                float m = 0.0f;
+                for (int u = lane; u < A.H; u += 64) m = fmaxf(m, fabsf(src[u]));
+                for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+                if (lane == 0) embmax[r] = m;
+            }
+        }
     }
     __syncthreads();
 
@@ -125,13 +169,14 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
     const int64_t ntiles = (A.R + 31) / 32;
     const int64_t t0 = ntiles * x / 8, t1 = ntiles * (x + 1) / 8;
     const int ksteps = K / 16;
-    // Per tile: the row context (row, frame, message, input pointer, type embedding, LLR).  Past the
-    // end a context points at a valid row (its loads are discarded): no branch around any load.
+    // Per tile: the row context (row, frame, message, input pointer, type embedding, LLR, the row's
+    // split scale).  Past the end a context points at a valid row (its loads are discarded): no
+    // branch around any load.
     struct Ctx {
         int64_t t, rr, fb, m;
         bool ok, live;
         const float *src, *eb;
-        float lv;
+        float lv, bnd;
     };
     auto ctx_of = [&](int64_t t) {
         Ctx c;
@@ -147,8 +192,17 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
             c.m = c.rr - c.fb * A.E;
         }
         c.src = A.in ? A.in + c.rr * A.in_stride + 8 * h : nullptr;
-        c.eb = A.mode == kGemm1 ? embs + A.msg_type[c.m] * A.H + 8 * h : nullptr;
+        const int ty = A.mode == kGemm1 ? A.msg_type[c.m] : 0;
+        c.eb = A.mode == kGemm1 ? embs + ty * A.H + 8 * h : nullptr;
         c.lv = (A.mode == kGemm1 && !A.in) ? A.llr[c.fb * A.N + A.msg_var[c.m]] : 0.0f;
+        c.bnd = 0.0f;
+        if constexpr (F16) {
+            // a bound on the row's largest |input|: recorded (h, x, group rows), or for layer 0's
+            // x = llr w_in + b_in, |llr| max |w_in| + max |b_in|; GEMM1 adds max |emb[type]|
+            if (A.in) c.bnd = __uint_as_float(A.in_max[c.rr]);
+            else c.bnd = fabsf(c.lv) * embmax[A.T] + embmax[A.T + 1];
+            if (A.mode == kGemm1) c.bnd = c.bnd + embmax[ty];
+        }
         return c;
     };
     // input chunk of k-step s: units 16 s + 8 h .. + 7 of the context's row (before the embedding)
@@ -171,9 +225,17 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
     float ring[kWAhead][8];
 #pragma unroll
     for (int a = 0; a < kWAhead; ++a) chunk(cur, a, ring[a]);  // K >= 96: ksteps >= kWAhead, ksteps % kWAhead == 0
-    const __bf16 *wl = img + j * rowb + 8 * h;
+    const w_t *wl = img + j * rowb + 8 * h;
     while (cur.live) {
         const Ctx nxt = ctx_of(cur.t + stride);
+        // the row's split scale (column j of B): csc = 2^cexp, the accumulators run at csc 2^wexp
+        float csc = 1.0f, asc = 1.0f, iasc = 1.0f;
+        if constexpr (F16) {
+            const int cexp = col_exp_w(cur.bnd, wexp);
+            csc = pow2f(cexp);
+            asc = pow2f(cexp + wexp);
+            iasc = pow2f(-cexp - wexp);
+        }
         // accumulators start from the additive term (GEMM1: the projected group row; GEMM2: b2 + x;
         // projection: b1), loaded with the tile's first chunks instead of after its last MFMA
         f32x16w acc[NT];
@@ -192,6 +254,9 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
                     }
                     acc[tt][4 * q] = iv.x; acc[tt][4 * q + 1] = iv.y; acc[tt][4 * q + 2] = iv.z; acc[tt][4 * q + 3] = iv.w;
                 }
+            if constexpr (F16)
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) acc[tt] *= asc;  // exact: a power of two
         }
         for (int s0 = 0; s0 < ksteps; s0 += kWAhead) {
 #pragma unroll
@@ -205,24 +270,48 @@ __global__ __launch_bounds__(kWThreads, 1) void gnn_wgemm_kernel(WArgs A, int ns
                         chunk(cur, s + kWAhead, ring[a]);
                     else
                         chunk(nxt, s + kWAhead - ksteps, ring[a]);
-                    bf16x8_t b0, b1, b2;
-                    split3w(v, b0, b1, b2);
+                    if constexpr (F16) {
 #pragma unroll
-                    for (int q = 0; q < NT; ++q) acc[q] = mfma6(wl + 32 * q * rowb + 16 * s, b0, b1, b2, acc[q], imgstride);
+                        for (int i = 0; i < 8; ++i) v[i] *= csc;
+                        f16x8_t b0, b1;
+                        split2h(v, b0, b1);
+#pragma unroll
+                        for (int q = 0; q < NT; ++q) acc[q] = mfma3h(wl + 32 * q * rowb + 16 * s, b0, b1, acc[q], imgstride);
+                    } else {
+                        bf16x8_t b0, b1, b2;
+                        split3w(v, b0, b1, b2);
+#pragma unroll
+                        for (int q = 0; q < NT; ++q) acc[q] = mfma6(wl + 32 * q * rowb + 16 * s, b0, b1, b2, acc[q], imgstride);
+                    }
                 }
             }
         }
+        if constexpr (F16)
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) acc[tt] *= iasc;
+        // register 4 q + i of tile tt holds unit n0 + 32 tt + 8 q + 4 h + i of the row
+        float om = 0.0f;  // the largest |output| of this lane's units (recorded for the row's consumer)
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float4 o = make_float4(acc[tt][4 * q], acc[tt][4 * q + 1], acc[tt][4 * q + 2], acc[tt][4 * q + 3]);
+                if (A.mode == kGemm1) o = make_float4(relu_nan(o.x), relu_nan(o.y), relu_nan(o.z), relu_nan(o.w));
+                acc[tt][4 * q] = o.x; acc[tt][4 * q + 1] = o.y; acc[tt][4 * q + 2] = o.z; acc[tt][4 * q + 3] = o.w;
+                om = fmaxf(om, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+            }
         if (cur.ok) {
-            // register 4 q + i of tile tt holds unit n0 + 32 tt + 8 q + 4 h + i of the row
             float *op = A.out + cur.rr * A.out_stride + n0 + 4 * h;
 #pragma unroll
             for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    float4 o = make_float4(acc[tt][4 * q], acc[tt][4 * q + 1], acc[tt][4 * q + 2], acc[tt][4 * q + 3]);
-                    if (A.mode == kGemm1) o = make_float4(relu_nan(o.x), relu_nan(o.y), relu_nan(o.z), relu_nan(o.w));
-                    *reinterpret_cast<float4 *>(op + 32 * tt + 8 * q) = o;
-                }
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4 *>(op + 32 * tt + 8 * q) =
+                        make_float4(acc[tt][4 * q], acc[tt][4 * q + 1], acc[tt][4 * q + 2], acc[tt][4 * q + 3]);
+        }
+        if (A.out_max) {  // both lane halves hold the row's units: one atomic per row and slice
+            om = fmaxf(om, __shfl_xor(om, 32, 64));
+            if (cur.ok && h == 0) atomicMax(A.out_max + cur.rr, __float_as_uint(om));
         }
         cur = nxt;
     }
@@ -240,6 +329,7 @@ struct WGm {
     int n_tiles;
     const float *inv_v, *inv_c;
     float *Mv, *Mc;
+    uint32_t *gmax_v, *gmax_c;  // F16: each row's largest |value| (bits), or null
     int Gv, Gc, H, N, gpw;  // gpw: groups per wave
     int64_t E, B;
 };
@@ -283,7 +373,17 @@ __global__ __launch_bounds__(256) void gnn_wide_gm_kernel(WGm A) {
     const int gg = isv ? g : g - A.Gv;
     const float inv = isv ? A.inv_v[gg] : A.inv_c[gg];
     float *dst = isv ? A.Mv + (b * A.Gv + gg) * A.H : A.Mc + (b * A.Gc + gg) * A.H;
-    *reinterpret_cast<float4 *>(dst + u) = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+    const float4 mean = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+    *reinterpret_cast<float4 *>(dst + u) = mean;
+    if (A.gmax_v) {  // the row's largest |value| over its lg lanes (a segmented max; no lane leaves it)
+        float m = fmaxf(fmaxf(fabsf(mean.x), fabsf(mean.y)), fmaxf(fabsf(mean.z), fabsf(mean.w)));
+        const int seg0 = (lane / lg) * lg;
+        for (int off = 1; off < lg; off <<= 1) {
+            const float o = __shfl_down(m, off, 64);
+            if (lane + off < seg0 + lg) m = fmaxf(m, o);
+        }
+        if (lane == seg0) (isv ? A.gmax_v + b * A.Gv + gg : A.gmax_c + b * A.Gc + gg)[0] = __float_as_uint(m);
+    }
 }
 
 // msg_out[r] = wo . y[r] + bo (16 lanes per row)
@@ -302,31 +402,39 @@ __global__ __launch_bounds__(256) void gnn_wide_head_kernel(const float *__restr
 
 int g_wcus = 0;
 
-template <int NT, int AH>
+template <int NT, int AH, bool F16>
 int go_wgemm(const WArgs &a, int nslices, dim3 grid, size_t lds, hipStream_t s) {
-    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_wgemm_kernel<NT, AH>),
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_wgemm_kernel<NT, AH, F16>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((gnn_wgemm_kernel<NT, AH>), grid, dim3(kWThreads), lds, s, a, nslices);
+    hipLaunchKernelGGL((gnn_wgemm_kernel<NT, AH, F16>), grid, dim3(kWThreads), lds, s, a, nslices);
     return LDPC_OK;
 }
 
-int launch_wgemm(WArgs a, hipStream_t s) {
+template <bool F16>
+int go_wgemm_nt(const WArgs &a, int nslices, dim3 grid, size_t lds, hipStream_t s, bool ah4) {
+    if (a.NS == 128) return ah4 ? go_wgemm<4, 4, F16>(a, nslices, grid, lds, s) : go_wgemm<4, 2, F16>(a, nslices, grid, lds, s);
+    if (a.NS == 64) return ah4 ? go_wgemm<2, 4, F16>(a, nslices, grid, lds, s) : go_wgemm<2, 2, F16>(a, nslices, grid, lds, s);
+    return ah4 ? go_wgemm<1, 4, F16>(a, nslices, grid, lds, s) : go_wgemm<1, 2, F16>(a, nslices, grid, lds, s);
+}
+
+int launch_wgemm(WArgs a, bool f16, hipStream_t s) {
     if (!g_wcus) {
         int dev = 0;
         LDPC_HIP(hipGetDevice(&dev));
         LDPC_HIP(hipDeviceGetAttribute(&g_wcus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     if (a.R <= 0) return LDPC_OK;
+    if (!f16) a.out_max = nullptr;
     // the widest output slice (4, 2 or 1 tiles of 32 units) whose split images fit the LDS
-    const size_t extra = (a.mode == kGemm1 ? (size_t)(a.T + 2) * a.H * 4 : 0) + 4 * 128 + 16;
+    const size_t extra = (a.mode == kGemm1 ? (size_t)(a.T + 2) * (a.H + 1) * 4 : 0) + 4 * 128 + 16;
     a.NS = 32;
     for (int nt : {4, 2}) {
-        if (a.H % (32 * nt) == 0 && wgemm_img_bytes(32 * nt, a.K) + extra <= 160 * 1024) {
+        if (a.H % (32 * nt) == 0 && wgemm_img_bytes(32 * nt, a.K, f16) + extra <= 160 * 1024) {
             a.NS = 32 * nt;
             break;
         }
     }
-    const size_t lds = wgemm_lds_bytes(a);
+    const size_t lds = wgemm_lds_bytes(a, f16);
     if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "hidden_dim too wide for the MFMA row GEMM's LDS image");
     const int nslices = a.H / a.NS;
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
@@ -335,11 +443,8 @@ int launch_wgemm(WArgs a, hipStream_t s) {
     if ((a.K / 16) % 2) return fail(LDPC_EUNSUPPORTED, "row GEMM reduction length must be a multiple of 32");
     const bool ah4 = (a.K / 16) % 4 == 0;
     const dim3 grid(8 * per_x);
-    int rc;
-    if (a.NS == 128) rc = ah4 ? go_wgemm<4, 4>(a, nslices, grid, lds, s) : go_wgemm<4, 2>(a, nslices, grid, lds, s);
-    else if (a.NS == 64) rc = ah4 ? go_wgemm<2, 4>(a, nslices, grid, lds, s) : go_wgemm<2, 2>(a, nslices, grid, lds, s);
-    else rc = ah4 ? go_wgemm<1, 4>(a, nslices, grid, lds, s) : go_wgemm<1, 2>(a, nslices, grid, lds, s);
-    if (rc) return rc;
+    if (int rc = f16 ? go_wgemm_nt<true>(a, nslices, grid, lds, s, ah4) : go_wgemm_nt<false>(a, nslices, grid, lds, s, ah4))
+        return rc;
     LDPC_CHECK_LAUNCH("gnn_wgemm_kernel");
     return LDPC_OK;
 }
@@ -360,6 +465,8 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         g.meta = L.plan->gt_meta; g.grp = L.plan->gt_grp; g.mem = L.plan->gt_mem; g.n_tiles = L.plan->n_gtiles;
         g.inv_v = L.plan->inv_v; g.inv_c = L.plan->inv_c;
         g.Mv = L.Mv; g.Mc = L.Mc;
+        g.gmax_v = L.f16 ? L.gmax_v : nullptr;
+        g.gmax_c = L.f16 ? L.gmax_c : nullptr;
         g.Gv = L.plan->Gv; g.Gc = L.plan->Gc; g.H = H; g.N = L.N;
         g.gpw = std::max(1, 64 / (H / 4));
         g.E = L.E; g.B = L.B;
@@ -385,9 +492,11 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         a.init_a = side ? L.b1c : L.b1v;
         a.out = side ? L.Pc : L.Pv;
         a.out_stride = H;
-        if (int rc = launch_wgemm(a, s)) return rc;
+        a.in_max = side ? L.gmax_c : L.gmax_v;
+        if (int rc = launch_wgemm(a, L.f16, s)) return rc;
     }
-    // h_s = relu(W1_s,left c + P_s[group]) into h (B E, 2 H)
+    // h_s = relu(W1_s,left c + P_s[group]) into h (B E, 2 H); both sides' row maxima into hmax
+    if (L.f16) LDPC_HIP(hipMemsetAsync(L.hmax, 0, (size_t)BE * 4, s));
     for (int side = 0; side < 2; ++side) {
         WArgs a = base;
         a.mode = kGemm1;
@@ -403,7 +512,9 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         a.G = side ? L.plan->Gc : L.plan->Gv;
         a.out = L.hbuf + side * H;
         a.out_stride = 2 * H;
-        if (int rc = launch_wgemm(a, s)) return rc;
+        a.in_max = L.xmax_in;
+        a.out_max = L.hmax;
+        if (int rc = launch_wgemm(a, L.f16, s)) return rc;
     }
     // y = W2_v h_v + W2_c h_c + (b2_v + b2_c) (+ x): the reference's MLP_v + MLP_c (+ residual)
     {
@@ -420,7 +531,10 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         a.resid = L.residual ? L.x_in : nullptr;
         a.out = L.y;
         a.out_stride = H;
-        if (int rc = launch_wgemm(a, s)) return rc;
+        a.in_max = L.hmax;
+        a.out_max = L.msg_out ? nullptr : L.xmax_out;  // the last layer's rows go to the head only
+        if (L.f16 && a.out_max) LDPC_HIP(hipMemsetAsync(a.out_max, 0, (size_t)BE * 4, s));
+        if (int rc = launch_wgemm(a, L.f16, s)) return rc;
     }
     if (L.msg_out) {
         hipLaunchKernelGGL(gnn_wide_head_kernel, dim3((unsigned)((BE * 16 + 255) / 256)), dim3(256), 0, s, L.y, H, BE,

@@ -247,21 +247,27 @@ class MessageGNNDecoder(nn.Module):
     SPLIT_RANGE = 2.0 ** -17
 
     def _split_range_ok(self):
-        """Whether the H = 64 fp32 kernels' f16 splits hold every weight row to fp32 accuracy: each
-        weight group shares one power-of-two scale (the projection: W1v / W1c right halves; the MLP:
-        the left halves, W2v, W2c and W1v_left + W1v_right), and a row keeps 22 bits while its largest
-        |w| is >= 2^-17 of its group's.  Checked once per weight version; otherwise the forward runs
-        the products on the fp32 MFMA (LDPC_GNN_FP32_PRODUCTS)."""
+        """Whether the fp32 kernels' f16 splits hold every weight row to fp32 accuracy: each weight
+        group shares one power-of-two scale, and a row keeps 22 bits while its largest |w| is >= 2^-17
+        of its group's.  H = 64 (csrc/gnn.hip): the projection's W1v / W1c right halves; the MLP's
+        left halves, W2v, W2c and W1v_left + W1v_right.  H = 96..256 (csrc/gnn_wide.hip: one scale per
+        workgroup slice of output rows; checked per whole matrix, which is stricter): each side's W1
+        right and left halves, W2v | W2c.  Checked once per weight version; otherwise the forward
+        runs the products on the fp32 MFMA / as bf16x6 splits (LDPC_GNN_FP32_PRODUCTS)."""
         H = self.hidden_dim
-        if H != 64:
-            return True
+        wide = H != 64 and H % 32 == 0 and 96 <= H <= 256
+        if H != 64 and not wide:
+            return True  # fp32 fma chains
         with torch.no_grad():
             for layer in self.gnn_layers:
                 v, c = layer.var_to_check_update, layer.check_to_var_update
                 w1v, w1c = v[0].weight.detach().float(), c[0].weight.detach().float()
-                groups = ((w1v[:, H:], w1c[:, H:]),
-                          (w1v[:, :H], w1c[:, :H], v[2].weight.detach().float(), c[2].weight.detach().float(),
-                           w1v[:, :H] + w1v[:, H:]))
+                w2v, w2c = v[2].weight.detach().float(), c[2].weight.detach().float()
+                if wide:
+                    groups = ((w1v[:, H:],), (w1c[:, H:],), (w1v[:, :H],), (w1c[:, :H],),
+                              (torch.cat([w2v, w2c], dim=1),))
+                else:
+                    groups = ((w1v[:, H:], w1c[:, H:]), (w1v[:, :H], w1c[:, :H], w2v, w2c, w1v[:, :H] + w1v[:, H:]))
                 for g in groups:
                     rows = torch.cat([w.abs().amax(dim=1) for w in g])
                     live = rows[rows > 0]

@@ -174,3 +174,32 @@ def test_split_mlp_fp32_accurate_wide_range(cuda, oracle_mod, monkeypatch, weigh
     else:
         assert dec._split_ok
     assert err["1"] <= 2 * max(err["0"], ref_err) + 1e-7, (err, ref_err)
+
+
+@pytest.mark.parametrize("weights", ["normal", "spread"])
+@pytest.mark.parametrize("hidden", [128, 96])
+def test_wide_split_fp32_accurate(cuda, oracle_mod, weights, hidden):
+    """hidden_dim 96 / 128 (csrc/gnn_wide.hip): the row GEMMs on scaled two-term f16 splits (each
+    input row scaled by the largest |value| its producer recorded) are fp32-accurate -- error against
+    the float64 oracle within 2x the fp32 oracle's own, + 1e-7; with weights beyond the splits' range
+    the decoder takes the three-term bf16 form (LDPC_GNN_FP32_PRODUCTS), at the same bar."""
+    base, H, dec, conv, types = _model(32, 4, cuda, seed=40 + hidden)
+    from ldpc_neural_decoder.models import create_message_gnn_decoder as _c
+    torch.manual_seed(40 + hidden)
+    dec, conv = _c(H, num_iterations=4, hidden_dim=hidden, base_graph=base, Z=32)
+    with torch.no_grad():
+        for p in dec.parameters():
+            p.mul_(0.5)
+    dec = dec.to(cuda)
+    if weights == "spread":
+        _spread_rows(dec, hidden)
+    llr = awgn_llr(24, H.shape[1], 1.0, seed=300 + hidden, device=cuda)
+    exact = _oracle(oracle_mod, dec, conv, H, types, llr, dtype=torch.float64)
+    f32 = _oracle(oracle_mod, dec, conv, H, types, llr)
+    got = _native(dec, conv, types, llr, cuda).cpu().numpy()
+    assert dec._split_ok == (weights == "normal")
+    err, ref_err = float(np.abs(got - exact).max()), float(np.abs(f32 - exact).max())
+    unsure = float((np.abs(exact - 0.5) < 0.49).mean())
+    print(f"H={hidden} {weights}: native {err:.3e}  oracle-f32 {ref_err:.3e}  (unsaturated {unsure:.3f})")
+    assert unsure > 0.01
+    assert err <= 2 * ref_err + 1e-7, (err, ref_err)
