@@ -1730,15 +1730,8 @@ __global__ void gnn_memb_kernel(const float *__restrict__ emb0, int64_t layer_st
 
 int64_t layer_floats(int H, int T) { return (int64_t)T * H + 2 * (2LL * H * H + H + (int64_t)H * H + H) + H + 1; }
 
-// H = 32 k other than 64 (gnn_wide.hip) on the MFMA row GEMMs; LDPC_GNN_WIDE=0 keeps the VALU
-// kernels (A/B runs).  Read once: the workspace size depends on it.
-bool wide_on(const ldpc_gnn_plan *p, int H) {
-    static const bool env = [] {
-        const char *e = std::getenv("LDPC_GNN_WIDE");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return env && gnn_wide_supported(H) && !p->weighted && p->n_gtiles > 0;
-}
+// H = 32 k other than 64 (gnn_wide.hip) on the MFMA row GEMMs (group plans; inference)
+bool wide_on(const ldpc_gnn_plan *p, int H) { return gnn_wide_supported(H) && !p->weighted && p->n_gtiles > 0; }
 
 struct Ws {
     float *xa, *xb, *Mv, *Mc, *msg_out, *wt;

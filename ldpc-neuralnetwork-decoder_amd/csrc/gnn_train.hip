@@ -1083,11 +1083,6 @@ __global__ __launch_bounds__(256) void train_outer_kernel(OuterT P) {
 // accumulator register is two 128-B row segments: the full-rate atomic shape).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// LDPC_GNN_OUTER_H64=0: the general weight-gradient kernels for H = 64 too (A/B); read per call
-int outer_h64() {
-    const char *e = std::getenv("LDPC_GNN_OUTER_H64");
-    return !(e && std::atoi(e) == 0);
-}
 
 // H64: H = J = 64 from zsrc: no per-load bounds or source checks, software-pipelined
 template <int NIT, int NJT, bool H64 = false>
@@ -1502,7 +1497,7 @@ int launch_outer(const OuterT &o, unsigned grid, hipStream_t s) {
     }
     const int nit = (o.H + 31) / 32, njt = (o.J + 31) / 32;
     // H = 64 from plain row sources: the specialised kernels (no per-load source / bounds checks)
-    const bool h64 = o.H == 64 && !o.G && o.J == 64 && outer_h64();
+    const bool h64 = o.H == 64 && !o.G && o.J == 64;
     if (h64 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2, true>), dim3(grid), dim3(256), 0, s, o);
     else if (nit == 2 && njt == 4) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 4>), dim3(grid), dim3(256), 0, s, o);
     else if (nit == 2 && njt == 2) hipLaunchKernelGGL((train_outer_mfma_kernel<2, 2>), dim3(grid), dim3(256), 0, s, o);
@@ -1754,13 +1749,6 @@ int bwd_overlap() {
     return e ? std::atoi(e) : 1;
 }
 
-int bwd_mfma() {
-    static const int v = [] {
-        const char *e = std::getenv("LDPC_GNN_TRAIN_MFMA");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
-}
 
 }  // namespace
 }  // namespace ldpc
@@ -1855,16 +1843,12 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
     }
     LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<512>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
-    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<256>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
     // projected groups (see train_mlp_bwd_mfma_kernel): H = 64 on MFMA with the plan's projection tiles
-    const bool pj = H == 64 && bwd_mfma() && bwd_proj() && p->n_ptiles > 0;
+    const bool pj = H == 64 && bwd_proj() && p->n_ptiles > 0;
     // the forward's saved projections (ldpc_gnn_forward_train_ex): no recompute here
     const bool sp = pj && d_proj != nullptr;
     if (pj) {
         LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<512, true>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
-        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_mfma_kernel<256, true>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_mfma_lds()));
         LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(train_mlp_bwd_s6_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlp_bwd_s6_lds()));
@@ -1985,17 +1969,12 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
         m.hv = w.hv; m.hc = w.hc; m.dhv = w.dhv; m.dhc = w.dhc;
         m.dco = w.dco; m.da = w.da; m.db = w.db;
         m.H = H; m.N = N; m.Gv = p->Gv; m.Gc = p->Gc; m.E = E; m.R = R;
-        if (H == 64 && bwd_mfma()) {  // LDPC_GNN_TRAIN_MFMA=0 selects the VALU kernel (A/B runs)
-            const int nt = bwd_mfma() == 2 ? 256 : 512;  // =2: 256 threads, 1 wave per SIMD
-            const unsigned grid = (unsigned)std::min<int64_t>((R + 32 * (nt / 64) - 1) / (32 * (nt / 64)), (int64_t)g_cus_t);
-            if (pj && nt == 512 && bwd_s6())
+        if (H == 64) {  // fp32 MFMA / split MFMA kernels, 8 waves per workgroup
+            const unsigned grid = (unsigned)std::min<int64_t>((R + 32 * 8 - 1) / (32 * 8), (int64_t)g_cus_t);
+            if (pj && bwd_s6())
                 hipLaunchKernelGGL(train_mlp_bwd_s6_kernel, dim3(grid), dim3(512), mlp_bwd_s6_lds(), s, m);
-            else if (pj && nt == 256)
-                hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<256, true>), dim3(grid), dim3(256), mlp_bwd_mfma_lds(), s, m);
             else if (pj)
                 hipLaunchKernelGGL((train_mlp_bwd_mfma_kernel<512, true>), dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);
-            else if (nt == 256)
-                hipLaunchKernelGGL(train_mlp_bwd_mfma_kernel<256>, dim3(grid), dim3(256), mlp_bwd_mfma_lds(), s, m);
             else
                 hipLaunchKernelGGL(train_mlp_bwd_mfma_kernel<512>, dim3(grid), dim3(512), mlp_bwd_mfma_lds(), s, m);
             LDPC_CHECK_LAUNCH("train_mlp_bwd_mfma_kernel");
@@ -2053,7 +2032,7 @@ extern "C" int ldpc_gnn_backward_ds_ex(const ldpc_gnn_plan *p, int hidden, int t
         // weight gradients
         OuterT o{};
         o.H = H; o.E = E; o.R = R;
-        if (H == 64 && outer_h64()) {  // dW2v and dW2c in one pass over dX
+        if (H == 64) {  // dW2v and dW2c in one pass over dX
             Dw2T d2{w.dX, w.hv, w.hc, Gw[3], Gw[7], Gw[4], Gw[8], R};
             hipLaunchKernelGGL(train_dw2_kernel, dim3(red_grid), dim3(256), 0, s, d2);
             LDPC_CHECK_LAUNCH("train_dw2_kernel");

@@ -326,14 +326,6 @@ __global__ __launch_bounds__(512) void check_group_idx_kernel(const float *__res
     }
 }
 
-bool gather_lds_enabled() {
-    static const bool on = [] {
-        const char *e = std::getenv("LDPC_GATHER_LDS");
-        return !e || std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 // d in[b][idx[i][k*]] += g[b][i] * sign_product * sgn(v_k*)  (k* = argmin; sgn(0) = 0 covers the
 // padded and zero entries, whose |v| was overwritten in place)
 __global__ void gather_minsum_bwd_kernel(const float *__restrict__ g, const float *__restrict__ in, int64_t B,
@@ -548,7 +540,7 @@ extern "C" int ldpc_gather_minsum(const float *d_in, int64_t B, int n_in, const 
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
     if (!d_in || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
-    if (const int fpw = gather_lds_enabled() ? gather_fpw(n_in) : 0)
+    if (const int fpw = gather_fpw(n_in))
         return launch_gather_lds<true>(fpw, d_in, nullptr, B, n_in, d_idx, n_out, K, d_out, d_argmin,
                                        static_cast<hipStream_t>(stream));
     hipLaunchKernelGGL(gather_minsum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
@@ -613,15 +605,8 @@ extern "C" int ldpc_gather_sum(const float *d_llr, const float *d_msgs, int64_t 
     if (B < 0 || n_in <= 0 || n_out < 0 || K <= 0) return fail(LDPC_EINVAL, "bad gather dimensions");
     if (!B || !n_out) return LDPC_OK;
     if (!d_msgs || !d_idx || !d_out) return fail(LDPC_EINVAL, "NULL tensor");
-    // the LDS-staged form is opt-in here (LDPC_GATHER_SUM_LDS=1): measured 12 % slower at BG2 Z=32,
-    // the index (K = 22, rows ending early) is then read once per 2 frames instead of 4
-    static const bool sum_lds = [] {
-        const char *e = std::getenv("LDPC_GATHER_SUM_LDS");
-        return e && std::atoi(e) != 0;
-    }();
-    if (const int fpw = sum_lds ? gather_fpw(n_in) : 0)
-        return launch_gather_lds<false>(fpw, d_msgs, d_llr, B, n_in, d_idx, n_out, K, d_out, nullptr,
-                                        static_cast<hipStream_t>(stream));
+    // (an LDS-staged form of this sum, as the min-sum gather's, measured 12 % slower at BG2 Z=32: the
+    // index, K = 22 with rows ending early, is then read once per 2 frames instead of 4)
     hipLaunchKernelGGL(gather_sum_kernel, grid_for((B + kFB - 1) / kFB * n_out), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_llr,
                        d_msgs, B, n_in, d_idx, n_out, K, d_out);
