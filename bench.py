@@ -124,6 +124,9 @@ PMC_KERNEL_SYMBOL = {
     "gnn-z32-bf16-i10": "gnn_bf16_mlp_kernel",
     "gnn-z32-h128": "gnn_wide",
     "lay-z32": "check_group",
+    # the fp32 GNN's dominant kernels (projection + split MLP) share gnn.hip's code object
+    "gnn-z32": "gnn_mlp2s_kernel",
+    "gnn-z4": "gnn_mlp2s_kernel",
 }
 
 
@@ -580,15 +583,19 @@ def main():
             per_launch_alg = (4 * 64 * 64 * E + 2 * 64 * 64 * g_m) * B * iters
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         elif kind == "gnn" and hid != 64:
-            # the reference's useful FLOPs (12 H^2 E per frame-layer) against the fp32 MFMA peak
-            # (the row GEMMs execute them as bf16x6 splits on the bf16 MFMA: see notes)
-            per_launch_alg = nominal_flops * B * iters
-            bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
-        elif kind in ("gnn-sweep", "gnn") and z == 32:
-            # SURVEY 8(d) cfg4, HBM: per frame-layer 3 passes over the fp32 features (E x 64) + the
-            # group rows written and read ((N + M) x 64 fp32, twice).  The binding resource of this
-            # build's fp32 path: its kernels move their bytes at 4-5 TB/s while its MFMA pipe (fp32
-            # products as bf16x6 splits) is a quarter busy (roofline_notes)
+            # gnn_wide.hip's row GEMMs (f16 two-term splits) are HBM-bound: SURVEY 8(d)'s per
+            # frame-layer bytes (3 passes over the (E, H) fp32 features + the group rows written and
+            # read) as the algorithmic figure; the design's own traffic (h round-trips HBM between
+            # GEMM1 and GEMM2) is in the notes
+            per_launch_alg = (3 * E * hid * 4 + 2 * (g_n + g_m) * hid * 4) * B * iters
+            wide_design_bytes = (12 * E * hid * 4 + 3 * (g_n + g_m) * hid * 4) * B * iters
+            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+        elif kind in ("gnn-sweep", "gnn"):
+            # SURVEY 8(d) cfg2 / cfg4, HBM: per frame-layer 3 passes over the fp32 features (E x 64) +
+            # the group rows written and read ((N + M) x 64 fp32, twice; 3.99 MB per cfg2 codeword).
+            # The binding resource of this build's fp32 path at both sizes: its kernels move their
+            # bytes at 4-5 TB/s while the matrix pipe (fp32 products as f16 two-term splits) is a
+            # fraction busy (roofline_notes)
             fp32_layer_bytes = (3 * E * 64 * 4 + 2 * (g_n + g_m) * 64 * 4) * B
             per_launch_alg = fp32_layer_bytes * iters * (len(sweep_snrs) if kind == "gnn-sweep" else 1)
             bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
@@ -603,13 +610,6 @@ def main():
             # outer products) per frame-layer, fp32 (VALU fp32 peak = fp32 MFMA peak)
             per_launch_alg = 36 * 64 * 64 * E * B * iters
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
-        elif kind == "gnn" and os.environ.get("LDPC_GNN_SPLIT", "1") != "0":
-            # cfg2 shape on the split MLP: its products run as scaled two-term f16 splits, three
-            # v_mfma_f32_32x32x16_f16 products per fp32 product (gnn.hip gnn_mlp2s_kernel), so the
-            # bound is the f16 MFMA pipe on those executed FLOPs; the reference's FLOPs against the fp32
-            # MFMA peak (SURVEY 8(d) cfg2's yardstick, > 1 here) are in the notes
-            per_launch_alg = 3 * mlp_flops * B * iters
-            bound, unit, peak = "mfma", "TFLOP/s", BF16_MFMA_PEAK_TFS
         else:
             # the reference's useful FLOPs, 12 H^2 E per frame-layer
             # (this build executes fewer: see the notes' executed_frac)
@@ -692,7 +692,7 @@ def main():
         notes = None
         if kind in ("gnn", "gnn-sweep"):
             reps = len(sweep_snrs) if kind == "gnn-sweep" else 1
-            split = os.environ.get("LDPC_GNN_SPLIT", "1") != "0"
+            split = os.environ.get("LDPC_GNN_SPLIT", "1") != "0" and hid == 64
             secs = kern_ms * 1e-3
             notes = {"flop_model": "the reference's per-message MLPs cost 12 H^2 E FLOP per frame-layer (SURVEY 8(d)); "
                                    "this build executes 8 H^2 E + 2 H^2 (N + M) fp32-equivalent FLOPs (W1's group half "
@@ -700,8 +700,12 @@ def main():
                      "nominal_fp32_tflops": nominal_flops * B * iters * reps / secs / 1e12,
                      "nominal_frac_of_fp32_mfma": nominal_flops * B * iters * reps / secs / 1e12 / FP32_MFMA_PEAK_TFS,
                      "executed_flops_per_launch": fwd_flops * B * iters * reps}
-            if bound != "hbm" and not split:  # Z = 4 (cfg2 shape) on the fp32 MFMA kernels
-                notes["executed_frac"] = fwd_flops / nominal_flops * achieved / peak
+            if hid != 64:  # gnn_wide.hip: the bytes its kernels move by design, and their rate
+                notes["wide_design_bytes_per_launch"] = wide_design_bytes
+                notes["wide_design_GBps"] = wide_design_bytes / secs / 1e9
+                notes["wide_design_frac_of_hbm_peak"] = wide_design_bytes / secs / 1e9 / HBM_PEAK_GBS
+                notes["wide_products"] = ("scaled two-term f16 splits on v_mfma_f32_32x32x16_f16, one power of two "
+                                          "per weight slice and per input row (recorded by its producer)")
             if split:
                 # gnn_mlp2s_kernel: the per-message products (8 H^2 E) as three f16 products each on the
                 # f16 MFMA (scaled two-term splits); the group projection (2 H^2 (N + M)) stays on the
@@ -711,7 +715,7 @@ def main():
                                          "(fp32-accurate: tests/test_gnn_depth_gpu.py::test_split_mlp_is_fp32_accurate)")
                 notes["mlp_f16_mfma_flops_per_launch"] = mlp_f16
                 notes["mlp_f16_mfma_frac_whole_forward"] = mlp_f16 / (kern_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFS
-                if bound == "mfma":
+                if nominal_flops * B * iters * reps / secs / 1e12 > FP32_MFMA_PEAK_TFS:
                     notes["nominal_over_fp32_peak"] = ("the reference's FLOPs per second exceed the fp32 MFMA "
                                                        "peak: the products run on the f16 MFMA (three per product)")
         if bound == "valu":
