@@ -135,6 +135,8 @@ __device__ __forceinline__ float4 hyb_x(float4 f, float v, float4 w, float4 c) {
 
 // feature u of message m of frame b *before* the type embedding
 __device__ __forceinline__ float x_feat(const GnnLayer &P, int64_t b, int64_t m, int u, int H) {
+    if (P.hv2c)  // hybrid decoder: x = (v2c w_in + b_in) + F (custom_combine_kernel's float sequence)
+        return (P.hv2c[b * P.E + m] * P.w_in[u] + P.b_in[u]) + P.x_in[(b * P.E + m) * H + u];
     if (P.x_in) return P.x_in[(b * P.E + m) * H + u];
     const float l = P.llr[b * P.N + P.msg_var[m]];
     return l * P.w_in[u] + P.b_in[u];  // Linear(1, H)
@@ -149,6 +151,7 @@ __global__ __launch_bounds__(256) void gnn_group_mean_kernel(GnnLayer P, int H) 
     const int64_t b = wid / G;
     const int g = (int)(wid - b * G);
     const bool isv = g < P.Gv;
+    if (isv && !P.vside) return;  // the hybrid decoder's check side alone
     const int gg = isv ? g : g - P.Gv;
     const int32_t *ptr = isv ? P.vg_ptr : P.cg_ptr;
     const int32_t *mem = isv ? P.vg_mem : P.cg_mem;
@@ -1535,7 +1538,7 @@ __global__ __launch_bounds__(256) void gnn_mlp_tiled_kernel(GnnLayer P, int H) {
         for (int o = lane; o < H; o += 64)
 #pragma unroll
             for (int i = 0; i < NM; ++i) yy[o * NM + i] = 0.0f;
-        for (int side = 0; side < 2; ++side) {
+        for (int side = P.vside ? 0 : 1; side < 2; ++side) {  // vside 0: the check side alone (hybrid)
             const float *W1T = P.wt + (int64_t)side * 3 * H * H, *W2T = W1T + 2LL * H * H;
             const float *b1 = side ? P.b1c : P.b1v, *b2 = side ? P.b2c : P.b2v;
             for (int i = 0; i < NM; ++i) {
@@ -1843,6 +1846,22 @@ __global__ __launch_bounds__(256) void custom_combine_kernel(float *__restrict__
     }
     const float4 k = reinterpret_cast<const float4 *>(wo)[q];
     float part = o.x * k.x + o.y * k.y + o.z * k.z + o.w * k.w;
+    for (int off = 8; off > 0; off >>= 1) part += __shfl_xor(part, off, 16);
+    if (q == 0) msg_out[r] = part + bo[0];
+}
+
+// The same head for any H: out_m = wo . ((v2c w_in + b_in) + F_m) + bo, 16 lanes per row over the units
+__global__ __launch_bounds__(256) void custom_combine_any_kernel(const float *__restrict__ x, const float *__restrict__ v2c,
+                                                                 const float *__restrict__ w_in, const float *__restrict__ b_in,
+                                                                 int H, int64_t R, const float *__restrict__ wo,
+                                                                 const float *__restrict__ bo, float *__restrict__ msg_out) {
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int q = threadIdx.x & 15;
+    if (r >= R) return;
+    const float v = v2c[r];
+    const float *f = x + r * H;
+    float part = 0.0f;
+    for (int u = q; u < H; u += 16) part += ((v * w_in[u] + b_in[u]) + f[u]) * wo[u];
     for (int off = 8; off > 0; off >>= 1) part += __shfl_xor(part, off, 16);
     if (q == 0) msg_out[r] = part + bo[0];
 }
@@ -2719,16 +2738,87 @@ extern "C" int ldpc_gnn_forward(const ldpc_gnn_plan *p, int hidden, int types, i
 // ------------------------------------------------------------------------ hybrid GNN host side
 extern "C" int64_t ldpc_gnn_custom_var_workspace_size(const ldpc_gnn_plan *p, int hidden, int N, int64_t B, int layers) {
     if (!p || hidden <= 0 || N <= 0 || B < 0 || layers <= 0) return fail(LDPC_EINVAL, "bad arguments");
-    // carve() with at least 3 layers keeps both feature buffers; + v2c (B, E)
-    return carve(p, hidden, N, B, std::max(layers, 3), 0, nullptr).bytes + (B * p->E * 4 + 255) / 256 * 256;
+    // carve() with at least 3 layers keeps both feature buffers (H != 64: the tiled kernel's
+    // transposed weights, never the wide path); + v2c (B, E)
+    return carve(p, hidden, N, B, std::max(layers, 3), 0, nullptr, hidden != kMfmaH).bytes + (B * p->E * 4 + 255) / 256 * 256;
 }
+
+namespace ldpc {
+namespace {
+// The hybrid GNN at H != 64 (up to kTiledMaxH): the check side of the generic kernels -- weighted-free
+// group means of the check groups (gnn_group_mean_kernel, vside 0), the tiled MLP over [c; b] with
+// the layer's own output head, then the same variable update and output as H = 64.
+int custom_var_forward_any(const ldpc_gnn_plan *p, int H, int types, int layers, const float *d_weights,
+                           const int32_t *d_msg_type, const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
+                           float *d_probs, void *d_work, hipStream_t s) {
+    Ws w = carve(p, H, N, B, std::max(layers, 3), 0, d_work, true);
+    float *v2c = reinterpret_cast<float *>(static_cast<char *>(d_work) + w.bytes);
+    if (!w.wt) return fail(LDPC_EUNSUPPORTED, "hidden_dim too wide for the hybrid GNN");
+    if (!g_num_cus) {
+        int dev = 0;
+        LDPC_HIP(hipGetDevice(&dev));
+        LDPC_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (int rc = gnn_build_var_csr(d_msg_var, p->E, N, w.csr, s)) return rc;
+    GnnLayer L{};
+    L.llr = d_llr; L.msg_var = d_msg_var; L.w_in = d_weights; L.b_in = d_weights + H; L.N = N; L.T = types;
+    L.msg_type = d_msg_type;
+    L.vgroup = p->vgroup; L.cgroup = p->cgroup; L.vg_ptr = p->vg_ptr; L.vg_mem = p->vg_mem;
+    L.cg_ptr = p->cg_ptr; L.cg_mem = p->cg_mem; L.inv_v = p->inv_v; L.inv_c = p->inv_c;
+    L.Gv = p->Gv; L.Gc = p->Gc; L.E = p->E; L.B = B; L.Mv = w.Mv; L.Mc = w.Mc;
+    L.vside = 0; L.residual = 0; L.last = 1; L.d1 = 0;
+    L.msg_out = w.msg_out;
+    const int64_t R = B * p->E;
+    const int tw = tiled_waves(H);
+    const size_t tl = (size_t)tw * kTiledNM * 4 * H * 4;
+    if (tl > 64 * 1024)
+        LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_mlp_tiled_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
+    const float *x_in = nullptr;
+    for (int l = 0; l < layers; ++l) {
+        const float *lw = d_weights + 2 * H + (int64_t)l * layer_floats(H, types);
+        L.emb = lw;
+        L.w1v = L.emb + (int64_t)types * H; L.b1v = L.w1v + 2LL * H * H; L.w2v = L.b1v + H; L.b2v = L.w2v + (int64_t)H * H;
+        L.w1c = L.b2v + H; L.b1c = L.w1c + 2LL * H * H; L.w2c = L.b1c + H; L.b2c = L.w2c + (int64_t)H * H;
+        L.wo = L.b2c + H; L.bo = L.wo + H;
+        L.x_in = x_in;
+        L.hv2c = l > 0 ? v2c : nullptr;        // layers >= 1 read x = (v2c w_in + b_in) + F_{l-1}
+        L.x_out = (l % 2 == 0) ? w.xa : w.xb;  // F
+        L.wt = w.wt + 6LL * H * H * l;
+        hipLaunchKernelGGL(gnn_wt_kernel, dim3((unsigned)((6LL * H * H + 255) / 256)), dim3(256), 0, s, L.w1v, L.w2v,
+                           L.w1c, L.w2c, H, w.wt + 6LL * H * H * l);
+        LDPC_CHECK_LAUNCH("gnn_wt_kernel (hybrid)");
+        const int64_t waves = B * (int64_t)(p->Gv + p->Gc);
+        hipLaunchKernelGGL(gnn_group_mean_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, H);
+        LDPC_CHECK_LAUNCH("gnn_group_mean_kernel (hybrid check side)");
+        const int64_t want = (R + (int64_t)tw * kTiledNM - 1) / ((int64_t)tw * kTiledNM);
+        const unsigned grid = (unsigned)std::min<int64_t>(want, (int64_t)std::max(1, g_num_cus * 16 / tw));
+        hipLaunchKernelGGL(gnn_mlp_tiled_kernel, dim3(grid), dim3(64 * tw), tl, s, L, H);
+        LDPC_CHECK_LAUNCH("gnn_mlp_tiled_kernel (hybrid check side)");
+        hipLaunchKernelGGL(custom_var_llr_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, w.msg_out, w.csr,
+                           d_llr, p->E, N, B, v2c);
+        LDPC_CHECK_LAUNCH("hybrid GNN variable update");
+        if (l == layers - 1) {
+            hipLaunchKernelGGL(custom_combine_any_kernel, dim3((unsigned)((R * 16 + 255) / 256)), dim3(256), 0, s, L.x_out,
+                               v2c, d_weights, d_weights + H, H, R, L.wo, L.bo, w.msg_out);
+            LDPC_CHECK_LAUNCH("hybrid GNN output head");
+        }
+        x_in = L.x_out;
+    }
+    hipLaunchKernelGGL(custom_output_kernel, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, s, w.msg_out, w.csr, d_llr,
+                       p->E, N, B * N, d_probs);
+    LDPC_CHECK_LAUNCH("custom_output_kernel");
+    return LDPC_OK;
+}
+}  // namespace
+}  // namespace ldpc
 
 extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, int types, int layers,
                                            const float *d_weights, const int32_t *d_msg_type,
                                            const int32_t *d_msg_var, const float *d_llr, int N, int64_t B,
                                            float *d_probs, void *d_work, int64_t work_bytes, void *stream) {
     if (!p) return fail(LDPC_EINVAL, "plan is NULL");
-    if (hidden != kMfmaH) return fail(LDPC_EUNSUPPORTED, "the hybrid GNN runs at hidden_dim 64");
+    if (hidden <= 0 || hidden > kTiledMaxH) return fail(LDPC_EUNSUPPORTED, "the hybrid GNN runs at hidden_dim <= 1024");
     if (p->weighted || p->n_ptiles == 0) return fail(LDPC_EUNSUPPORTED, "the hybrid GNN needs a group plan");
     if (types <= 0 || layers <= 0 || N <= 0 || B < 0) return fail(LDPC_EINVAL, "bad dimensions");
     if (B == 0) return LDPC_OK;
@@ -2736,6 +2826,9 @@ extern "C" int ldpc_gnn_custom_var_forward(const ldpc_gnn_plan *p, int hidden, i
     const int64_t need = ldpc_gnn_custom_var_workspace_size(p, hidden, N, B, layers);
     if (!d_work || work_bytes < need) return fail(LDPC_EINVAL, "workspace too small: need " + std::to_string(need) + " bytes");
     if (B * p->E >= (1LL << 31) / 16) return fail(LDPC_EUNSUPPORTED, "batch too large for one launch (chunk it)");
+    if (hidden != kMfmaH)
+        return custom_var_forward_any(p, hidden, types, layers, d_weights, d_msg_type, d_msg_var, d_llr, N, B, d_probs,
+                                      d_work, static_cast<hipStream_t>(stream));
     const int H = kMfmaH;
     hipStream_t s = static_cast<hipStream_t>(stream);
     Ws w = carve(p, H, N, B, std::max(layers, 3), 0, d_work);

@@ -283,9 +283,10 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
 
     and the output (:855-877): out_m = output_projection_L(x_m), probs_v = sigmoid(mean over v's
     messages of out_m + llr_v).  forward(...) returns (probs, None), or (probs, max over bits of
-    the per-bit BCE) with ground truth, as the reference does.  hidden_dim 64; clique / identity
-    check adjacencies.  Kernels: ldpc_gnn_custom_var_forward (csrc/gnn.hip).  Oracle:
-    oracle/oracle.py custom_variable_forward.
+    the per-bit BCE) with ground truth, as the reference does.  Any hidden_dim up to 1024 (the
+    reference's constructor takes any, MGD:765: 64 runs the split-MFMA kernels, other widths the tiled
+    fp32 kernels); clique / identity check adjacencies.  Kernels: ldpc_gnn_custom_var_forward
+    (csrc/gnn.hip).  Oracle: oracle/oracle.py custom_variable_forward.
 
     Training: this build has no backward for the hybrid GNN.  With grad enabled and trainable
     parameters the probs carry a grad_fn whose backward raises NotImplementedError (naming this
@@ -294,9 +295,9 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
     by construction, whatever the backward."""
 
     def __init__(self, num_messages, num_iterations=5, hidden_dim=64, num_message_types=1, depth_L=3):
-        if hidden_dim != 64:  # refused up front rather than at the first forward
+        if not 0 < hidden_dim <= 1024:  # refused up front rather than at the first forward
             raise ValueError(f"CustomVariableMessageGNNDecoder: this build's kernels run the hybrid GNN at "
-                             f"hidden_dim 64 only (got hidden_dim={hidden_dim})")
+                             f"hidden_dim 1 .. 1024 (got hidden_dim={hidden_dim})")
         super().__init__(num_messages, num_iterations, hidden_dim, num_message_types)
         self.gnn_layers = nn.ModuleList([
             CustomVariableMessageGNNLayer(num_message_types, hidden_dim, depth_L) for _ in range(num_iterations)])
@@ -337,18 +338,19 @@ class CustomVariableMessageGNNDecoder(MessageGNNDecoder):
         probs = torch.empty((B, Nv), dtype=torch.float32, device=dev)
         if B:
             lib = N.lib()
-            ws1 = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, 64, Nv, 1, L))
-            per = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, 64, Nv, 2, L)) - ws1
+            Hd = self.hidden_dim
+            ws1 = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, Hd, Nv, 1, L))
+            per = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, Hd, Nv, 2, L)) - ws1
             budget = int(os.environ.get("LDPC_GNN_WORKSPACE_BYTES", 48 << 30))
             limit = max(1, ((1 << 31) // 16 - 1) // E)  # the kernels' per-launch message bound
             chunk = max(1, min(B, limit, max(1, (budget - ws1) // max(per, 1))))
-            wsb = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, 64, Nv, chunk, L))
+            wsb = N.check(lib.ldpc_gnn_custom_var_workspace_size(plan.handle, Hd, Nv, chunk, L))
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             with torch.no_grad():
                 for s in range(0, B, chunk):
                     n = min(chunk, B - s)
                     N.check(lib.ldpc_gnn_custom_var_forward(
-                        plan.handle, 64, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr[s:s + n]), Nv, n,
+                        plan.handle, Hd, T, L, N.ptr(blob), N.ptr(types), N.ptr(io_map), N.ptr(llr[s:s + n]), Nv, n,
                         N.ptr(probs[s:s + n]), N.ptr(ws), wsb, N.stream_ptr(dev)))
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             probs = _NoHybridBackward.apply(probs, *[p for p in self.parameters() if p.requires_grad])

@@ -18,11 +18,11 @@ pytestmark = pytest.mark.gpu
 TOL = 2e-5
 
 
-def setup(z, layers, seed):
+def setup(z, layers, seed, hidden=64):
     base = load_base_matrix(code_path(z))
     H = expand_base_matrix(base, z)
     torch.manual_seed(seed)
-    dec, conv = create_custom_variable_message_gnn_decoder(H, num_iterations=layers, hidden_dim=64,
+    dec, conv = create_custom_variable_message_gnn_decoder(H, num_iterations=layers, hidden_dim=hidden,
                                                            base_graph=base, Z=z)
     types = conv.get_message_types(base, z)
     return H, dec, conv, types
@@ -36,6 +36,22 @@ def test_hybrid_gnn_vs_oracle(cuda, oracle_mod, z, layers, B, identity):
     Av = None if identity else conv.var_to_check_adjacency
     probs, loss = dec(llr.to(cuda), conv.message_to_var_index().to(cuda), types.to(cuda), Av, Ac)
     assert loss is None
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    ref = oracle_mod.custom_variable_forward(sd, llr, conv.edge_var, conv.edge_chk, H.shape[1], H.shape[0],
+                                             types=types, check_identity=identity)
+    np.testing.assert_allclose(probs.detach().cpu().numpy(), ref.numpy(), atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("hidden,z,identity", [(8, 4, False), (32, 4, True), (96, 32, False), (128, 4, False)])
+def test_hybrid_gnn_any_hidden_dim_vs_oracle(cuda, oracle_mod, hidden, z, identity):
+    """hidden_dim other than 64 (the reference's constructor takes any, MGD:765; its min-sum factory's
+    default is 8, :1254): the check side of the generic fp32 kernels (group means, the tiled MLP with
+    the layer's own head), the same variable update and output; against the oracle at the same bar."""
+    H, dec, conv, types = setup(z, 3, 300 + hidden, hidden=hidden)
+    llr = torch.randn(5, H.shape[1]) * 2.0 + 1.0
+    Ac = None if identity else conv.check_to_var_adjacency
+    Av = None if identity else conv.var_to_check_adjacency
+    probs, _ = dec(llr.to(cuda), conv.message_to_var_index().to(cuda), types.to(cuda), Av, Ac)
     sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
     ref = oracle_mod.custom_variable_forward(sd, llr, conv.edge_var, conv.edge_chk, H.shape[1], H.shape[0],
                                              types=types, check_identity=identity)

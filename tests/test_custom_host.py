@@ -151,9 +151,12 @@ def test_variable_decoder_state_dict_layout_matches_reference():
     assert [len(sd[k].shape) and sd[k].numel() for k in sorted(sd)] == list(d["sdv_numel"])
 
 
-def test_variable_decoder_refuses_other_hidden_dims():
-    """The hybrid GNN's kernels are built for hidden_dim 64: other sizes are refused when the
-    decoder is constructed, with a message that says so (not at the first forward)."""
+def test_variable_decoder_hidden_dims():
+    """The reference's constructor takes any hidden_dim (MGD:765): this build runs 1 .. 1024 (64 on the
+    split-MFMA kernels, other widths on the tiled fp32 kernels) and refuses the rest when the decoder
+    is constructed, with a message that says so (not at the first forward)."""
     from ldpc_neural_decoder.models import CustomVariableMessageGNNDecoder
-    with pytest.raises(ValueError, match="hidden_dim 64"):
-        CustomVariableMessageGNNDecoder(40, 3, 32, 1, 3)
+    for h in (8, 32, 96, 1024):
+        CustomVariableMessageGNNDecoder(40, 3, h, 1, 3)
+    with pytest.raises(ValueError, match="hidden_dim 1 .. 1024"):
+        CustomVariableMessageGNNDecoder(40, 3, 2048, 1, 3)

@@ -1,0 +1,45 @@
+# Round-6 evidence: profiles + stamped PMC summaries of the workloads whose kernels changed this round
+# (the headline min-sum kernel is re-profiled on the same box as its bench line), then every bench line.
+# usage: TAG=r06 bash tools/gpu_evidence_r06.sh [profile|bench]
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R
+T=${TAG:-r06}; O=$R/gpurun_out/evidence_$T; mkdir -p $O
+summ() {  # workload kernel-substring per-call-kernel|- batch expected-read|- note
+  local W=$1 K=$2 PC=$3 B=$4 X=$5 N=$6 w=${1//-/_}
+  if [ "$PC" = "-" ]; then
+    python3 tools/pmc_summary.py gpurun_out/prof_${T}_${W} "$K" profiles/${T}_pmc_${w}.json $X > /dev/null || return 1
+  else
+    python3 tools/pmc_summary.py gpurun_out/prof_${T}_${W} "$K" profiles/${T}_pmc_${w}.json $X $PC > /dev/null || return 1
+  fi
+  python3 - profiles/${T}_pmc_${w}.json "$B" "$N" <<'PY' || return 1
+import json, sys
+f, b, note = sys.argv[1], float(sys.argv[2]), sys.argv[3]
+d = json.load(open(f)); d["batch"] = b
+if note: d["note"] = note
+json.dump(d, open(f, "w"), indent=1)
+PY
+  cp profiles/${T}_pmc_${w}.json $O/
+  mkdir -p $O/prof_${W}
+  cp gpurun_out/prof_${T}_${W}/trace/run_kernel_stats.csv $O/prof_${W}/kernel_stats.csv
+  cp gpurun_out/prof_${T}_${W}/lib_sha256.txt gpurun_out/prof_${T}_${W}/code_objects_sha256.txt $O/prof_${W}/
+  cp gpurun_out/prof_${T}_${W}/trace_bench.log $O/prof_${W}/trace_bench.json 2>/dev/null || true
+  python3 tools/pmc_kernels.py gpurun_out/prof_${T}_${W} > $O/prof_${W}/pmc_per_kernel.txt || true
+}
+if [ "${1:-profile}" = profile ]; then
+  bash tools/gpu_profile.sh minsum-z32 $T > $O/prof_minsum-z32.log 2>&1 || exit 1
+  summ minsum-z32 flood_fixed - 65536 436207616 "" || exit 1
+  bash tools/gpu_profile.sh gnn-z4 $T > $O/prof_gnn-z4.log 2>&1 || exit 1
+  summ gnn-z4 "gnn_|csr_" csr_count_kernel 4096 - "per call = one 5-layer fp32 GNN forward on B=4096 Z=4 frames (cfg2); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
+  bash tools/gpu_profile.sh gnn-z32 $T > $O/prof_gnn-z32.log 2>&1 || exit 1
+  summ gnn-z32 "gnn_|csr_" csr_count_kernel 10922.666666666666 - "per call = one fp32 GNN forward call on one workspace chunk (bench's B=32768 runs as 3 chunks of ~10923 frames); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
+  bash tools/gpu_profile.sh gnn-z32-h128 $T > $O/prof_gnn-z32-h128.log 2>&1 || exit 1
+  summ gnn-z32-h128 "gnn_|csr_" csr_count_kernel 2730.6666666666665 - "per call = one H=128 fp32 GNN forward call on one workspace chunk (B=8192 runs as 3 chunks); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
+  bash tools/gpu_profile.sh gnn-z32-bf16-i10 $T > $O/prof_gnn-z32-bf16-i10.log 2>&1 || exit 1
+  summ gnn-z32-bf16-i10 "gnn_|csr_" gnn_bf16_info_kernel 16384 - "per call = one 10-layer bf16 GNN forward on one 16384-frame chunk (B=32768 runs as 2 chunks); every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1
+  bash tools/gpu_profile.sh gnn-z32-bf16 $T > $O/prof_gnn-z32-bf16.log 2>&1 || exit 1
+  summ gnn-z32-bf16 "gnn_|csr_" gnn_bf16_info_kernel 16384 - "per call = one 15-layer bf16 GNN forward with per-frame early termination on one 16384-frame chunk (B=32768 runs as 2 chunks), random codewords at 2 dB; every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1
+  echo "profiles ok"
+else
+  bash tools/gpu_bench_all.sh || exit $?
+  mkdir -p $O/bench_all && cp gpurun_out/bench_all/*.json $O/bench_all/
+fi
