@@ -38,11 +38,11 @@ TOL = 2e-5
 KINDS = ("zero", "big", "posinf", "neginf", "nan", "mixed")
 
 
-def _model(z, layers, cuda, seed, precision="fp32", scale=0.5):
+def _model(z, layers, cuda, seed, precision="fp32", scale=0.5, hidden=64):
     torch.manual_seed(seed)
     base = load_base_matrix(code_path(z))
     H = expand_base_matrix(base, z)
-    dec, conv = create_message_gnn_decoder(H, num_iterations=layers, hidden_dim=64, base_graph=base, Z=z)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=layers, hidden_dim=hidden, base_graph=base, Z=z)
     with torch.no_grad():
         for p in dec.parameters():
             p.mul_(scale)
@@ -95,9 +95,12 @@ def _bf16_ok(p, ref):
     return d.mean() <= 5e-3 and agree >= 0.995, (float(d.mean()), float(agree))
 
 
-@pytest.mark.parametrize("precision,z,layers", [("fp32", 4, 3), ("fp32", 32, 3), ("bf16", 4, 3), ("bf16", 32, 3)])
-def test_special_llr_frames(cuda, oracle_mod, precision, z, layers):
-    base, H, dec, conv, types = _model(z, layers, cuda, seed=21)
+@pytest.mark.parametrize("precision,z,layers,hidden", [("fp32", 4, 3, 64), ("fp32", 32, 3, 64), ("bf16", 4, 3, 64),
+                                                      ("bf16", 32, 3, 64), ("fp32", 4, 3, 128), ("fp32", 4, 3, 40)])
+def test_special_llr_frames(cuda, oracle_mod, precision, z, layers, hidden):
+    """(hidden 128: the wide row GEMMs, whose per-row f16 scales come from recorded row maxima;
+    hidden 40: the tiled fp32 kernel)"""
+    base, H, dec, conv, types = _model(z, layers, cuda, seed=21, hidden=hidden)
     dec.precision = precision
     n = H.shape[1]
     ordinary, llr, where = _special_batch(n, 20, seed=z)
