@@ -42,4 +42,9 @@ if [ "${1:-profile}" = profile ]; then
 else
   bash tools/gpu_bench_all.sh || exit $?
   mkdir -p $O/bench_all && cp gpurun_out/bench_all/*.json $O/bench_all/
+  # the headline kernel under rocprof on the same box, right after its plain bench line
+  mkdir -p $O/headline && cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/headline/trace -o run -- python3 $R/bench.py --steps 20 --warmup 3 --cpu-baseline-seconds 0 > $O/headline/bench_under_rocprof.json 2> $O/headline/rocprof.err || exit $?
+  cd $R && timeout -k 10 120 python3 bench.py --steps 20 --warmup 3 --cpu-baseline-seconds 0 > $O/headline/bench_after.json 2>/dev/null || exit $?
+  echo "headline ok"
 fi
