@@ -490,7 +490,11 @@ struct ProjTiles {
     int first;  // tiles before `first` are skipped (the var-side tiles, for the check side alone)
 };
 
-template <int NT, bool HYB = false, bool F16 = true>
+// GEN = false (the row walk's launches): the generic gather of typed member rows is compiled out.
+// Under the row walk every tile takes another branch (check side: S_in; var side: memb_v; layer 0:
+// the LLRs), and that branch's registers (two members x 8 groups x float4 rows and their types in
+// flight) were what spilled the whole 12-wave kernel (20 VGPRs at the 168-VGPR budget).
+template <int NT, bool HYB = false, bool F16 = true, bool GEN = true>
 __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group_proj_kernel(GnnLayer P, ProjTiles T) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
@@ -616,7 +620,7 @@ __global__ __launch_bounds__(NT, (NT == 256 ? LDPC_PROJ_WPS : 2)) void gnn_group
                 *reinterpret_cast<float4 *>(gm + slot * kPS + c4) = mean;
             }
         } else {
-        if (P.x_in) {
+        if (GEN && P.x_in) {
             const float *xb = P.x_in + (int64_t)b * P.E * 64 + c4;
             const float *eb = lds + kPOffEmb + c4;
             int mi[8], mj[8];
@@ -2433,6 +2437,9 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
                                                 : reinterpret_cast<const void *>(gnn_group_proj_kernel<256, false, false>))
                               : (proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT>)
                                                 : reinterpret_cast<const void *>(gnn_group_proj_kernel<256>));
+    // the row walk's projection without the generic typed gather (see gnn_group_proj_kernel)
+    const void *proj_fn_rw = proj_nt != 256 ? reinterpret_cast<const void *>(gnn_group_proj_kernel<LDPC_PROJ_NT, false, true, false>)
+                                            : reinterpret_cast<const void *>(gnn_group_proj_kernel<256, false, true, false>);
     int mlp2_per_cu = 1, proj_per_cu = 1;
     if (proj) {
         if (mlp2_lds > 160 * 1024 || proj_lds > 160 * 1024)
@@ -2441,6 +2448,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
         // workgroups per CU: bounded by LDS and by kMlp2Wps waves per SIMD
         mlp2_per_cu = std::max<int>(1, std::min<int>(4 * kMlp2Wps / (kMlp2Nt / 64), (int)((160 * 1024) / mlp2_lds)));
         LDPC_HIP(hipFuncSetAttribute(proj_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
+        LDPC_HIP(hipFuncSetAttribute(proj_fn_rw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)proj_lds));
         LDPC_HIP(hipFuncSetAttribute(split ? (rw ? (pc_lds ? reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true, true>)
                                                            : reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false, true>))
                                                  : reinterpret_cast<const void *>(gnn_mlp2s_kernel<kMlp2sNt, kMlp2sWps, false>))
@@ -2544,7 +2552,14 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             const int64_t ptiles = nb * (int64_t)p->n_ptiles;
             const int pw = proj_nt / 64;
             const unsigned pgrid = (unsigned)std::min<int64_t>((ptiles + pw - 1) / pw, (int64_t)g_num_cus * proj_per_cu);
-            if (fp32_products && proj_nt != 256)
+            // the row walk's tiles never take the typed gather: without x_in they read the LLRs, with it
+            // the check side reads the sums S_in and the var side the mean embeddings memb_v (set above)
+            const bool gen = !(rw && L.memb_v && (!L.x_in || L.S_in));
+            if (!fp32_products && !gen && proj_nt != 256)
+                hipLaunchKernelGGL((gnn_group_proj_kernel<LDPC_PROJ_NT, false, true, false>), dim3(pgrid), dim3(LDPC_PROJ_NT), proj_lds, st, L, T);
+            else if (!fp32_products && !gen)
+                hipLaunchKernelGGL((gnn_group_proj_kernel<256, false, true, false>), dim3(pgrid), dim3(256), proj_lds, st, L, T);
+            else if (fp32_products && proj_nt != 256)
                 hipLaunchKernelGGL((gnn_group_proj_kernel<LDPC_PROJ_NT, false, false>), dim3(pgrid), dim3(LDPC_PROJ_NT), proj_lds, st, L, T);
             else if (fp32_products)
                 hipLaunchKernelGGL((gnn_group_proj_kernel<256, false, false>), dim3(pgrid), dim3(256), proj_lds, st, L, T);
