@@ -583,12 +583,15 @@ def main():
             per_launch_alg = (4 * 64 * 64 * E + 2 * 64 * 64 * g_m) * B * iters
             bound, unit, peak = "mfma", "TFLOP/s", FP32_MFMA_PEAK_TFS
         elif kind == "gnn" and hid != 64:
-            # gnn_wide.hip's row GEMMs (f16 two-term splits) are HBM-bound: SURVEY 8(d)'s per
-            # frame-layer bytes (3 passes over the (E, H) fp32 features + the group rows written and
-            # read) as the algorithmic figure; the design's own traffic (h round-trips HBM between
-            # GEMM1 and GEMM2) is in the notes
+            # gnn_wide.hip (f16 two-term splits) is HBM-bound: SURVEY 8(d)'s per frame-layer bytes (3
+            # passes over the (E, H) fp32 features + the group rows written and read) as the
+            # algorithmic figure; the design's own traffic in the notes: at H = 96 / 128 the fused MLP
+            # (x read twice, both sides' projected group rows gathered, y written: 5 E H words, + 3 (N +
+            # M) H for the group means and projections), else the row GEMMs (12 E H: h round-trips HBM
+            # between GEMM1 and GEMM2)
+            wide_fused = hid in (96, 128) and os.environ.get("LDPC_GNN_WIDE_FUSED", "1") != "0"
             per_launch_alg = (3 * E * hid * 4 + 2 * (g_n + g_m) * hid * 4) * B * iters
-            wide_design_bytes = (12 * E * hid * 4 + 3 * (g_n + g_m) * hid * 4) * B * iters
+            wide_design_bytes = ((5 if wide_fused else 12) * E * hid * 4 + 3 * (g_n + g_m) * hid * 4) * B * iters
             bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
         elif kind in ("gnn-sweep", "gnn"):
             # SURVEY 8(d) cfg2 / cfg4, HBM: per frame-layer 3 passes over the fp32 features (E x 64) +
@@ -704,8 +707,13 @@ def main():
                 notes["wide_design_bytes_per_launch"] = wide_design_bytes
                 notes["wide_design_GBps"] = wide_design_bytes / secs / 1e9
                 notes["wide_design_frac_of_hbm_peak"] = wide_design_bytes / secs / 1e9 / HBM_PEAK_GBS
-                notes["wide_products"] = ("scaled two-term f16 splits on v_mfma_f32_32x32x16_f16, one power of two "
+                notes["wide_products"] = ("scaled two-term f16 splits on v_mfma_f32_32x32x16_f16: one power of two "
+                                          "per weight matrix and per input row, h's per row and hidden slice under a "
+                                          "running exponent" if wide_fused else
+                                          "scaled two-term f16 splits on v_mfma_f32_32x32x16_f16, one power of two "
                                           "per weight slice and per input row (recorded by its producer)")
+                notes["wide_mlp"] = ("fused per 32-row tile (gnn_wide_mlp_kernel: GEMM1 -> GEMM2 -> head, h in "
+                                     "registers)" if wide_fused else "row GEMMs (gnn_wgemm_kernel), h through HBM")
             if split:
                 # gnn_mlp2s_kernel: the per-message products (8 H^2 E) as three f16 products each on the
                 # f16 MFMA (scaled two-term splits); the group projection (2 H^2 (N + M)) stays on the

@@ -1743,6 +1743,8 @@ bool wide_on(const ldpc_gnn_plan *p, int H) { return gnn_wide_supported(H) && !p
 struct Ws {
     float *xa, *xb, *Mv, *Mc, *msg_out, *wt;
     float *Pv, *Pc, *hbuf;  // wide path: projected group rows (B, G, H), MLP hidden rows (B, E, 2 H)
+    char *wimg;             // wide path, H = 96 / 128: every layer's fused-MLP slice images
+    int *wexp;              // ... and their weight exponents (2 per layer)
     uint32_t *xmax[2], *hmax, *gmax_v, *gmax_c;  // wide path: each row's largest |value| (f16 splits)
     float *S, *memb;  // row walk (H = 64, plan rw_*): per-check feature sums (B, Gc, H), mean type embeddings (L, Gc, H)
     float *memb_v;    // ... and per var group (L, Gv, H)
@@ -1792,7 +1794,11 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     w.hmax = wide ? reinterpret_cast<uint32_t *>(z + 2 * rm) : nullptr;
     w.gmax_v = wide ? reinterpret_cast<uint32_t *>(z + 3 * rm) : nullptr;
     w.gmax_c = wide ? reinterpret_cast<uint32_t *>(z + 3 * rm + gmv) : nullptr;
-    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb + (wide ? mv + mc + hb + 3 * rm + gmv + gmc : 0);
+    const int64_t fib = wide ? al(gnn_wide_fused_bytes(H, layers)) : 0, feb = fib ? al(2LL * layers * 4) : 0;
+    char *f = z + (wide ? 3 * rm + gmv + gmc : 0);
+    w.wimg = fib ? f : nullptr;
+    w.wexp = fib ? reinterpret_cast<int *>(f + fib) : nullptr;
+    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb + (wide ? mv + mc + hb + 3 * rm + gmv + gmc : 0) + fib + feb;
     return w;
 }
 
@@ -2465,6 +2471,10 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
                            layer_floats(H, types), d_msg_type, p->vg_ptr, p->vg_mem, p->inv_v, p->Gv, layers, w.memb_v);
         LDPC_CHECK_LAUNCH("gnn_memb_kernel");
     }
+    // wide H = 96 / 128 on f16 splits: every layer's fused-MLP slice images, once per call
+    const bool wfused = wide && !fp32_products && w.wimg && gnn_wide_fused_fits(H, types);
+    if (wfused)
+        if (int rc = gnn_wide_prep(H, layers, d_weights, layer_floats(H, types), types, w.wimg, w.wexp, s)) return rc;
     // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
     const GnnLayer L0 = L;
     auto run_range = [&](int64_t b0, int64_t nb, hipStream_t st) -> int {
@@ -2515,6 +2525,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             W.hmax = w.hmax + roff;
             W.gmax_v = w.gmax_v + b0 * p->Gv;
             W.gmax_c = w.gmax_c + b0 * p->Gc;
+            W.wimg = wfused ? w.wimg + (int64_t)l * (gnn_wide_fused_bytes(H, 1)) : nullptr;
+            W.wexp = wfused ? w.wexp + 2 * l : nullptr;
             if (int rc = gnn_wide_layer(W, st)) return rc;
             x_in = W.y;
             continue;

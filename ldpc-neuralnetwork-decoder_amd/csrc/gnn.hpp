@@ -126,9 +126,18 @@ struct GnnWideLayer {
     bool f16;
     const uint32_t *xmax_in;
     uint32_t *xmax_out, *hmax, *gmax_v, *gmax_c;
+    // H = 96 / 128 with f16 splits: this layer's fused-MLP slice images and weight exponents
+    // (gnn_wide_prep), or null for the row-GEMM sequence
+    const char *wimg;
+    const int *wexp;
 };
 bool gnn_wide_supported(int H);
 int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s);
+// bytes of every layer's fused-MLP slice images (0: this H runs the row GEMMs); whether the fused
+// kernel's LDS image holds T message types
+int64_t gnn_wide_fused_bytes(int H, int layers);
+bool gnn_wide_fused_fits(int H, int T);
+int gnn_wide_prep(int H, int layers, const float *blob, int64_t layer_floats, int T, char *wimg, int *wexp, hipStream_t s);
 
 // The per-device side stream and the calling thread's fork/join events the forwards split their
 // frames over (thread-safe: see gnn.hip).

@@ -18,7 +18,9 @@
 //                        h_s = relu(W1_s,left c + P_s[group(m)])        (mode GEMM1, per side)
 //                        y = W2_v h_v + W2_c h_c + b2_v + b2_c (+ x)    (mode GEMM2, K = 2 H)
 //   gnn_wide_head_kernel msg_out = wo . y + bo on the last layer (MGD:142, :270)
-// h (B, E, 2 H) fp32 is the one extra round trip through HBM.  Each launch is persistent: a
+// At H = 96 and 128 (round 6) GEMM1, GEMM2 and the head are one kernel, gnn_wide_mlp_kernel, that
+// keeps h in registers and streams the weights slice by slice (below); the other widths run the
+// row GEMMs, where h (B, E, 2 H) fp32 is the one extra round trip through HBM.  Each launch is persistent: a
 // workgroup holds one output slice's split images in LDS and its waves walk 32-row tiles; the
 // slices of one XCD walk the same tiles in step, so the input rows are read from HBM once per XCD
 // and hit L2 for the other slices (placement changes speed only, never results).
@@ -400,6 +402,270 @@ __global__ __launch_bounds__(256) void gnn_wide_head_kernel(const float *__restr
     if (q == 0) msg_out[r] = part + bo[0];
 }
 
+// ------------------------------------------------------------------------ fused MLP (H = 96, 128)
+// The layer's whole MLP per 32-row tile, h never leaving registers: for each slice of 32 hidden units
+// (side s, units 32 tt ..), h = relu(W1_s,left c + P_s[group]) on the tile (GEMM1, K = H), then its
+// contribution W2_s[:, slice] relu(h) to every output unit of y (GEMM2 over the slice's 32 columns).
+// The 2 H / 32 slices' split weight images (W1 rows of the slice, W2 columns of the slice; 38 KB at
+// H = 128) stream from a per-forward global copy (gnn_wide_prep_kernel) through a two-slot LDS ring
+// shared by the workgroup's eight waves, one barrier per slice; each wave owns one tile per pass.
+// Scales: the tile's c per row from its exact largest |c|; relu(h) per row and slice from the slice's
+// largest value, under a running exponent that only moves down (a larger slice maximum lowers it and
+// rescales y's accumulators by the exact power of two), so every slice's split is at least as fine
+// as one scale over the row's whole h would be.  This replaces GEMM1, GEMM2 and the head: h's
+// (B, E, 2 H) round trip through HBM (4 E H of the layer's 12 E H words) disappears.
+template <int H>
+struct WFused {
+    static constexpr int NT = H / 32;                  // 32-unit tiles per side (hidden or output)
+    static constexpr int S = 2 * NT;                   // slices per layer (both sides)
+    static constexpr int R1 = H + 8, R2 = 40;          // f16 per image row (W1: K = H; W2: K = 32) + pad
+    static constexpr int I1 = 32 * R1, I2 = H * R2;    // elements per split image
+    static constexpr int W2OFF = 2 * I1;               // W2's images after W1's two
+    // waves per workgroup (one workgroup per CU, two waves per SIMD)
+    static constexpr int NW = 8, NTH = 64 * NW;
+    // bytes per slice, padded to whole 1-KB LDS-DMA rounds of the workgroup's waves
+    static constexpr int BYTES = ((2 * I1 + 2 * I2) * 2 + 1024 * NW - 1) / (1024 * NW) * (1024 * NW);
+    static constexpr int KS = H / 16;                  // GEMM1 k-steps
+    static constexpr int ES = H + 4;                   // emb table row stride (floats)
+};
+
+// one workgroup per layer: both power-of-two weight scales, then every slice image of the layer
+template <int H>
+__global__ __launch_bounds__(1024) void gnn_wide_prep_kernel(const float *blob, int64_t layer_floats, int T,
+                                                              char *wimg, int *wexp) {
+    using F = WFused<H>;
+    __shared__ uint32_t m1b, m2b;
+    const int tid = threadIdx.x, l = blockIdx.x;
+    const float *w1v = blob + 2 * H + (int64_t)l * layer_floats + (int64_t)T * H;
+    const float *w2v = w1v + 2 * H * H + H, *w1c = w2v + H * H + H, *w2c = w1c + 2 * H * H + H;
+    if (tid == 0) { m1b = 0u; m2b = 0u; }
+    __syncthreads();
+    float m1 = 0.0f, m2 = 0.0f;
+    for (int i = tid; i < H * H; i += 1024) {
+        const int u = i / H, k = i - u * H;
+        m1 = fmaxf(m1, fmaxf(fabsf(w1v[u * 2 * H + k]), fabsf(w1c[u * 2 * H + k])));
+        m2 = fmaxf(m2, fmaxf(fabsf(w2v[i]), fabsf(w2c[i])));
+    }
+    atomicMax(&m1b, __float_as_uint(m1));
+    atomicMax(&m2b, __float_as_uint(m2));
+    __syncthreads();
+    const int e1 = min(col_exp(__uint_as_float(m1b)), 126), e2 = min(col_exp(__uint_as_float(m2b)), 126);
+    if (tid == 0) { wexp[2 * l] = e1; wexp[2 * l + 1] = e2; }
+    const float s1 = pow2f(e1), s2 = pow2f(e2);
+    _Float16 *base = reinterpret_cast<_Float16 *>(wimg + (int64_t)l * F::S * F::BYTES);
+    for (int sl = 0; sl < F::S; ++sl) {
+        const int side = sl / F::NT, tt = sl - side * F::NT;
+        const float *W1 = side ? w1c : w1v, *W2 = side ? w2c : w2v;
+        _Float16 *img = base + (int64_t)sl * (F::BYTES / 2);
+        // W1 rows: hidden unit 32 tt + r, column p = x unit pi16(p) (GEMM1's B operand order)
+        for (int i = tid; i < 32 * H; i += 1024) {
+            const int r = i / H, p = i - r * H;
+            split2h_store(W1[(32 * tt + r) * 2 * H + pi16(p)] * s1, img + r * F::R1 + p, F::I1);
+        }
+        // W2 columns of the slice: output unit o, column q = hidden unit 32 tt + pi16(q) (the order
+        // in which a lane's h accumulator registers feed GEMM2's B operand)
+        for (int i = tid; i < H * 32; i += 1024) {
+            const int o = i >> 5, q = i & 31;
+            split2h_store(W2[o * H + 32 * tt + pi16(q)] * s2, img + F::W2OFF + o * F::R2 + q, F::I2);
+        }
+    }
+}
+
+struct WMlp {
+    const char *wimg;   // this layer's slice images (gnn_wide_prep_kernel)
+    const int *wexp;    // this layer's {W1 scale, W2 scale} exponents
+    const float *x_in;  // (R, H), null at layer 0
+    const float *llr, *w_in, *b_in, *emb;
+    const int32_t *msg_type, *msg_var, *vgroup, *cgroup;
+    const float *Pv, *Pc;
+    const float *b2v, *b2c, *wo, *bo;
+    float *y, *msg_out;  // msg_out: the last layer's head (y then unused)
+    int residual, N, T, Gv, Gc;
+    int64_t E, R;
+};
+
+template <int H>
+inline size_t wide_mlp_lds_bytes(int T) { return 2 * (size_t)WFused<H>::BYTES + ((size_t)T * WFused<H>::ES + 4 * H) * 4; }
+
+template <int H>
+__global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A) {
+    using F = WFused<H>;
+    constexpr int NT = F::NT, S = F::S, KS = F::KS, NW = F::NW, NTH = F::NTH;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5, wave = tid >> 6;
+    float *tab = reinterpret_cast<float *>(smem + 2 * F::BYTES);
+    float *embs = tab, *win = tab + A.T * F::ES, *bin = win + H, *b2 = bin + H, *wo = b2 + H;
+    for (int i = tid; i < A.T * H; i += NTH) embs[(i / H) * F::ES + i % H] = A.emb[i];
+    for (int i = tid; i < H; i += NTH) {
+        win[i] = A.w_in[i];
+        bin[i] = A.b_in[i];
+        b2[i] = A.b2v[i] + A.b2c[i];
+        wo[i] = A.msg_out ? A.wo[i] : 0.0f;
+    }
+    constexpr int NF4 = F::BYTES / 16, CP = NF4 / NTH;  // float4 per slice, per thread (exact)
+    const float4 *gimg = reinterpret_cast<const float4 *>(A.wimg);
+    auto slot = [&](int64_t k) { return reinterpret_cast<float4 *>(smem + (k & 1) * F::BYTES); };
+    for (int i = tid; i < NF4; i += NTH) slot(0)[i] = gimg[i];
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int wexp1 = A.wexp[0], wexp2 = A.wexp[1];
+    const float bo = A.msg_out ? A.bo[0] : 0.0f;
+
+    // passes: this XCD's tiles, NW per pass (one per wave) per workgroup
+    const int64_t ntiles = (A.R + 31) / 32;
+    const int x = blockIdx.x % 8, rank = blockIdx.x / 8, nrank = gridDim.x / 8;
+    const int64_t t0 = ntiles * x / 8, t1 = ntiles * (x + 1) / 8;
+    const int64_t npass = (t1 - t0 + (int64_t)NW * nrank - 1) / ((int64_t)NW * nrank);
+    __syncthreads();
+    for (int64_t ps = 0; ps < npass; ++ps) {
+        const int64_t t = t0 + (ps * nrank + rank) * NW + wave;
+        const int64_t r = t * 32 + j;
+        const bool ok = t < t1 && r < A.R;
+        const int64_t rr = ok ? r : A.R - 1;  // past the end: a valid row, nothing written
+        const int64_t b = rr / A.E, m = rr - b * A.E;
+        const int ty = A.msg_type[m];
+        const float *pv = A.Pv + (b * A.Gv + A.vgroup[m]) * H + 4 * h, *pc = A.Pc + (b * A.Gc + A.cgroup[m]) * H + 4 * h;
+        // x in GEMM1's B operand order: x[s][e] = unit pi16(16 s + 8 h + e); layer 0 from the LLR
+        float xv[KS][8];
+        if (A.x_in) {
+            const float *xr = A.x_in + rr * H + 4 * h;
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const float4 v = *reinterpret_cast<const float4 *>(xr + 32 * (s >> 1) + 16 * (s & 1) + 8 * q);
+                    xv[s][4 * q] = v.x; xv[s][4 * q + 1] = v.y; xv[s][4 * q + 2] = v.z; xv[s][4 * q + 3] = v.w;
+                }
+        } else {
+            const float lv = A.llr[b * A.N + A.msg_var[m]];
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int u = pi16(16 * s + 8 * h + e);
+                    xv[s][e] = lv * win[u] + bin[u];
+                }
+        }
+        // y starts from b2v + b2c (+ x): register 4 q + i of tile ot is unit 32 ot + 8 q + 4 h + i
+        f32x16w y[NT];
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    y[ot][4 * q + i] = (A.residual ? xv[2 * ot + (q >> 1)][4 * (q & 1) + i] : 0.0f) + b2[32 * ot + 8 * q + 4 * h + i];
+        // c = x + emb[type] under the row's scale, split once for every slice
+        const float *eb = embs + ty * F::ES;
+        float cm = 0.0f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                xv[s][e] += eb[pi16(16 * s + 8 * h + e)];
+                cm = fmaxf(cm, fabsf(xv[s][e]));
+            }
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        const int cexp = col_exp_w(cm, wexp1);
+        const float csc = pow2f(cexp), asc = pow2f(cexp + wexp1), iasc = pow2f(-cexp - wexp1);
+        f16x8_t c0[KS], c1[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[s][e] *= csc;
+            split2h(xv[s], c0[s], c1[s]);
+        }
+        int erun = 1 << 20, ys = 0;  // relu(h)'s running exponent (none yet); y holds y_true 2^ys
+#pragma unroll 1
+        for (int sl = 0; sl < S; ++sl) {
+            const int64_t k = ps * S + sl;  // slice counter over the whole walk: ring slot k & 1
+            const bool more = k + 1 < npass * S;
+            const _Float16 *img = reinterpret_cast<const _Float16 *>(slot(k));
+            const int side = sl / NT, tt = sl - side * NT;
+            // GEMM1: the slice's 32 hidden units from the projected group row (loaded before the
+            // ring's copy is issued: waiting for it then does not wait for the copy)
+            f32x16w hacc;
+            {
+                const float *pr = (side ? pc : pv) + 32 * tt;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = *reinterpret_cast<const float4 *>(pr + 8 * q);
+                    hacc[4 * q] = v.x; hacc[4 * q + 1] = v.y; hacc[4 * q + 2] = v.z; hacc[4 * q + 3] = v.w;
+                }
+            }
+            // the next slice's image into the other ring slot by LDS-DMA, 1 KB per wave instruction
+            if (more) {
+                const float4 *src = gimg + (int64_t)((sl + 1) % S) * NF4 + lane;
+                char *dst = reinterpret_cast<char *>(slot(k + 1));
+#pragma unroll
+                for (int c = 0; c < CP; ++c) {
+                    const int q = c * NW + wv;  // this wave's 1-KB rounds
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + 64 * q),
+                                                     (__attribute__((address_space(3))) void *)(dst + 1024 * q), 16, 0, 0);
+                }
+            }
+            hacc *= asc;
+            const _Float16 *w1 = img + j * F::R1 + 8 * h;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) hacc = mfma3h(w1 + 16 * s, c0[s], c1[s], hacc, F::I1);
+            float hm = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                hacc[i] = relu_nan(hacc[i] * iasc);
+                hm = fmaxf(hm, hacc[i]);
+            }
+            hm = fmaxf(hm, __shfl_xor(hm, 32, 64));
+            // the running exponent moves down only; a zero slice leaves it (its split is exact anyway)
+            const int e = col_exp_w(hm, wexp2);
+            const int en = hm > 0.0f ? min(erun, e) : erun;
+            if (en != erun) {
+                const int d = en + wexp2 - ys;
+#pragma unroll
+                for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) y[ot][i] = ldexpf(y[ot][i], d);
+                ys = en + wexp2;
+                erun = en;
+            }
+            const float hsc = pow2f(erun < (1 << 20) ? erun : 0);
+            f16x8_t r0[2], r1[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                float hr[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) hr[i] = hacc[8 * a + i] * hsc;
+                split2h(hr, r0[a], r1[a]);
+            }
+            // GEMM2: this slice's 32 columns of W2_side into every output tile
+            const _Float16 *w2 = img + F::W2OFF + j * F::R2 + 8 * h;
+#pragma unroll
+            for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) y[ot] = mfma3h(w2 + 32 * ot * F::R2 + 16 * a, r0[a], r1[a], y[ot], F::I2);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the next image landed
+            __syncthreads();
+        }
+        // y back to scale; write it (and the head on the last layer)
+        float part = 0.0f;
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int u = 32 * ot + 8 * q + 4 * h;
+                float4 v = make_float4(ldexpf(y[ot][4 * q], -ys), ldexpf(y[ot][4 * q + 1], -ys),
+                                       ldexpf(y[ot][4 * q + 2], -ys), ldexpf(y[ot][4 * q + 3], -ys));
+                if (A.msg_out) {
+                    part += v.x * wo[u]; part += v.y * wo[u + 1]; part += v.z * wo[u + 2]; part += v.w * wo[u + 3];
+                } else if (ok) {
+                    *reinterpret_cast<float4 *>(A.y + rr * H + u) = v;
+                }
+            }
+        if (A.msg_out) {
+            part += __shfl_xor(part, 32, 64);
+            if (ok && h == 0) A.msg_out[rr] = part + bo;
+        }
+    }
+}
+
 int g_wcus = 0;
 
 template <int NT, int AH, bool F16>
@@ -449,9 +715,50 @@ int launch_wgemm(WArgs a, bool f16, hipStream_t s) {
     return LDPC_OK;
 }
 
+template <int H>
+int launch_wide_mlp(const WMlp &a, hipStream_t s) {
+    const size_t lds = wide_mlp_lds_bytes<H>(a.T);
+    if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the fused wide MLP's LDS image");
+    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_wide_mlp_kernel<H>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // one workgroup per CU, a multiple of the eight XCDs
+    const int64_t tiles = (a.R + 31) / 32;
+    const int per_x = (int)std::max<int64_t>(1, std::min<int64_t>(g_wcus / 8, (tiles + 8 * WFused<H>::NW - 1) / (8 * WFused<H>::NW)));
+    hipLaunchKernelGGL(gnn_wide_mlp_kernel<H>, dim3(8 * per_x), dim3(WFused<H>::NTH), lds, s, a);
+    LDPC_CHECK_LAUNCH("gnn_wide_mlp_kernel");
+    return LDPC_OK;
+}
+
 }  // namespace
 
 bool gnn_wide_supported(int H) { return H != 64 && H % 32 == 0 && H >= 96 && H <= 256; }
+
+// LDPC_GNN_WIDE_FUSED=0: the row-GEMM sequence at H = 96 / 128 too (A/B)
+int64_t gnn_wide_fused_bytes(int H, int layers) {
+    static const bool on = [] {
+        const char *e = std::getenv("LDPC_GNN_WIDE_FUSED");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (!on) return 0;
+    if (H == 96) return (int64_t)layers * WFused<96>::S * WFused<96>::BYTES;
+    if (H == 128) return (int64_t)layers * WFused<128>::S * WFused<128>::BYTES;
+    return 0;
+}
+
+bool gnn_wide_fused_fits(int H, int T) {
+    return H == 96 ? wide_mlp_lds_bytes<96>(T) <= 160 * 1024 : H == 128 && wide_mlp_lds_bytes<128>(T) <= 160 * 1024;
+}
+
+int gnn_wide_prep(int H, int layers, const float *blob, int64_t layer_floats, int T, char *wimg, int *wexp, hipStream_t s) {
+    if (H == 96)
+        hipLaunchKernelGGL(gnn_wide_prep_kernel<96>, dim3(layers), dim3(1024), 0, s, blob, layer_floats, T, wimg, wexp);
+    else if (H == 128)
+        hipLaunchKernelGGL(gnn_wide_prep_kernel<128>, dim3(layers), dim3(1024), 0, s, blob, layer_floats, T, wimg, wexp);
+    else
+        return fail(LDPC_EINVAL, "fused wide MLP: H must be 96 or 128");
+    LDPC_CHECK_LAUNCH("gnn_wide_prep_kernel");
+    return LDPC_OK;
+}
 
 int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
     const int H = L.H;
@@ -494,6 +801,23 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         a.out_stride = H;
         a.in_max = side ? L.gmax_c : L.gmax_v;
         if (int rc = launch_wgemm(a, L.f16, s)) return rc;
+    }
+    if (L.wimg) {  // H = 96 / 128: GEMM1 -> GEMM2 (-> head) fused per tile
+        if (!g_wcus) {
+            int dev = 0;
+            LDPC_HIP(hipGetDevice(&dev));
+            LDPC_HIP(hipDeviceGetAttribute(&g_wcus, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        WMlp a{};
+        a.wimg = L.wimg; a.wexp = L.wexp;
+        a.x_in = L.x_in; a.llr = L.llr; a.w_in = L.w_in; a.b_in = L.b_in; a.emb = L.emb;
+        a.msg_type = L.msg_type; a.msg_var = L.msg_var; a.vgroup = L.plan->vgroup; a.cgroup = L.plan->cgroup;
+        a.Pv = L.Pv; a.Pc = L.Pc;
+        a.b2v = L.b2v; a.b2c = L.b2c; a.wo = L.wo; a.bo = L.bo;
+        a.y = L.y; a.msg_out = L.msg_out;
+        a.residual = L.residual; a.N = L.N; a.T = L.T; a.Gv = L.plan->Gv; a.Gc = L.plan->Gc;
+        a.E = L.E; a.R = BE;
+        return H == 96 ? launch_wide_mlp<96>(a, s) : launch_wide_mlp<128>(a, s);
     }
     // h_s = relu(W1_s,left c + P_s[group]) into h (B E, 2 H); both sides' row maxima into hmax
     if (L.f16) LDPC_HIP(hipMemsetAsync(L.hmax, 0, (size_t)BE * 4, s));
