@@ -26,7 +26,8 @@ Workloads (BASELINE.json configs):
               per-frame early-termination syndrome check after every layer (avg_layers reported)
   gnn-z32-bf16-i10  cfg4 shape (10 layers) on the bf16 path: the north-star "10 iterations" GNN line
   gnn-z32-h128  cfg4's code and depth at hidden_dim 128 (the reference builds any width, MGD:22/:162):
-              the MFMA row GEMMs of gnn_wide.hip, fp32, random weights
+              gnn_wide.hip (group means, projections, the fused per-tile MLP), fp32, random weights
+  gnn-z32-h192  the same at hidden_dim 192 (the fused MLP at one wave per SIMD)
   gnn-z32-sweep  cfg4 as BASELINE states it: the on-device SNR sweep 0..6 dB step 1 (sweep.py
               evaluate_message_gnn = run_comparison_all.py:245-295), fp32, B frames per GPU per SNR;
               one step = one whole sweep (channel + decode + counters, RCCL all-reduce at the end)
@@ -58,7 +59,7 @@ VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 VALU instructions/s (1e9): 1024 SIMDs
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X fp32 matrix (spec), same guide
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X bf16 dense MFMA (spec, no sparsity)
 
-HIDDEN = {"gnn-z32-h128": 128}  # hidden_dim of the GNN workloads (default 64)
+HIDDEN = {"gnn-z32-h128": 128, "gnn-z32-h192": 192}  # hidden_dim of the GNN workloads (default 64)
 
 WORKLOADS = {
     # name: (decoder, Z, iterations, default batch per GPU, SNR dB)
@@ -70,6 +71,7 @@ WORKLOADS = {
     "gnn-z4": ("gnn", 4, 5, 4096, 2.0),
     "gnn-z32": ("gnn", 32, 10, 32768, 2.0),
     "gnn-z32-h128": ("gnn", 32, 10, 8192, 2.0),
+    "gnn-z32-h192": ("gnn", 32, 10, 8192, 2.0),
     "gnn-z32-bf16": ("gnn-bf16", 32, 15, 32768, 2.0),
     "gnn-z4-bf16": ("gnn-bf16", 4, 5, 4096, 2.0),
     "gnn-z32-bf16-i10": ("gnn-bf16", 32, 10, 32768, 2.0),
@@ -123,6 +125,7 @@ PMC_KERNEL_SYMBOL = {
     "gnn-z32-bf16": "gnn_bf16_mlp_kernel",
     "gnn-z32-bf16-i10": "gnn_bf16_mlp_kernel",
     "gnn-z32-h128": "gnn_wide",
+    "gnn-z32-h192": "gnn_wide",
     "lay-z32": "check_group",
     # the fp32 GNN's dominant kernels (projection + split MLP) share gnn.hip's code object
     "gnn-z32": "gnn_mlp2s_kernel",
@@ -589,7 +592,8 @@ def main():
             # (x read twice, both sides' projected group rows gathered, y written: 5 E H words, + 3 (N +
             # M) H for the group means and projections), else the row GEMMs (12 E H: h round-trips HBM
             # between GEMM1 and GEMM2)
-            wide_fused = hid in (96, 128) and os.environ.get("LDPC_GNN_WIDE_FUSED", "1") != "0"
+            wide_fused = (hid in (96, 128, 160, 192) and os.environ.get("LDPC_GNN_WIDE_FUSED", "1") != "0"
+                          and hid <= int(os.environ.get("LDPC_GNN_WIDE_FUSED_MAX", "192")))
             per_launch_alg = (3 * E * hid * 4 + 2 * (g_n + g_m) * hid * 4) * B * iters
             wide_design_bytes = ((5 if wide_fused else 12) * E * hid * 4 + 3 * (g_n + g_m) * hid * 4) * B * iters
             bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS

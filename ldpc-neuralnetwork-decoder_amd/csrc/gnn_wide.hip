@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256) void gnn_wide_head_kernel(const float *__restr
     if (q == 0) msg_out[r] = part + bo[0];
 }
 
-// ------------------------------------------------------------------------ fused MLP (H = 96, 128)
+// ------------------------------------------------------------------------ fused MLP (H = 96 .. 192)
 // The layer's whole MLP per 32-row tile, h never leaving registers: for each slice of 32 hidden units
 // (side s, units 32 tt ..), h = relu(W1_s,left c + P_s[group]) on the tile (GEMM1, K = H), then its
 // contribution W2_s[:, slice] relu(h) to every output unit of y (GEMM2 over the slice's 32 columns).
@@ -421,8 +421,9 @@ struct WFused {
     static constexpr int R1 = H + 8, R2 = 40;          // f16 per image row (W1: K = H; W2: K = 32) + pad
     static constexpr int I1 = 32 * R1, I2 = H * R2;    // elements per split image
     static constexpr int W2OFF = 2 * I1;               // W2's images after W1's two
-    // waves per workgroup (one workgroup per CU, two waves per SIMD)
-    static constexpr int NW = 8, NTH = 64 * NW;
+    // waves per workgroup (one workgroup per CU): two per SIMD up to H = 128; past it the tile's y
+    // and c split (H / 2 registers each) need one wave per SIMD's 512 registers
+    static constexpr int NW = H <= 128 ? 8 : 4, NTH = 64 * NW;
     // bytes per slice, padded to whole 1-KB LDS-DMA rounds of the workgroup's waves
     static constexpr int BYTES = ((2 * I1 + 2 * I2) * 2 + 1024 * NW - 1) / (1024 * NW) * (1024 * NW);
     static constexpr int KS = H / 16;                  // GEMM1 k-steps
@@ -734,28 +735,53 @@ int launch_wide_mlp(const WMlp &a, hipStream_t s) {
 bool gnn_wide_supported(int H) { return H != 64 && H % 32 == 0 && H >= 96 && H <= 256; }
 
 // LDPC_GNN_WIDE_FUSED=0: the row-GEMM sequence at H = 96 / 128 too (A/B)
+// LDPC_GNN_WIDE_FUSED_MAX=n: the fused MLP up to H = n (96, 128, 160 or 192; default 192)
+int fused_max_h() {
+    static const int v = [] {
+        const char *e = std::getenv("LDPC_GNN_WIDE_FUSED_MAX");
+        return e ? std::atoi(e) : 192;
+    }();
+    return v;
+}
+
 int64_t gnn_wide_fused_bytes(int H, int layers) {
     static const bool on = [] {
         const char *e = std::getenv("LDPC_GNN_WIDE_FUSED");
         return !e || std::atoi(e) != 0;
     }();
-    if (!on) return 0;
-    if (H == 96) return (int64_t)layers * WFused<96>::S * WFused<96>::BYTES;
-    if (H == 128) return (int64_t)layers * WFused<128>::S * WFused<128>::BYTES;
-    return 0;
+    if (!on || H > fused_max_h()) return 0;
+    switch (H) {
+        case 96: return (int64_t)layers * WFused<96>::S * WFused<96>::BYTES;
+        case 128: return (int64_t)layers * WFused<128>::S * WFused<128>::BYTES;
+        case 160: return (int64_t)layers * WFused<160>::S * WFused<160>::BYTES;
+        case 192: return (int64_t)layers * WFused<192>::S * WFused<192>::BYTES;
+        default: return 0;
+    }
 }
 
 bool gnn_wide_fused_fits(int H, int T) {
-    return H == 96 ? wide_mlp_lds_bytes<96>(T) <= 160 * 1024 : H == 128 && wide_mlp_lds_bytes<128>(T) <= 160 * 1024;
+    switch (H) {
+        case 96: return wide_mlp_lds_bytes<96>(T) <= 160 * 1024;
+        case 128: return wide_mlp_lds_bytes<128>(T) <= 160 * 1024;
+        case 160: return wide_mlp_lds_bytes<160>(T) <= 160 * 1024;
+        case 192: return wide_mlp_lds_bytes<192>(T) <= 160 * 1024;
+        default: return false;
+    }
+}
+
+template <int H>
+void go_prep(int layers, const float *blob, int64_t layer_floats, int T, char *wimg, int *wexp, hipStream_t s) {
+    hipLaunchKernelGGL(gnn_wide_prep_kernel<H>, dim3(layers), dim3(1024), 0, s, blob, layer_floats, T, wimg, wexp);
 }
 
 int gnn_wide_prep(int H, int layers, const float *blob, int64_t layer_floats, int T, char *wimg, int *wexp, hipStream_t s) {
-    if (H == 96)
-        hipLaunchKernelGGL(gnn_wide_prep_kernel<96>, dim3(layers), dim3(1024), 0, s, blob, layer_floats, T, wimg, wexp);
-    else if (H == 128)
-        hipLaunchKernelGGL(gnn_wide_prep_kernel<128>, dim3(layers), dim3(1024), 0, s, blob, layer_floats, T, wimg, wexp);
-    else
-        return fail(LDPC_EINVAL, "fused wide MLP: H must be 96 or 128");
+    switch (H) {
+        case 96: go_prep<96>(layers, blob, layer_floats, T, wimg, wexp, s); break;
+        case 128: go_prep<128>(layers, blob, layer_floats, T, wimg, wexp, s); break;
+        case 160: go_prep<160>(layers, blob, layer_floats, T, wimg, wexp, s); break;
+        case 192: go_prep<192>(layers, blob, layer_floats, T, wimg, wexp, s); break;
+        default: return fail(LDPC_EINVAL, "fused wide MLP: H must be 96, 128, 160 or 192");
+    }
     LDPC_CHECK_LAUNCH("gnn_wide_prep_kernel");
     return LDPC_OK;
 }
@@ -817,7 +843,12 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         a.y = L.y; a.msg_out = L.msg_out;
         a.residual = L.residual; a.N = L.N; a.T = L.T; a.Gv = L.plan->Gv; a.Gc = L.plan->Gc;
         a.E = L.E; a.R = BE;
-        return H == 96 ? launch_wide_mlp<96>(a, s) : launch_wide_mlp<128>(a, s);
+        switch (H) {
+            case 96: return launch_wide_mlp<96>(a, s);
+            case 128: return launch_wide_mlp<128>(a, s);
+            case 160: return launch_wide_mlp<160>(a, s);
+            default: return launch_wide_mlp<192>(a, s);
+        }
     }
     // h_s = relu(W1_s,left c + P_s[group]) into h (B E, 2 H); both sides' row maxima into hmax
     if (L.f16) LDPC_HIP(hipMemsetAsync(L.hmax, 0, (size_t)BE * 4, s));

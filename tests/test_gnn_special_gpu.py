@@ -180,12 +180,14 @@ def test_split_mlp_fp32_accurate_wide_range(cuda, oracle_mod, monkeypatch, weigh
 
 
 @pytest.mark.parametrize("weights", ["normal", "spread"])
-@pytest.mark.parametrize("hidden", [128, 96])
+@pytest.mark.parametrize("hidden", [128, 96, 192, 224])
 def test_wide_split_fp32_accurate(cuda, oracle_mod, weights, hidden):
-    """hidden_dim 96 / 128 (csrc/gnn_wide.hip): the row GEMMs on scaled two-term f16 splits (each
-    input row scaled by the largest |value| its producer recorded) are fp32-accurate -- error against
-    the float64 oracle within 2x the fp32 oracle's own, + 1e-7; with weights beyond the splits' range
-    the decoder takes the three-term bf16 form (LDPC_GNN_FP32_PRODUCTS), at the same bar."""
+    """hidden_dim 96 / 128 / 192 (csrc/gnn_wide.hip's fused MLP: c split per row from its exact
+    largest |c|, relu(h) per row and hidden slice under a running exponent) and 224 (the row GEMMs:
+    each input row scaled by the largest |value| its producer recorded), both on scaled two-term f16
+    splits, are fp32-accurate -- error against the float64 oracle within 2x the fp32 oracle's own,
+    + 1e-7; with weights beyond the splits' range the decoder takes the three-term bf16 row GEMMs
+    (LDPC_GNN_FP32_PRODUCTS), at the same bar."""
     base, H, dec, conv, types = _model(32, 4, cuda, seed=40 + hidden)
     from ldpc_neural_decoder.models import create_message_gnn_decoder as _c
     torch.manual_seed(40 + hidden)
