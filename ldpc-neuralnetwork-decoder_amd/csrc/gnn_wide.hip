@@ -430,6 +430,19 @@ struct WFused {
     static constexpr int ES = H + 4;                   // emb table row stride (floats)
 };
 
+// One 16-B LDS-DMA load per lane: the wave's 64 lanes' 16 B land at LDS byte address lds (wave
+// uniform) + 16 lane.  Inline asm, because hipcc waits for a builtin LDS-DMA before every later
+// ds_read it cannot prove disjoint (here: each weight read of the other ring slot), which drains the
+// copy as soon as it is issued; the caller counts completion itself (s_waitcnt vmcnt, then a barrier).
+// M0 is the compiler's: saved and restored inside the statement.
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds)
+                 : "memory");
+}
+
 // one workgroup per layer: both power-of-two weight scales, then every slice image of the layer
 template <int H>
 __global__ __launch_bounds__(1024) void gnn_wide_prep_kernel(const float *blob, int64_t layer_floats, int T,
@@ -488,7 +501,8 @@ struct WMlp {
 template <int H>
 inline size_t wide_mlp_lds_bytes(int T) { return 2 * (size_t)WFused<H>::BYTES + ((size_t)T * WFused<H>::ES + 4 * H) * 4; }
 
-template <int H>
+// L0: layer 0 (x from the LLRs; no x rows to prefetch)
+template <int H, bool L0>
 __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A) {
     using F = WFused<H>;
     constexpr int NT = F::NT, S = F::S, KS = F::KS, NW = F::NW, NTH = F::NTH;
@@ -508,6 +522,7 @@ __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A)
     auto slot = [&](int64_t k) { return reinterpret_cast<float4 *>(smem + (k & 1) * F::BYTES); };
     for (int i = tid; i < NF4; i += NTH) slot(0)[i] = gimg[i];
     const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)smem;
     const int wexp1 = A.wexp[0], wexp2 = A.wexp[1];
     const float bo = A.msg_out ? A.bo[0] : 0.0f;
 
@@ -517,33 +532,50 @@ __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A)
     const int64_t t0 = ntiles * x / 8, t1 = ntiles * (x + 1) / 8;
     const int64_t npass = (t1 - t0 + (int64_t)NW * nrank - 1) / ((int64_t)NW * nrank);
     __syncthreads();
+    // a pass's row: tile t = t0 + (ps nrank + rank) NW + wave, slot j (past the end: a valid row,
+    // nothing written); the index loads for the next pass are issued a pass ahead
+    struct Ctx {
+        int64_t rr;
+        bool ok;
+        int ty;
+        const float *pv, *pc;
+        float lv;
+    };
+    auto ctx_of = [&](int64_t ps) {
+        Ctx c;
+        const int64_t t = t0 + (ps * nrank + rank) * NW + wave, r = t * 32 + j;
+        c.ok = t < t1 && r < A.R;
+        c.rr = c.ok ? r : A.R - 1;
+        const int64_t b = c.rr / A.E, m = c.rr - b * A.E;
+        c.ty = A.msg_type[m];
+        c.pv = A.Pv + (b * A.Gv + A.vgroup[m]) * H + 4 * h;
+        c.pc = A.Pc + (b * A.Gc + A.cgroup[m]) * H + 4 * h;
+        c.lv = L0 ? A.llr[b * A.N + A.msg_var[m]] : 0.0f;
+        return c;
+    };
+    // x in GEMM1's B operand order: x[s][e] = unit pi16(16 s + 8 h + e)
+    float xv[KS][8];
+    auto load_x = [&](const Ctx &c) {
+        const float *xr = A.x_in + c.rr * H + 4 * h;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float4 v = *reinterpret_cast<const float4 *>(xr + 32 * (s >> 1) + 16 * (s & 1) + 8 * q);
+                xv[s][4 * q] = v.x; xv[s][4 * q + 1] = v.y; xv[s][4 * q + 2] = v.z; xv[s][4 * q + 3] = v.w;
+            }
+    };
+    Ctx cur = ctx_of(0);
+    if (!L0 && npass > 0) load_x(cur);
     for (int64_t ps = 0; ps < npass; ++ps) {
-        const int64_t t = t0 + (ps * nrank + rank) * NW + wave;
-        const int64_t r = t * 32 + j;
-        const bool ok = t < t1 && r < A.R;
-        const int64_t rr = ok ? r : A.R - 1;  // past the end: a valid row, nothing written
-        const int64_t b = rr / A.E, m = rr - b * A.E;
-        const int ty = A.msg_type[m];
-        const float *pv = A.Pv + (b * A.Gv + A.vgroup[m]) * H + 4 * h, *pc = A.Pc + (b * A.Gc + A.cgroup[m]) * H + 4 * h;
-        // x in GEMM1's B operand order: x[s][e] = unit pi16(16 s + 8 h + e); layer 0 from the LLR
-        float xv[KS][8];
-        if (A.x_in) {
-            const float *xr = A.x_in + rr * H + 4 * h;
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const float4 v = *reinterpret_cast<const float4 *>(xr + 32 * (s >> 1) + 16 * (s & 1) + 8 * q);
-                    xv[s][4 * q] = v.x; xv[s][4 * q + 1] = v.y; xv[s][4 * q + 2] = v.z; xv[s][4 * q + 3] = v.w;
-                }
-        } else {
-            const float lv = A.llr[b * A.N + A.msg_var[m]];
+        const Ctx nxt = ctx_of(ps + 1 < npass ? ps + 1 : ps);
+        if (L0) {  // layer 0: x = Linear(1, H) of the message's LLR
 #pragma unroll
             for (int s = 0; s < KS; ++s)
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const int u = pi16(16 * s + 8 * h + e);
-                    xv[s][e] = lv * win[u] + bin[u];
+                    xv[s][e] = cur.lv * win[u] + bin[u];
                 }
         }
         // y starts from b2v + b2c (+ x): register 4 q + i of tile ot is unit 32 ot + 8 q + 4 h + i
@@ -556,7 +588,7 @@ __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A)
                 for (int i = 0; i < 4; ++i)
                     y[ot][4 * q + i] = (A.residual ? xv[2 * ot + (q >> 1)][4 * (q & 1) + i] : 0.0f) + b2[32 * ot + 8 * q + 4 * h + i];
         // c = x + emb[type] under the row's scale, split once for every slice
-        const float *eb = embs + ty * F::ES;
+        const float *eb = embs + cur.ty * F::ES;
         float cm = 0.0f;
 #pragma unroll
         for (int s = 0; s < KS; ++s)
@@ -576,32 +608,36 @@ __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A)
             split2h(xv[s], c0[s], c1[s]);
         }
         int erun = 1 << 20, ys = 0;  // relu(h)'s running exponent (none yet); y holds y_true 2^ys
-#pragma unroll 1
-        for (int sl = 0; sl < S; ++sl) {
-            const int64_t k = ps * S + sl;  // slice counter over the whole walk: ring slot k & 1
-            const bool more = k + 1 < npass * S;
-            const _Float16 *img = reinterpret_cast<const _Float16 *>(slot(k));
+        // the slice's projected group row (its 32 hidden units), one slice ahead
+        auto prow = [&](int sl, f32x16w &v) {
             const int side = sl / NT, tt = sl - side * NT;
-            // GEMM1: the slice's 32 hidden units from the projected group row (loaded before the
-            // ring's copy is issued: waiting for it then does not wait for the copy)
-            f32x16w hacc;
-            {
-                const float *pr = (side ? pc : pv) + 32 * tt;
+            const float *pr = (side ? cur.pc : cur.pv) + 32 * tt;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 v = *reinterpret_cast<const float4 *>(pr + 8 * q);
-                    hacc[4 * q] = v.x; hacc[4 * q + 1] = v.y; hacc[4 * q + 2] = v.z; hacc[4 * q + 3] = v.w;
-                }
+            for (int q = 0; q < 4; ++q) {
+                const float4 f = *reinterpret_cast<const float4 *>(pr + 8 * q);
+                v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
             }
+        };
+        f32x16w pnext;
+        prow(0, pnext);
+        // A slice in two halves: GEMM1 -> relu(h)'s split (r0, r1), then GEMM2 + the ring's barrier.
+        // Between them on the pass's last slice, c's registers are free and the next pass's x rows
+        // are loaded into them (after the ring copy: the barrier's wait then leaves them in flight)
+        auto gemm1 = [&](int sl, f16x8_t (&r0)[2], f16x8_t (&r1)[2]) {
+            const int64_t k = ps * S + sl;  // slice counter over the whole walk: ring slot k & 1
+            const _Float16 *img = reinterpret_cast<const _Float16 *>(slot(k));
+            // GEMM1 starts from the slice's projected group row; the next slice's row is loaded
+            // before the ring's copy is issued (waiting for it then does not wait for the copy)
+            f32x16w hacc = pnext;
+            if (sl + 1 < S) prow(sl + 1, pnext);
             // the next slice's image into the other ring slot by LDS-DMA, 1 KB per wave instruction
-            if (more) {
+            if (k + 1 < npass * S) {
                 const float4 *src = gimg + (int64_t)((sl + 1) % S) * NF4 + lane;
-                char *dst = reinterpret_cast<char *>(slot(k + 1));
+                const uint32_t dst = lds_base + (uint32_t)((k + 1) & 1) * F::BYTES;
 #pragma unroll
                 for (int c = 0; c < CP; ++c) {
                     const int q = c * NW + wv;  // this wave's 1-KB rounds
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + 64 * q),
-                                                     (__attribute__((address_space(3))) void *)(dst + 1024 * q), 16, 0, 0);
+                    glds16(src + 64 * q, __builtin_amdgcn_readfirstlane(dst + 1024 * q));
                 }
             }
             hacc *= asc;
@@ -628,7 +664,6 @@ __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A)
                 erun = en;
             }
             const float hsc = pow2f(erun < (1 << 20) ? erun : 0);
-            f16x8_t r0[2], r1[2];
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
                 float hr[8];
@@ -636,14 +671,37 @@ __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A)
                 for (int i = 0; i < 8; ++i) hr[i] = hacc[8 * a + i] * hsc;
                 split2h(hr, r0[a], r1[a]);
             }
-            // GEMM2: this slice's 32 columns of W2_side into every output tile
+        };
+        // GEMM2: the slice's 32 columns of W2_side into every output tile, then the ring's barrier
+        // (vmcnt: the loads issued after the ring copy may stay in flight)
+        auto gemm2 = [&](int sl, const f16x8_t (&r0)[2], const f16x8_t (&r1)[2], bool xpre) {
+            const _Float16 *img = reinterpret_cast<const _Float16 *>(slot(ps * S + sl));
             const _Float16 *w2 = img + F::W2OFF + j * F::R2 + 8 * h;
 #pragma unroll
             for (int ot = 0; ot < NT; ++ot)
 #pragma unroll
                 for (int a = 0; a < 2; ++a) y[ot] = mfma3h(w2 + 32 * ot * F::R2 + 16 * a, r0[a], r1[a], y[ot], F::I2);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the next image landed
+            if (xpre)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");  // the 2 KS x loads are the youngest
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the next image landed
             __syncthreads();
+        };
+#pragma unroll 1
+        for (int sl = 0; sl < S - 1; ++sl) {
+            f16x8_t r0[2], r1[2];
+            gemm1(sl, r0, r1);
+            gemm2(sl, r0, r1, false);
+        }
+        {
+            f16x8_t r0[2], r1[2];
+            gemm1(S - 1, r0, r1);
+            if (!L0) {  // (the last pass loads its own rows again: a valid address, discarded)
+                __builtin_amdgcn_sched_barrier(0);  // the x loads stay after the ring copy's
+                load_x(nxt);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            gemm2(S - 1, r0, r1, !L0);
         }
         // y back to scale; write it (and the head on the last layer)
         float part = 0.0f;
@@ -656,14 +714,15 @@ __global__ __launch_bounds__(WFused<H>::NTH, 1) void gnn_wide_mlp_kernel(WMlp A)
                                        ldexpf(y[ot][4 * q + 2], -ys), ldexpf(y[ot][4 * q + 3], -ys));
                 if (A.msg_out) {
                     part += v.x * wo[u]; part += v.y * wo[u + 1]; part += v.z * wo[u + 2]; part += v.w * wo[u + 3];
-                } else if (ok) {
-                    *reinterpret_cast<float4 *>(A.y + rr * H + u) = v;
+                } else if (cur.ok) {
+                    *reinterpret_cast<float4 *>(A.y + cur.rr * H + u) = v;
                 }
             }
         if (A.msg_out) {
             part += __shfl_xor(part, 32, 64);
-            if (ok && h == 0) A.msg_out[rr] = part + bo;
+            if (cur.ok && h == 0) A.msg_out[cur.rr] = part + bo;
         }
+        cur = nxt;
     }
 }
 
@@ -720,12 +779,16 @@ template <int H>
 int launch_wide_mlp(const WMlp &a, hipStream_t s) {
     const size_t lds = wide_mlp_lds_bytes<H>(a.T);
     if (lds > 160 * 1024) return fail(LDPC_EUNSUPPORTED, "too many message types for the fused wide MLP's LDS image");
-    LDPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gnn_wide_mlp_kernel<H>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const void *fn = a.x_in ? reinterpret_cast<const void *>(gnn_wide_mlp_kernel<H, false>)
+                            : reinterpret_cast<const void *>(gnn_wide_mlp_kernel<H, true>);
+    LDPC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // one workgroup per CU, a multiple of the eight XCDs
     const int64_t tiles = (a.R + 31) / 32;
     const int per_x = (int)std::max<int64_t>(1, std::min<int64_t>(g_wcus / 8, (tiles + 8 * WFused<H>::NW - 1) / (8 * WFused<H>::NW)));
-    hipLaunchKernelGGL(gnn_wide_mlp_kernel<H>, dim3(8 * per_x), dim3(WFused<H>::NTH), lds, s, a);
+    if (a.x_in)
+        hipLaunchKernelGGL((gnn_wide_mlp_kernel<H, false>), dim3(8 * per_x), dim3(WFused<H>::NTH), lds, s, a);
+    else
+        hipLaunchKernelGGL((gnn_wide_mlp_kernel<H, true>), dim3(8 * per_x), dim3(WFused<H>::NTH), lds, s, a);
     LDPC_CHECK_LAUNCH("gnn_wide_mlp_kernel");
     return LDPC_OK;
 }
