@@ -261,8 +261,11 @@ __device__ __forceinline__ int col_exp(float m) {
 // ... for an activation column multiplied by weights scaled 2^wexp: clamped so that the product scale
 // 2^(e + wexp) and its inverse stay normal floats, so csc * wsc, asc and iasc invert each other
 // exactly.  The upper clamp only lowers the column's scale (its split stays in range);
-// the lower one binds only where the fp32 products themselves overflow.
-__device__ __forceinline__ int col_exp_w(float m, int wexp) { return min(max(col_exp(m), -126 - wexp), 126 - wexp); }
+// the lower one binds only where the fp32 products themselves overflow.  The outer clamp keeps the
+// column's own scale 2^e a normal float too (pow2f exact) when the weights' exponent is far from 0.
+__device__ __forceinline__ int col_exp_w(float m, int wexp) {
+    return min(max(min(max(col_exp(m), -126 - wexp), 126 - wexp), -126), 127);
+}
 // acc += A B over one K = 16 step: A's two split images at img and img + img_stride
 __device__ __forceinline__ f32x16_t mfma3h(const _Float16 *img, const f16x8_t &b0, const f16x8_t &b1, f32x16_t acc,
                                            int img_stride) {
