@@ -250,10 +250,11 @@ class MessageGNNDecoder(nn.Module):
         """Whether the fp32 kernels' f16 splits hold every weight row to fp32 accuracy: each weight
         group shares one power-of-two scale, and a row keeps 22 bits while its largest |w| is >= 2^-17
         of its group's.  H = 64 (csrc/gnn.hip): the projection's W1v / W1c right halves; the MLP's
-        left halves, W2v, W2c and W1v_left + W1v_right.  H = 96..256 (csrc/gnn_wide.hip: one scale per
-        workgroup slice of output rows; checked per whole matrix, which is stricter): each side's W1
-        right and left halves, W2v | W2c.  Checked once per weight version; otherwise the forward
-        runs the products on the fp32 MFMA / as bf16x6 splits (LDPC_GNN_FP32_PRODUCTS)."""
+        left halves, W2v, W2c and W1v_left + W1v_right.  H = 96..256 (csrc/gnn_wide.hip): each side's
+        W1 right half (the projections: one scale per workgroup slice; checked per whole matrix, which
+        is stricter), both sides' W1 left halves together and W2v | W2c (the fused MLP's two scales).
+        Checked once per weight version; otherwise the forward runs the products on the fp32 MFMA /
+        as bf16x6 splits (LDPC_GNN_FP32_PRODUCTS)."""
         H = self.hidden_dim
         wide = H != 64 and H % 32 == 0 and 96 <= H <= 256
         if H != 64 and not wide:
@@ -264,7 +265,7 @@ class MessageGNNDecoder(nn.Module):
                 w1v, w1c = v[0].weight.detach().float(), c[0].weight.detach().float()
                 w2v, w2c = v[2].weight.detach().float(), c[2].weight.detach().float()
                 if wide:
-                    groups = ((w1v[:, H:],), (w1c[:, H:],), (w1v[:, :H],), (w1c[:, :H],),
+                    groups = ((w1v[:, H:],), (w1c[:, H:],), (w1v[:, :H], w1c[:, :H]),
                               (torch.cat([w2v, w2c], dim=1),))
                 else:
                     groups = ((w1v[:, H:], w1c[:, H:]), (w1v[:, :H], w1c[:, :H], w2v, w2c, w1v[:, :H] + w1v[:, H:]))

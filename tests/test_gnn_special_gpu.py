@@ -208,3 +208,38 @@ def test_wide_split_fp32_accurate(cuda, oracle_mod, weights, hidden):
     print(f"H={hidden} {weights}: native {err:.3e}  oracle-f32 {ref_err:.3e}  (unsaturated {unsure:.3f})")
     assert unsure > 0.01
     assert err <= 2 * ref_err + 1e-7, (err, ref_err)
+
+
+@pytest.mark.parametrize("hidden", [96, 128, 192])
+def test_wide_fused_hidden_slice_scales(cuda, oracle_mod, hidden):
+    """The fused wide MLP (csrc/gnn_wide.hip gnn_wide_mlp_kernel) splits relu(h) per row and hidden
+    slice of 32 units under a running exponent that only moves down, rescaling y's accumulators when
+    a later slice holds larger values.  Rows of W1 (and b1) scaled by 2^U(-6, 6), the matching
+    columns of W2 by the inverse (the same function): the slices' maxima then differ by up to 2^12
+    inside the splits' range (the fused path runs), and the result stays fp32-accurate -- within 2x
+    the fp32 oracle's own error against float64, + 1e-7."""
+    base, H, dec, conv, types = _model(32, 4, cuda, seed=50 + hidden)
+    from ldpc_neural_decoder.models import create_message_gnn_decoder as _c
+    torch.manual_seed(50 + hidden)
+    dec, conv = _c(H, num_iterations=4, hidden_dim=hidden, base_graph=base, Z=32)
+    g = torch.Generator().manual_seed(hidden)
+    with torch.no_grad():
+        for p in dec.parameters():
+            p.mul_(0.5)
+        for layer in dec.gnn_layers:
+            for seq in (layer.var_to_check_update, layer.check_to_var_update):
+                r = 2.0 ** torch.floor(torch.rand(seq[0].weight.shape[0], generator=g) * 12 - 6)
+                seq[0].weight.mul_(r.view(-1, 1))
+                seq[0].bias.mul_(r)
+                seq[2].weight.div_(r.view(1, -1))
+    dec = dec.to(cuda)
+    llr = awgn_llr(24, H.shape[1], 1.0, seed=500 + hidden, device=cuda)
+    exact = _oracle(oracle_mod, dec, conv, H, types, llr, dtype=torch.float64)
+    f32 = _oracle(oracle_mod, dec, conv, H, types, llr)
+    got = _native(dec, conv, types, llr, cuda).cpu().numpy()
+    assert dec._split_ok  # inside the splits' range: the fused MLP ran
+    err, ref_err = float(np.abs(got - exact).max()), float(np.abs(f32 - exact).max())
+    unsure = float((np.abs(exact - 0.5) < 0.49).mean())
+    print(f"H={hidden}: native {err:.3e}  oracle-f32 {ref_err:.3e}  (unsaturated {unsure:.3f})")
+    assert unsure > 0.01
+    assert err <= 2 * ref_err + 1e-7, (err, ref_err)
