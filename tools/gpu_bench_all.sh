@@ -14,6 +14,7 @@ run gnn-z4 --workload gnn-z4 --steps 10 --warmup 3 --cpu-baseline-seconds 10
 run gnn-z4-bf16 --workload gnn-z4-bf16 --steps 10 --warmup 3 --cpu-baseline-seconds 0
 run gnn-z32 --workload gnn-z32 --steps 3 --warmup 1 --cpu-baseline-seconds 10
 run gnn-z32-h128 --workload gnn-z32-h128 --steps 3 --warmup 1 --cpu-baseline-seconds 10
+run gnn-z32-h192 --workload gnn-z32-h192 --steps 2 --warmup 1 --cpu-baseline-seconds 0
 run gnn-z32-codewords --workload gnn-z32 --data codewords --steps 3 --warmup 1 --cpu-baseline-seconds 0
 run gnn-z32-bf16 --workload gnn-z32-bf16 --steps 3 --warmup 1 --cpu-baseline-seconds 10
 run gnn-z32-bf16-codewords --workload gnn-z32-bf16 --data codewords --steps 3 --warmup 1 --cpu-baseline-seconds 0
