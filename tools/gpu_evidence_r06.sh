@@ -26,18 +26,18 @@ PY
   python3 tools/pmc_kernels.py gpurun_out/prof_${T}_${W} > $O/prof_${W}/pmc_per_kernel.txt || true
 }
 if [ "${1:-profile}" = profile ]; then
-  bash tools/gpu_profile.sh minsum-z32 $T > $O/prof_minsum-z32.log 2>&1 || exit 1
-  summ minsum-z32 flood_fixed - 65536 436207616 "" || exit 1
-  bash tools/gpu_profile.sh gnn-z4 $T > $O/prof_gnn-z4.log 2>&1 || exit 1
-  summ gnn-z4 "gnn_|csr_" csr_count_kernel 4096 - "per call = one 5-layer fp32 GNN forward on B=4096 Z=4 frames (cfg2); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
-  bash tools/gpu_profile.sh gnn-z32 $T > $O/prof_gnn-z32.log 2>&1 || exit 1
-  summ gnn-z32 "gnn_|csr_" csr_count_kernel 10922.666666666666 - "per call = one fp32 GNN forward call on one workspace chunk (bench's B=32768 runs as 3 chunks of ~10923 frames); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
-  bash tools/gpu_profile.sh gnn-z32-h128 $T > $O/prof_gnn-z32-h128.log 2>&1 || exit 1
-  summ gnn-z32-h128 "gnn_|csr_" csr_count_kernel 2730.6666666666665 - "per call = one H=128 fp32 GNN forward call on one workspace chunk (B=8192 runs as 3 chunks); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1
-  bash tools/gpu_profile.sh gnn-z32-bf16-i10 $T > $O/prof_gnn-z32-bf16-i10.log 2>&1 || exit 1
-  summ gnn-z32-bf16-i10 "gnn_|csr_" gnn_bf16_info_kernel 16384 - "per call = one 10-layer bf16 GNN forward on one 16384-frame chunk (B=32768 runs as 2 chunks); every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1
-  bash tools/gpu_profile.sh gnn-z32-bf16 $T > $O/prof_gnn-z32-bf16.log 2>&1 || exit 1
-  summ gnn-z32-bf16 "gnn_|csr_" gnn_bf16_info_kernel 16384 - "per call = one 15-layer bf16 GNN forward with per-frame early termination on one 16384-frame chunk (B=32768 runs as 2 chunks), random codewords at 2 dB; every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1
+  # WL: the workloads to profile (default: all six)
+  for w in ${WL:-minsum-z32 gnn-z4 gnn-z32 gnn-z32-h128 gnn-z32-bf16-i10 gnn-z32-bf16}; do
+    bash tools/gpu_profile.sh $w $T > $O/prof_$w.log 2>&1 || exit 1
+    case $w in
+      minsum-z32) summ minsum-z32 flood_fixed - 65536 436207616 "" || exit 1 ;;
+      gnn-z4) summ gnn-z4 "gnn_|csr_" csr_count_kernel 4096 - "per call = one 5-layer fp32 GNN forward on B=4096 Z=4 frames (cfg2); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1 ;;
+      gnn-z32) summ gnn-z32 "gnn_|csr_" csr_count_kernel 10922.666666666666 - "per call = one fp32 GNN forward call on one workspace chunk (bench's B=32768 runs as 3 chunks of ~10923 frames); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1 ;;
+      gnn-z32-h128) summ gnn-z32-h128 "gnn_|csr_" csr_count_kernel 2730.6666666666665 - "per call = one H=128 fp32 GNN forward call on one workspace chunk (B=8192 runs as 3 chunks); every gnn_*/csr_* kernel of the call summed, divided by the csr_count_kernel launches (one per call)" || exit 1 ;;
+      gnn-z32-bf16-i10) summ gnn-z32-bf16-i10 "gnn_|csr_" gnn_bf16_info_kernel 16384 - "per call = one 10-layer bf16 GNN forward on one 16384-frame chunk (B=32768 runs as 2 chunks); every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1 ;;
+      gnn-z32-bf16) summ gnn-z32-bf16 "gnn_|csr_" gnn_bf16_info_kernel 16384 - "per call = one 15-layer bf16 GNN forward with per-frame early termination on one 16384-frame chunk (B=32768 runs as 2 chunks), random codewords at 2 dB; every gnn_*/csr_* kernel of the call summed, divided by the gnn_bf16_info_kernel launches (one per call)" || exit 1 ;;
+    esac
+  done
   echo "profiles ok"
 else
   bash tools/gpu_bench_all.sh || exit $?
