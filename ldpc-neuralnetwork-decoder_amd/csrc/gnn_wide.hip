@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void gnn_wide_head_kernel(const float *__restr
 // contribution W2_s[:, slice] relu(h) to every output unit of y (GEMM2 over the slice's 32 columns).
 // The 2 H / 32 slices' split weight images (W1 rows of the slice, W2 columns of the slice; 38 KB at
 // H = 128) stream from a per-forward global copy (gnn_wide_prep_kernel) through a two-slot LDS ring
-// shared by the workgroup's eight waves, one barrier per slice; each wave owns one tile per pass.
+// shared by the workgroup's waves, one barrier per slice; each wave owns one tile per pass.
 // Scales: the tile's c per row from its exact largest |c|; relu(h) per row and slice from the slice's
 // largest value, under a running exponent that only moves down (a larger slice maximum lowers it and
 // rescales y's accumulators by the exact power of two), so every slice's split is at least as fine
