@@ -336,49 +336,76 @@ struct WGm {
     int64_t E, B;
 };
 
+// V float4 per lane (V = 2: half the lanes per group, twice the groups per wave -- most groups are
+// of degree 1, so a wave's life is mostly its dispatch and its first load; V = 2 measured +4.3 % on
+// gnn-z32-h128 against V = 1, profiles/r06/wgm_v/)
+template <int V>
 __global__ __launch_bounds__(256) void gnn_wide_gm_kernel(WGm A) {
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, lg = A.H / 4;
+    const int lane = threadIdx.x & 63, lg = A.H / (4 * V);
     const int wpt = 8 / A.gpw;  // waves per tile
     const int64_t tile_w = w / wpt;
     if (tile_w >= A.B * A.n_tiles) return;
     const int64_t b = tile_w / A.n_tiles;
     const int t = (int)(tile_w - b * A.n_tiles);
-    const int q = (int)(w - tile_w * wpt) * A.gpw + lane / lg, u = 4 * (lane % lg);
+    const int q = (int)(w - tile_w * wpt) * A.gpw + lane / lg, u = 4 * V * (lane % lg);
     if (lane / lg >= A.gpw) return;
     const int2 md = A.meta[t];
     const int g = A.grp[8 * t + q];
     if (g < 0) return;
     const int32_t *mem = A.mem + md.y + q;
-    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    auto feat = [&](int mm) {
-        if (A.x) return *reinterpret_cast<const float4 *>(A.x + (b * A.E + mm) * A.H + u);
+    float4 s[V];
+#pragma unroll
+    for (int c = 0; c < V; ++c) s[c] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    auto feat = [&](int mm, int c) {
+        if (A.x) return *reinterpret_cast<const float4 *>(A.x + (b * A.E + mm) * A.H + u + 4 * c);
         const float l = A.llr[b * A.N + A.msg_var[mm]];
-        const float4 wi = *reinterpret_cast<const float4 *>(A.w_in + u), bi = *reinterpret_cast<const float4 *>(A.b_in + u);
+        const float4 wi = *reinterpret_cast<const float4 *>(A.w_in + u + 4 * c), bi = *reinterpret_cast<const float4 *>(A.b_in + u + 4 * c);
         return make_float4(l * wi.x + bi.x, l * wi.y + bi.y, l * wi.z + bi.z, l * wi.w + bi.w);
     };
-    auto add = [&](float4 v, int mm) {
-        const float4 e = *reinterpret_cast<const float4 *>(A.emb + (int64_t)A.msg_type[mm] * A.H + u);
-        s.x += v.x + e.x; s.y += v.y + e.y; s.z += v.z + e.z; s.w += v.w + e.w;
+    auto add = [&](float4 v, int mm, int c) {
+        const float4 e = *reinterpret_cast<const float4 *>(A.emb + (int64_t)A.msg_type[mm] * A.H + u + 4 * c);
+        s[c].x += v.x + e.x; s[c].y += v.y + e.y; s[c].z += v.z + e.z; s[c].w += v.w + e.w;
     };
     int i = 0;
     for (; i + 4 <= md.x; i += 4) {  // four members' rows in flight, summed in ascending order
         const int m0 = mem[8 * i], m1 = mem[8 * i + 8], m2 = mem[8 * i + 16], m3 = mem[8 * i + 24];
-        const float4 v0 = feat(m0), v1 = feat(m1), v2 = feat(m2), v3 = feat(m3);
-        add(v0, m0);
-        add(v1, m1);
-        add(v2, m2);
-        add(v3, m3);
+        float4 v0[V], v1[V], v2[V], v3[V];
+#pragma unroll
+        for (int c = 0; c < V; ++c) {
+            v0[c] = feat(m0, c);
+            v1[c] = feat(m1, c);
+            v2[c] = feat(m2, c);
+            v3[c] = feat(m3, c);
+        }
+#pragma unroll
+        for (int c = 0; c < V; ++c) {
+            add(v0[c], m0, c);
+            add(v1[c], m1, c);
+            add(v2[c], m2, c);
+            add(v3[c], m3, c);
+        }
     }
-    for (; i < md.x; ++i) add(feat(mem[8 * i]), mem[8 * i]);
+    for (; i < md.x; ++i) {
+        const int mm = mem[8 * i];
+        float4 v[V];
+#pragma unroll
+        for (int c = 0; c < V; ++c) v[c] = feat(mm, c);
+#pragma unroll
+        for (int c = 0; c < V; ++c) add(v[c], mm, c);
+    }
     const bool isv = g < A.Gv;
     const int gg = isv ? g : g - A.Gv;
     const float inv = isv ? A.inv_v[gg] : A.inv_c[gg];
     float *dst = isv ? A.Mv + (b * A.Gv + gg) * A.H : A.Mc + (b * A.Gc + gg) * A.H;
-    const float4 mean = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
-    *reinterpret_cast<float4 *>(dst + u) = mean;
+    float m = 0.0f;
+#pragma unroll
+    for (int c = 0; c < V; ++c) {
+        const float4 mean = make_float4(s[c].x * inv, s[c].y * inv, s[c].z * inv, s[c].w * inv);
+        *reinterpret_cast<float4 *>(dst + u + 4 * c) = mean;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(mean.x), fabsf(mean.y)), fmaxf(fabsf(mean.z), fabsf(mean.w))));
+    }
     if (A.gmax_v) {  // the row's largest |value| over its lg lanes (a segmented max; no lane leaves it)
-        float m = fmaxf(fmaxf(fabsf(mean.x), fabsf(mean.y)), fmaxf(fabsf(mean.z), fabsf(mean.w)));
         const int seg0 = (lane / lg) * lg;
         for (int off = 1; off < lg; off <<= 1) {
             const float o = __shfl_down(m, off, 64);
@@ -793,6 +820,19 @@ int launch_wide_mlp(const WMlp &a, hipStream_t s) {
     return LDPC_OK;
 }
 
+// LDPC_GNN_WIDE_GM_V=1 / 2 / 4: float4 per lane in the group means (A/B); default LDPC_WIDE_GM_V
+#ifndef LDPC_WIDE_GM_V
+#define LDPC_WIDE_GM_V 2
+#endif
+int gm_v() {
+    static const int v = [] {
+        const char *e = std::getenv("LDPC_GNN_WIDE_GM_V");
+        const int x = e ? std::atoi(e) : LDPC_WIDE_GM_V;
+        return x == 1 || x == 4 ? x : 2;
+    }();
+    return v;
+}
+
 }  // namespace
 
 bool gnn_wide_supported(int H) { return H != 64 && H % 32 == 0 && H >= 96 && H <= 256; }
@@ -864,10 +904,20 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         g.gmax_v = L.f16 ? L.gmax_v : nullptr;
         g.gmax_c = L.f16 ? L.gmax_c : nullptr;
         g.Gv = L.plan->Gv; g.Gc = L.plan->Gc; g.H = H; g.N = L.N;
-        g.gpw = std::max(1, 64 / (H / 4));
+        // groups per wave: a power of two dividing a tile's 8 that fits the wave's 64 lanes
+        const int v2 = gm_v();
+        const int lg = H / (4 * v2);
+        g.gpw = 1;
+        while (g.gpw * 2 <= 8 && g.gpw * 2 * lg <= 64) g.gpw *= 2;
         g.E = L.E; g.B = L.B;
         const int64_t waves = L.B * (int64_t)g.n_tiles * (8 / g.gpw);
-        hipLaunchKernelGGL(gnn_wide_gm_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, g);
+        const dim3 grid((unsigned)((waves + 3) / 4));
+        if (v2 == 4)
+            hipLaunchKernelGGL(gnn_wide_gm_kernel<4>, grid, dim3(256), 0, s, g);
+        else if (v2 == 2)
+            hipLaunchKernelGGL(gnn_wide_gm_kernel<2>, grid, dim3(256), 0, s, g);
+        else
+            hipLaunchKernelGGL(gnn_wide_gm_kernel<1>, grid, dim3(256), 0, s, g);
         LDPC_CHECK_LAUNCH("gnn_wide_gm_kernel");
     }
     WArgs base{};
