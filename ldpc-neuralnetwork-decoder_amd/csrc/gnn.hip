@@ -1745,6 +1745,7 @@ struct Ws {
     float *Pv, *Pc, *hbuf;  // wide path: projected group rows (B, G, H), MLP hidden rows (B, E, 2 H)
     char *wimg;             // wide path, H = 96 / 128: every layer's fused-MLP slice images
     int *wexp;              // ... and their weight exponents (2 per layer)
+    float *wmemb;           // wide path: every layer's mean type embedding per group (L, Gv + Gc, H)
     uint32_t *xmax[2], *hmax, *gmax_v, *gmax_c;  // wide path: each row's largest |value| (f16 splits)
     float *S, *memb;  // row walk (H = 64, plan rw_*): per-check feature sums (B, Gc, H), mean type embeddings (L, Gc, H)
     float *memb_v;    // ... and per var group (L, Gv, H)
@@ -1798,7 +1799,9 @@ Ws carve(const ldpc_gnn_plan *p, int H, int N, int64_t B, int layers, int precis
     char *f = z + (wide ? 3 * rm + gmv + gmc : 0);
     w.wimg = fib ? f : nullptr;
     w.wexp = fib ? reinterpret_cast<int *>(f + fib) : nullptr;
-    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb + (wide ? mv + mc + hb + 3 * rm + gmv + gmc : 0) + fib + feb;
+    const int64_t wmb = wide ? al((int64_t)layers * (p->Gv + p->Gc) * H * 4) : 0;
+    w.wmemb = wmb ? reinterpret_cast<float *>(f + fib + feb) : nullptr;
+    w.bytes = xb + xb2 + mv + mc + vs + cs + wtb + rwb + mbb + (wide ? mv + mc + hb + 3 * rm + gmv + gmc : 0) + fib + feb + wmb;
     return w;
 }
 
@@ -2475,6 +2478,8 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
     const bool wfused = wide && !fp32_products && w.wimg && gnn_wide_fused_fits(H, types);
     if (wfused)
         if (int rc = gnn_wide_prep(H, layers, d_weights, layer_floats(H, types), types, w.wimg, w.wexp, s)) return rc;
+    if (wide && w.wmemb)
+        if (int rc = gnn_wide_memb(p, H, layers, d_weights + 2 * H, layer_floats(H, types), d_msg_type, w.wmemb, s)) return rc;
     // frames [b0, b0 + nb) through every layer on stream st (pointers offset to the range)
     const GnnLayer L0 = L;
     auto run_range = [&](int64_t b0, int64_t nb, hipStream_t st) -> int {
@@ -2527,6 +2532,7 @@ int ldpc::gnn_fp32_forward(const ldpc_gnn_plan *p, int hidden, int types, int la
             W.gmax_c = w.gmax_c + b0 * p->Gc;
             W.wimg = wfused ? w.wimg + (int64_t)l * (gnn_wide_fused_bytes(H, 1)) : nullptr;
             W.wexp = wfused ? w.wexp + 2 * l : nullptr;
+            W.memb = w.wmemb ? w.wmemb + (int64_t)l * (p->Gv + p->Gc) * H : nullptr;
             if (int rc = gnn_wide_layer(W, st)) return rc;
             x_in = W.y;
             continue;

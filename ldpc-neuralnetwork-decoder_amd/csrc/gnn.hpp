@@ -130,6 +130,8 @@ struct GnnWideLayer {
     // (gnn_wide_prep), or null for the row-GEMM sequence
     const char *wimg;
     const int *wexp;
+    // this layer's mean type embedding per group ((Gv + Gc), H; gnn_wide_memb), or null
+    const float *memb;
 };
 bool gnn_wide_supported(int H);
 int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s);
@@ -137,6 +139,9 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s);
 // kernel's LDS image holds T message types
 int64_t gnn_wide_fused_bytes(int H, int layers);
 bool gnn_wide_fused_fits(int H, int T);
+// every layer's mean type embedding per var / check group (the group-mean pass adds it once)
+int gnn_wide_memb(const ldpc_gnn_plan *p, int H, int layers, const float *emb0, int64_t layer_stride,
+                  const int32_t *msg_type, float *memb, hipStream_t s);
 int gnn_wide_prep(int H, int layers, const float *blob, int64_t layer_floats, int T, char *wimg, int *wexp, hipStream_t s);
 
 // The per-device side stream and the calling thread's fork/join events the forwards split their

@@ -332,9 +332,33 @@ struct WGm {
     const float *inv_v, *inv_c;
     float *Mv, *Mc;
     uint32_t *gmax_v, *gmax_c;  // F16: each row's largest |value| (bits), or null
+    // this layer's mean type embedding per group ((Gv + Gc), H; gnn_wide_memb_kernel), or null: the
+    // group mean is then mean(x) + memb[g] (the members' types are not read per frame)
+    const float *memb;
     int Gv, Gc, H, N, gpw;  // gpw: groups per wave
     int64_t E, B;
 };
+
+// every layer's mean type embedding per var / check group: memb[l][g][u] = mean over g's members of
+// emb_l[type][u] (ascending member order), g < Gv the var groups, then the check groups
+__global__ void gnn_wide_memb_kernel(const float *__restrict__ emb0, int64_t layer_stride, int H,
+                                     const int32_t *__restrict__ msg_type, const int32_t *__restrict__ vg_ptr,
+                                     const int32_t *__restrict__ vg_mem, const float *__restrict__ inv_v,
+                                     const int32_t *__restrict__ cg_ptr, const int32_t *__restrict__ cg_mem,
+                                     const float *__restrict__ inv_c, int Gv, int Gc, int layers,
+                                     float *__restrict__ memb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, G = Gv + Gc;
+    if (i >= (int64_t)layers * G * H) return;
+    const int64_t l = i / (G * H);
+    const int g = (int)(i / H - l * G), u = (int)(i % H);
+    const float *emb = emb0 + l * layer_stride;
+    const bool v = g < Gv;
+    const int gg = v ? g : g - Gv;
+    const int32_t *ptr = v ? vg_ptr : cg_ptr, *mem = v ? vg_mem : cg_mem;
+    float s = 0.0f;
+    for (int k = ptr[gg]; k < ptr[gg + 1]; ++k) s += emb[(int64_t)msg_type[mem[k]] * H + u];
+    memb[i] = s * (v ? inv_v : inv_c)[gg];
+}
 
 // V float4 per lane (V = 2: half the lanes per group, twice the groups per wave -- most groups are
 // of degree 1, so a wave's life is mostly its dispatch and its first load; V = 2 measured +4.3 % on
@@ -364,8 +388,12 @@ __global__ __launch_bounds__(256) void gnn_wide_gm_kernel(WGm A) {
         return make_float4(l * wi.x + bi.x, l * wi.y + bi.y, l * wi.z + bi.z, l * wi.w + bi.w);
     };
     auto add = [&](float4 v, int mm, int c) {
-        const float4 e = *reinterpret_cast<const float4 *>(A.emb + (int64_t)A.msg_type[mm] * A.H + u + 4 * c);
-        s[c].x += v.x + e.x; s[c].y += v.y + e.y; s[c].z += v.z + e.z; s[c].w += v.w + e.w;
+        if (A.memb) {  // (uniform) the type embeddings' mean is added once, below
+            s[c].x += v.x; s[c].y += v.y; s[c].z += v.z; s[c].w += v.w;
+        } else {
+            const float4 e = *reinterpret_cast<const float4 *>(A.emb + (int64_t)A.msg_type[mm] * A.H + u + 4 * c);
+            s[c].x += v.x + e.x; s[c].y += v.y + e.y; s[c].z += v.z + e.z; s[c].w += v.w + e.w;
+        }
     };
     int i = 0;
     for (; i + 4 <= md.x; i += 4) {  // four members' rows in flight, summed in ascending order
@@ -401,7 +429,11 @@ __global__ __launch_bounds__(256) void gnn_wide_gm_kernel(WGm A) {
     float m = 0.0f;
 #pragma unroll
     for (int c = 0; c < V; ++c) {
-        const float4 mean = make_float4(s[c].x * inv, s[c].y * inv, s[c].z * inv, s[c].w * inv);
+        float4 mean = make_float4(s[c].x * inv, s[c].y * inv, s[c].z * inv, s[c].w * inv);
+        if (A.memb) {
+            const float4 e = *reinterpret_cast<const float4 *>(A.memb + (int64_t)g * A.H + u + 4 * c);
+            mean = make_float4(mean.x + e.x, mean.y + e.y, mean.z + e.z, mean.w + e.w);
+        }
         *reinterpret_cast<float4 *>(dst + u + 4 * c) = mean;
         m = fmaxf(m, fmaxf(fmaxf(fabsf(mean.x), fabsf(mean.y)), fmaxf(fabsf(mean.z), fabsf(mean.w))));
     }
@@ -877,6 +909,15 @@ void go_prep(int layers, const float *blob, int64_t layer_floats, int T, char *w
     hipLaunchKernelGGL(gnn_wide_prep_kernel<H>, dim3(layers), dim3(1024), 0, s, blob, layer_floats, T, wimg, wexp);
 }
 
+int gnn_wide_memb(const ldpc_gnn_plan *p, int H, int layers, const float *emb0, int64_t layer_stride,
+                  const int32_t *msg_type, float *memb, hipStream_t s) {
+    const int64_t n = (int64_t)layers * (p->Gv + p->Gc) * H;
+    hipLaunchKernelGGL(gnn_wide_memb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, emb0, layer_stride, H,
+                       msg_type, p->vg_ptr, p->vg_mem, p->inv_v, p->cg_ptr, p->cg_mem, p->inv_c, p->Gv, p->Gc, layers, memb);
+    LDPC_CHECK_LAUNCH("gnn_wide_memb_kernel");
+    return LDPC_OK;
+}
+
 int gnn_wide_prep(int H, int layers, const float *blob, int64_t layer_floats, int T, char *wimg, int *wexp, hipStream_t s) {
     switch (H) {
         case 96: go_prep<96>(layers, blob, layer_floats, T, wimg, wexp, s); break;
@@ -903,6 +944,7 @@ int gnn_wide_layer(const GnnWideLayer &L, hipStream_t s) {
         g.Mv = L.Mv; g.Mc = L.Mc;
         g.gmax_v = L.f16 ? L.gmax_v : nullptr;
         g.gmax_c = L.f16 ? L.gmax_c : nullptr;
+        g.memb = L.memb;
         g.Gv = L.plan->Gv; g.Gc = L.plan->Gc; g.H = H; g.N = L.N;
         // groups per wave: a power of two dividing a tile's 8 that fits the wave's 64 lanes
         const int v2 = gm_v();
