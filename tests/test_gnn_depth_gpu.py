@@ -166,7 +166,8 @@ def test_split_mlp_is_fp32_accurate(cuda, oracle_mod, monkeypatch):
 @pytest.mark.parametrize("hidden,layers", [(128, 10), (96, 6), (192, 4), (256, 3)])
 def test_wide_hidden_mfma_vs_oracle(cuda, oracle_mod, hidden, layers):
     """hidden_dim = 32 k other than 64 (message_gnn_decoder.py:22, :162 take any width) on the MFMA
-    row GEMMs of gnn_wide.hip (bf16x6 splits: fp32 products): BG2 Z=32 against the oracle at the
+    kernels of gnn_wide.hip (scaled f16 two-term splits: fp32-accurate products; H = 96 / 128 / 192
+    through the fused per-tile MLP, 256 through the row GEMMs): BG2 Z=32 against the oracle at the
     H = 64 bar (|dprobs| <= 2e-5), H = 128 at cfg4's 10 layers; a sub-batch decodes bit-identically
     to its rows of the full batch (a frame's output depends on that frame alone)."""
     base, H, dec, conv, types = _model(layers, cuda, seed=hidden, hidden=hidden)
@@ -181,12 +182,35 @@ def test_wide_hidden_mfma_vs_oracle(cuda, oracle_mod, hidden, layers):
 
 @pytest.mark.parametrize("hidden", [96, 160, 224])
 def test_wide_hidden_multi_tile_walk(cuda, oracle_mod, hidden):
-    """H = 96 / 160 / 224: the projection's and GEMM1's reduction (K = H) has a k-step count that 4
-    does not divide, so gnn_wgemm_kernel's input ring runs 2 deep there (a 4-deep ring
-    fed the next tile permuted chunks).  B = 48 frames at Z=32 give every wave several tiles to walk;
-    the oracle checks every frame at the H = 64 bar."""
+    """H = 96 / 160 / 224: the projection's reduction (K = H; and GEMM1's at 224, where the row GEMMs
+    run) has a k-step count that 4 does not divide, so gnn_wgemm_kernel's input ring runs 2 deep there
+    (a 4-deep ring fed the next tile permuted chunks).  B = 48 frames at Z=32 give every
+    wave several tiles to walk (and the fused MLP several passes at 96 / 160); the oracle checks
+    every frame at the H = 64 bar."""
     base, H, dec, conv, types = _model(2, cuda, seed=hidden + 1, hidden=hidden)
     llr = awgn_llr(48, H.shape[1], 1.0, seed=hidden + 2, device=cuda)
+    got = _native(dec, conv, types, llr, cuda).cpu().numpy()
+    ref = _oracle(oracle_mod, dec, conv, H, types, llr)
+    err = float(np.abs(got - ref).max())
+    assert err <= TOL, err
+
+
+@pytest.mark.parametrize("hidden,z,batch", [(128, 32, 1), (192, 32, 2), (96, 4, 1), (128, 4, 3)])
+def test_wide_fused_tiny_batches(cuda, oracle_mod, hidden, z, batch):
+    """The fused wide MLP (gnn_wide_mlp_kernel) on batches far smaller than its grid: most XCD tile
+    ranges hold less than one pass, so workgroups run passes whose waves own no tile (they still
+    take every slice's barrier and copy share) and Z = 4 leaves whole workgroups without a tile.
+    Every frame against the oracle at the H = 64 bar."""
+    torch.manual_seed(hidden + z)
+    base = load_base_matrix(code_path(z))
+    H = expand_base_matrix(base, z)
+    dec, conv = create_message_gnn_decoder(H, num_iterations=3, hidden_dim=hidden, base_graph=base, Z=z)
+    with torch.no_grad():
+        for p in dec.parameters():
+            p.mul_(0.5)
+    dec = dec.to(cuda)
+    types = conv.get_message_types(base, z)
+    llr = awgn_llr(batch, H.shape[1], 1.0, seed=hidden + batch, device=cuda)
     got = _native(dec, conv, types, llr, cuda).cpu().numpy()
     ref = _oracle(oracle_mod, dec, conv, H, types, llr)
     err = float(np.abs(got - ref).max())
